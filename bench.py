@@ -1,0 +1,237 @@
+"""bench.py — hyperspace attribute hashing throughput on MI355X.
+
+Metric (BASELINE.json): hashed GiB/s (device-resident) + Mobjects/s on
+16-attr x 64 B batches.  Workload at N=1: config 3a of SURVEY §8d —
+10M objects, key STRING 64 B + 16 STRING x 64 B (17 coordinates/object),
+synthetic bytes generated in HBM.  A step = one launch hashing the whole
+batch (every attribute of every object -> coords[n, 17]).
+
+Multi-GPU (torchrun, one rank per GPU): each rank owns its own 10M-object
+shard (weak scaling, no collective in the timed region); the RCCL all-gather
+of the coordinates is timed separately and reported as `allgather`.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+ALGO_EXTRA_PER_ATTR = 4 + 8  # u32 length read + u64 coordinate write
+HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cfg3a")
+    ap.add_argument("--objects", type=int, default=10_000_000, help="objects per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--host-path", action="store_true",
+                    help="also time the host-resident (PCIe-inclusive) path")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    cfg, n = args.config, args.objects
+    types, blob, base, lens = synth.make_batch_device(cfg, n, first=rank * n, device=dev)
+    A = len(types)
+    payload = int(blob.numel())
+    coords = torch.empty((n, A), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    log("rank %d: %s n=%d A=%d payload %.2f GB" % (rank, cfg, n, A, payload / 1e9))
+
+    stream = torch.cuda.current_stream(dev)
+    for _ in range(args.warmup):
+        hdx.hash_batch(types, blob, base, lens, coords=coords, stream=stream)
+    torch.cuda.synchronize()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record(stream)
+        hdx.hash_batch(types, blob, base, lens, coords=coords, stream=stream)
+        e.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    if world > 1:
+        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kernel_ms = float(t[0]), float(t[1])
+
+    ms_per_step = elapsed / args.steps * 1e3
+    total_payload = payload * world
+    total_objs = n * world
+    gib_s = total_payload / (ms_per_step / 1e3) / 2**30
+    mobj_s = total_objs / (ms_per_step / 1e3) / 1e6
+    algo_bytes = payload + n * A * ALGO_EXTRA_PER_ATTR  # per launch, this rank
+    achieved = algo_bytes / (kernel_ms / 1e3) / 1e9
+
+    result = {
+        "metric": "hashed GiB/s (device-resident) + Mobjects/s, 16-attr×64B batches",
+        "value": round(gib_s, 3),
+        "unit": "GiB/s",
+        "mobjects_per_s": round(mobj_s, 2),
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 seed 0x4859504552444558, generated in HBM)",
+        "config": {"workload": {"cfg3a": "config 3a", "cfg3b": "config 3b", "cfg2": "config 2",
+                                "cfg1": "config 1"}.get(cfg, cfg) +
+                   ": %dM objects/GPU, key + %d attrs" % (n // 1_000_000, A - 1),
+                   "objects_per_gpu": n, "attrs": A, "payload_bytes_per_gpu": payload,
+                   "parallelism": "shard%d" % world},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                     "traffic": None, "kernel_ms": round(kernel_ms, 4),
+                     "algorithmic_bytes_per_launch": algo_bytes},
+    }
+
+    if world > 1 and not args.no_allgather:
+        result["allgather"] = time_allgather(coords, world, dev)
+
+    if args.host_path and rank == 0:
+        result["host_path"] = time_host_path(types, blob, base, lens, A)
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(types, blob, base, lens, A, args.cpu_seconds,
+                                              coords)
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def time_allgather(coords, world, dev, reps=5):
+    import torch
+    import torch.distributed as dist
+    out = torch.empty((world * coords.shape[0], coords.shape[1]), dtype=coords.dtype, device=dev)
+    dist.all_gather_into_tensor(out, coords)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        dist.all_gather_into_tensor(out, coords)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t[0])
+    nbytes = out.numel() * 8
+    return {"ms": round(dt * 1e3, 3), "bytes": nbytes,
+            "busbw_GBps": round(nbytes * (world - 1) / world / dt / 1e9, 2)}
+
+
+def time_host_path(types, blob, base, lens, A, n_host=2_000_000):
+    """PCIe-inclusive rate: pinned host batch -> hdx_hash_batch_host -> pinned coords."""
+    import ctypes
+
+    import hyperdex_amd as hdx
+    lib = hdx.lib()
+    n = min(n_host, base.numel())
+    nb = int((base[n - 1] + lens.view(-1, A)[n - 1].to(dtype=base.dtype).sum()).item()) if n else 0
+    ptrs = {}
+    for name, nbytes in (("blob", nb), ("base", n * 8), ("lens", n * A * 4), ("out", n * A * 8)):
+        p = ctypes.c_void_p()
+        hdx._lib.check(lib.hdx_alloc_pinned(nbytes, ctypes.byref(p)))
+        ptrs[name] = p.value
+    for name, src in (("blob", blob[:nb]), ("base", base[:n]), ("lens", lens[:n * A])):
+        ctypes.memmove(ptrs[name], src.cpu().numpy().ctypes.data, src.numel() * src.element_size())
+    t = np.array(types, np.uint32)
+    hdx._lib.check(lib.hdx_hash_batch_host(t.ctypes.data, A, ptrs["blob"], nb, ptrs["base"],
+                                           ptrs["lens"], n, ptrs["out"]))
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        hdx._lib.check(lib.hdx_hash_batch_host(t.ctypes.data, A, ptrs["blob"], nb, ptrs["base"],
+                                               ptrs["lens"], n, ptrs["out"]))
+    dt = (time.perf_counter() - t0) / reps
+    for p in ptrs.values():
+        lib.hdx_free_pinned(p)
+    return {"objects": n, "ms": round(dt * 1e3, 3), "GiB_s": round(nb / dt / 2**30, 3),
+            "mobjects_per_s": round(n / dt / 1e6, 2)}
+
+
+def cpu_baseline(types, blob, base, lens, A, seconds, coords):
+    """The oracle (C restatement of common/hash.cc, -O2) on this host's cores,
+    on a bounded sample of the same batch.  Also verifies the sample's GPU
+    coordinates against it (a failed check aborts the bench)."""
+    from oracle import oracle
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
+    ns = min(200_000, base.numel())
+    nb = int((base[ns - 1] + lens.view(-1, A)[ns - 1].to(dtype=base.dtype).sum()).item())
+    hb = blob[:nb].cpu().numpy()
+    ho = base[:ns].cpu().numpy().view(np.uint64)
+    hl = lens[:ns * A].cpu().numpy().view(np.uint32)
+    want, err = oracle.hash_batch(types, hb, ho, hl, nthreads=threads)
+    got = coords[:ns].cpu().numpy().view(np.uint64)
+    if err or not np.array_equal(got, want):
+        raise SystemExit("cpu_baseline: GPU coordinates differ from the oracle")
+
+    def rate(nthreads, budget):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            oracle.hash_batch(types, hb, ho, hl, nthreads=nthreads)
+            reps += 1
+            dt = time.perf_counter() - t0
+            if dt >= budget:
+                return reps * nb / dt, reps * ns / dt, reps
+
+    multi_b, multi_o, reps = rate(threads, seconds)
+    one_b, one_o, _ = rate(1, max(2.0, seconds / 5))
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": round(multi_b / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "mobjects_per_s": round(multi_o / 1e6, 3),
+            "single_thread_GiB_s": round(one_b / 2**30, 3),
+            "sample": "%d objects (%.0f MB) of the same batch, %d passes, oracle/hdx_oracle.c -O2 "
+                      "pthreads; verified equal to the GPU coords" % (ns, nb / 1e6, reps),
+            "cpu_model": model}
+
+
+if __name__ == "__main__":
+    main()

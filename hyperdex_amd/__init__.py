@@ -1,0 +1,16 @@
+"""hyperdex_amd — MI355X-native hyperspace attribute hashing.
+
+Drop-in for HyperDex's per-object attribute hashing (common/hash.{h,cc},
+cityhash/city.cc, common/ordered_encoding.cc, common/datatype_*.cc::hash):
+the hash runs as hand-written gfx950 HIP kernels in libhdxhash.so behind the
+C-ABI of include/hdxhash.h.  This package is the Python host side; the C++
+host side is include/hyperdex_amd/hash.h.
+"""
+from ._lib import HdxError, lib  # noqa: F401
+from .datatypes import *  # noqa: F401,F403
+from .datatypes import Attribute, Schema  # noqa: F401
+from .hashing import (hash, hash_batch, hash_batch_host, hash_key, hash_object,  # noqa: F401
+                      hashable, schema_check)
+
+__all__ = ["HdxError", "Attribute", "Schema", "hash", "hash_key", "hash_object", "hash_batch",
+           "hash_batch_host", "hashable", "schema_check", "lib"]

@@ -1,0 +1,496 @@
+// hdx_capi.cpp — C-ABI of libhdxhash.so (include/hdxhash.h).
+//
+// Host side of the engine: argument validation, the hyperdatatype -> dispatch
+// code table, per-thread streams, the pipelined host-resident batch path and
+// the per-object entry points that mirror common/hash.h.  Every compute entry
+// point runs the gfx950 kernels; there is no CPU hashing code in this library.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "hdx_internal.h"
+
+#define HDX_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace hdx {
+
+// ---- errors -------------------------------------------------------------
+
+static thread_local std::string t_err;
+
+static hdx_status fail(hdx_status s, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+static hdx_status fail(hdx_status s, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    t_err = buf;
+    return s;
+}
+
+static hdx_status hip_fail(hipError_t e, const char* what) {
+    return fail(HDX_E_DEVICE, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                  \
+    do {                                               \
+        hipError_t e_ = (expr);                        \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+    } while (0)
+
+// ---- types (include/hyperdex.h:53-102; datatype_info.cc:72-141) ----------
+
+int type_code(uint32_t t) {
+    switch (t) {
+        case 9217: return CODE_STRING;
+        case 9218: return CODE_INT64;
+        case 9219: return CODE_FLOAT;
+        case 9473: case 9474: case 9475: case 9476: case 9477: case 9478:
+            return CODE_TS_SECOND + (int)(t - 9473);
+        // lookup() returns a datatype whose hashable() is false (hash.cc:40-43)
+        case 9223:                                   // document
+        case 9281: case 9282: case 9283:             // list string/int64/float
+        case 9345: case 9346: case 9347:             // set string/int64/float
+        case 9417: case 9418: case 9419:             // map string->*
+        case 9425: case 9426: case 9427:             // map int64->*
+        case 9433: case 9434: case 9435:             // map float->*
+        case 9664:                                   // macaroon secret
+            return CODE_ZERO;
+        default:  // generic, *_GENERIC, *_KEYONLY, garbage, anything else: lookup() == NULL
+            return -1;
+    }
+}
+
+static hdx_status check_schema(const uint32_t* types, uint32_t A, uint8_t* codes_out) {
+    if (!types) return fail(HDX_E_INVALID, "types is NULL");
+    if (A == 0 || A > HDX_MAX_ATTRS)
+        return fail(HDX_E_INVALID, "attrs_sz=%u outside [1, %d]", A, HDX_MAX_ATTRS);
+    for (uint32_t j = 0; j < A; ++j) {
+        const int c = type_code(types[j]);
+        if (c < 0) return fail(HDX_E_BADTYPE, "attribute %u: unknown hyperdatatype %u", j, types[j]);
+        if (codes_out) codes_out[j] = (uint8_t)c;
+    }
+    return HDX_OK;
+}
+
+// ---- device binding -------------------------------------------------------
+
+static std::once_flag g_probe_once;
+static int g_ndev = -1;
+static std::vector<int> g_is_gfx950;
+
+static void probe() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        n = 0;
+    }
+    g_ndev = n;
+    g_is_gfx950.assign(n, 0);
+    for (int d = 0; d < n; ++d) {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, d) == hipSuccess)
+            g_is_gfx950[d] = std::strncmp(p.gcnArchName, "gfx950", 6) == 0;
+    }
+}
+
+struct ThreadState {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    // host-path pipeline: two slots, each with device + pinned staging
+    struct Slot {
+        hipStream_t s = nullptr;
+        uint8_t* d_blob = nullptr; size_t cap_blob = 0;
+        uint64_t* d_base = nullptr; uint32_t* d_len = nullptr; uint64_t* d_coords = nullptr;
+        size_t cap_obj = 0, cap_attr = 0, cap_coords = 0;
+        uint64_t* h_base = nullptr; size_t cap_hbase = 0;
+        uint8_t* h_blob = nullptr; size_t cap_hblob = 0;    // only for pageable inputs
+        uint64_t* h_coords = nullptr; size_t cap_hcoords = 0;
+        uint32_t* h_len = nullptr; size_t cap_hlen = 0;
+    } slot[2];
+    uint32_t* d_status = nullptr;
+    ~ThreadState() {
+        if (device < 0) return;
+        (void)hipSetDevice(device);
+        for (auto& s : slot) {
+            if (s.s) (void)hipStreamSynchronize(s.s);
+            (void)hipFree(s.d_blob); (void)hipFree(s.d_base); (void)hipFree(s.d_len);
+            (void)hipFree(s.d_coords);
+            (void)hipHostFree(s.h_base); (void)hipHostFree(s.h_blob);
+            (void)hipHostFree(s.h_coords); (void)hipHostFree(s.h_len);
+            if (s.s) (void)hipStreamDestroy(s.s);
+        }
+        (void)hipFree(d_status);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+static thread_local ThreadState t_state;
+
+static hdx_status bind_device(int want /* -1: current */) {
+    std::call_once(g_probe_once, probe);
+    if (g_ndev <= 0) return fail(HDX_E_DEVICE, "no HIP device visible (this library has no CPU path)");
+    int dev = want;
+    if (dev < 0) {
+        if (t_state.device >= 0) return HDX_OK;
+        HIP_TRY(hipGetDevice(&dev));
+    }
+    if (dev >= g_ndev) return fail(HDX_E_INVALID, "device %d >= device count %d", dev, g_ndev);
+    if (!g_is_gfx950[dev]) return fail(HDX_E_DEVICE, "device %d is not gfx950 (MI355X)", dev);
+    HIP_TRY(hipSetDevice(dev));
+    if (t_state.device != dev) {
+        if (t_state.device >= 0)
+            return fail(HDX_E_INVALID, "thread already bound to device %d", t_state.device);
+        t_state.device = dev;
+    }
+    return HDX_OK;
+}
+
+static hdx_status thread_stream(hipStream_t* out) {
+    hdx_status st = bind_device(-1);
+    if (st != HDX_OK) return st;
+    if (!t_state.stream) HIP_TRY(hipStreamCreateWithFlags(&t_state.stream, hipStreamNonBlocking));
+    *out = t_state.stream;
+    return HDX_OK;
+}
+
+template <typename T>
+static hdx_status grow_dev(T** p, size_t* cap, size_t need) {
+    if (need <= *cap) return HDX_OK;
+    size_t n = std::max(need, *cap * 3 / 2);
+    (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc((void**)p, n * sizeof(T)) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(HDX_E_NOMEM, "hipMalloc(%zu) failed", n * sizeof(T));
+    }
+    *cap = n;
+    return HDX_OK;
+}
+
+template <typename T>
+static hdx_status grow_pinned(T** p, size_t* cap, size_t need) {
+    if (need <= *cap) return HDX_OK;
+    size_t n = std::max(need, *cap * 3 / 2);
+    (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipHostMalloc((void**)p, n * sizeof(T), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(HDX_E_NOMEM, "hipHostMalloc(%zu) failed", n * sizeof(T));
+    }
+    *cap = n;
+    return HDX_OK;
+}
+
+static bool is_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+static bool is_numeric_code(uint8_t c) { return c >= CODE_INT64; }
+
+// ---- host-resident pipeline ------------------------------------------------
+
+static constexpr uint64_t kChunkBytes = 128ull << 20;  // blob bytes per in-flight chunk
+
+static hdx_status hash_host(const uint8_t* codes, uint32_t A, const uint8_t* blob,
+                            uint64_t blob_bytes, const uint64_t* obj_base,
+                            const uint32_t* attr_len, uint64_t n, uint64_t* coords) {
+    hdx_status st = bind_device(-1);
+    if (st != HDX_OK) return st;
+    ThreadState& ts = t_state;
+
+    // Host-side validation (the reference asserts here) + per-object extents.
+    std::vector<uint64_t> size(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t s = 0;
+        for (uint32_t j = 0; j < A; ++j) {
+            const uint32_t L = attr_len[i * A + j];
+            if (is_numeric_code(codes[j]) && L != 0 && L != 8)
+                return fail(HDX_E_BADSIZE, "object %llu attribute %u: numeric value of %u bytes",
+                            (unsigned long long)i, j, L);
+            s += L;
+        }
+        if (s >= (1ull << 32))
+            return fail(HDX_E_INVALID, "object %llu is %llu bytes (limit 4 GiB)",
+                        (unsigned long long)i, (unsigned long long)s);
+        if (obj_base[i] > blob_bytes || s > blob_bytes - obj_base[i])
+            return fail(HDX_E_INVALID, "object %llu [%llu,+%llu) outside blob of %llu bytes",
+                        (unsigned long long)i, (unsigned long long)obj_base[i],
+                        (unsigned long long)s, (unsigned long long)blob_bytes);
+        size[i] = s;
+    }
+
+    const bool blob_pinned = is_pinned(blob);
+    const bool len_pinned = is_pinned(attr_len);
+    const bool coords_pinned = is_pinned(coords);
+    for (auto& s : ts.slot)
+        if (!s.s) HIP_TRY(hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking));
+
+    BatchArgs args{};
+    args.A = A;
+    std::memcpy(args.codes, codes, A);
+
+    struct Pending { uint64_t first = 0, cnt = 0; bool live = false; } pend[2];
+    auto finish = [&](int k) -> hdx_status {
+        auto& sl = ts.slot[k];
+        if (!pend[k].live) return HDX_OK;
+        HIP_TRY(hipStreamSynchronize(sl.s));
+        if (!coords_pinned)
+            std::memcpy(coords + pend[k].first * A, sl.h_coords, pend[k].cnt * A * sizeof(uint64_t));
+        pend[k].live = false;
+        return HDX_OK;
+    };
+
+    uint64_t i = 0;
+    int k = 0;
+    while (i < n) {
+        // Grow the chunk while its byte extent stays under kChunkBytes.
+        uint64_t lo = obj_base[i], hi = obj_base[i] + size[i], e = i + 1;
+        while (e < n) {
+            const uint64_t nlo = std::min(lo, obj_base[e]);
+            const uint64_t nhi = std::max(hi, obj_base[e] + size[e]);
+            if (nhi - nlo > kChunkBytes) break;
+            lo = nlo; hi = nhi; ++e;
+        }
+        const uint64_t cnt = e - i, bytes = hi - lo;
+        auto& sl = ts.slot[k];
+        if ((st = finish(k)) != HDX_OK) return st;
+        if ((st = grow_dev(&sl.d_blob, &sl.cap_blob, std::max<uint64_t>(bytes, 1))) != HDX_OK) return st;
+        if ((st = grow_dev(&sl.d_base, &sl.cap_obj, cnt)) != HDX_OK) return st;
+        if ((st = grow_dev(&sl.d_len, &sl.cap_attr, cnt * A)) != HDX_OK) return st;
+        if ((st = grow_dev(&sl.d_coords, &sl.cap_coords, cnt * A)) != HDX_OK) return st;
+        if ((st = grow_pinned(&sl.h_base, &sl.cap_hbase, cnt)) != HDX_OK) return st;
+        for (uint64_t t = 0; t < cnt; ++t) sl.h_base[t] = obj_base[i + t] - lo;
+
+        const uint8_t* src_blob = blob + lo;
+        if (!blob_pinned) {
+            if ((st = grow_pinned(&sl.h_blob, &sl.cap_hblob, std::max<uint64_t>(bytes, 1))) != HDX_OK)
+                return st;
+            std::memcpy(sl.h_blob, blob + lo, bytes);
+            src_blob = sl.h_blob;
+        }
+        const uint32_t* src_len = attr_len + i * A;
+        if (!len_pinned) {
+            if ((st = grow_pinned(&sl.h_len, &sl.cap_hlen, cnt * A)) != HDX_OK) return st;
+            std::memcpy(sl.h_len, attr_len + i * A, cnt * A * sizeof(uint32_t));
+            src_len = sl.h_len;
+        }
+        HIP_TRY(hipMemcpyAsync(sl.d_blob, src_blob, bytes, hipMemcpyHostToDevice, sl.s));
+        HIP_TRY(hipMemcpyAsync(sl.d_base, sl.h_base, cnt * 8, hipMemcpyHostToDevice, sl.s));
+        HIP_TRY(hipMemcpyAsync(sl.d_len, src_len, cnt * A * 4, hipMemcpyHostToDevice, sl.s));
+        args.blob = sl.d_blob;
+        args.obj_base = sl.d_base;
+        args.attr_len = sl.d_len;
+        args.coords = sl.d_coords;
+        args.status = nullptr;  // sizes validated above
+        args.n = cnt;
+        HIP_TRY(launch_hash_batch(args, sl.s));
+        uint64_t* dst = coords + i * A;
+        if (!coords_pinned) {
+            if ((st = grow_pinned(&sl.h_coords, &sl.cap_hcoords, cnt * A)) != HDX_OK) return st;
+            dst = sl.h_coords;
+        }
+        HIP_TRY(hipMemcpyAsync(dst, sl.d_coords, cnt * A * 8, hipMemcpyDeviceToHost, sl.s));
+        pend[k] = {i, cnt, true};
+        i = e;
+        k ^= 1;
+    }
+    if ((st = finish(k)) != HDX_OK) return st;
+    return finish(k ^ 1);
+}
+
+}  // namespace hdx
+
+using namespace hdx;
+
+// ---- exported C-ABI --------------------------------------------------------
+
+HDX_EXPORT int hdx_abi_version(void) { return HDX_ABI_VERSION; }
+
+HDX_EXPORT const char* hdx_version(void) {
+    return "hdxhash " "1.0" " (gfx950; CityHash64 v1.1 / ordered encodings / timestamp)";
+}
+
+HDX_EXPORT const char* hdx_last_error(void) { return t_err.c_str(); }
+
+HDX_EXPORT int hdx_device_count(void) {
+    std::call_once(g_probe_once, probe);
+    return g_ndev < 0 ? 0 : g_ndev;
+}
+
+HDX_EXPORT hdx_status hdx_init(int device) {
+    if (device < 0) return fail(HDX_E_INVALID, "device %d", device);
+    return bind_device(device);
+}
+
+HDX_EXPORT hdx_status hdx_sync(hdx_stream stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (!s) {
+        hdx_status st = thread_stream(&s);
+        if (st != HDX_OK) return st;
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    return HDX_OK;
+}
+
+HDX_EXPORT hdx_status hdx_schema_check(const uint32_t* types, uint32_t attrs_sz) {
+    return check_schema(types, attrs_sz, nullptr);
+}
+
+HDX_EXPORT int hdx_type_hashable(uint32_t type) { return type_code(type) > 0 ? 1 : 0; }
+
+HDX_EXPORT hdx_status hdx_hash_batch_device(const uint32_t* types, uint32_t attrs_sz,
+                                            const uint8_t* blob, const uint64_t* obj_base,
+                                            const uint32_t* attr_len, uint64_t n,
+                                            uint64_t* coords, uint32_t* status_dev,
+                                            hdx_stream stream) {
+    BatchArgs args{};
+    hdx_status st = check_schema(types, attrs_sz, args.codes);
+    if (st != HDX_OK) return st;
+    if (n == 0) return HDX_OK;
+    if (!blob || !obj_base || !attr_len || !coords)
+        return fail(HDX_E_INVALID, "NULL device pointer");
+    if ((st = bind_device(-1)) != HDX_OK) return st;
+    hipStream_t s = (hipStream_t)stream;
+    if (!s && (st = thread_stream(&s)) != HDX_OK) return st;
+    args.blob = blob;
+    args.obj_base = obj_base;
+    args.attr_len = attr_len;
+    args.coords = coords;
+    args.status = status_dev;
+    args.n = n;
+    args.A = attrs_sz;
+    HIP_TRY(launch_hash_batch(args, s));
+    return HDX_OK;
+}
+
+HDX_EXPORT hdx_status hdx_hash_batch_host(const uint32_t* types, uint32_t attrs_sz,
+                                          const uint8_t* blob, uint64_t blob_bytes,
+                                          const uint64_t* obj_base, const uint32_t* attr_len,
+                                          uint64_t n, uint64_t* coords) {
+    uint8_t codes[HDX_MAX_ATTRS];
+    hdx_status st = check_schema(types, attrs_sz, codes);
+    if (st != HDX_OK) return st;
+    if (n == 0) return HDX_OK;
+    if (!obj_base || !attr_len || !coords || (!blob && blob_bytes))
+        return fail(HDX_E_INVALID, "NULL host pointer");
+    static const uint8_t one = 0;
+    return hash_host(codes, attrs_sz, blob ? blob : &one, blob_bytes, obj_base, attr_len, n, coords);
+}
+
+HDX_EXPORT hdx_status hdx_hash_object(const uint32_t* types, uint32_t attrs_sz,
+                                      const uint8_t* key, size_t key_len,
+                                      const uint8_t* const* values, const size_t* value_lens,
+                                      uint64_t* hs) {
+    uint8_t codes[HDX_MAX_ATTRS];
+    hdx_status st = check_schema(types, attrs_sz, codes);
+    if (st != HDX_OK) return st;
+    if (!hs || (!key && key_len) || (attrs_sz > 1 && (!values || !value_lens)))
+        return fail(HDX_E_INVALID, "NULL pointer");
+    // Pack {key, value[0..A-2]} contiguously: one object, one launch.
+    uint64_t total = key_len;
+    uint32_t lens[HDX_MAX_ATTRS];
+    lens[0] = (uint32_t)key_len;
+    if (key_len >= (1ull << 32)) return fail(HDX_E_INVALID, "key of %zu bytes", key_len);
+    for (uint32_t j = 1; j < attrs_sz; ++j) {
+        if (value_lens[j - 1] >= (1ull << 32))
+            return fail(HDX_E_INVALID, "value of %zu bytes", value_lens[j - 1]);
+        lens[j] = (uint32_t)value_lens[j - 1];
+        total += lens[j];
+    }
+    std::vector<uint8_t> packed(std::max<uint64_t>(total, 1));
+    uint64_t off = 0;
+    if (key_len) std::memcpy(packed.data(), key, key_len);
+    off = key_len;
+    for (uint32_t j = 1; j < attrs_sz; ++j) {
+        if (lens[j]) std::memcpy(packed.data() + off, values[j - 1], lens[j]);
+        off += lens[j];
+    }
+    const uint64_t base = 0;
+    return hash_host(codes, attrs_sz, packed.data(), total, &base, lens, 1, hs);
+}
+
+HDX_EXPORT hdx_status hdx_hash_key(const uint32_t* types, uint32_t attrs_sz, const uint8_t* key,
+                                   size_t key_len, uint64_t* h) {
+    if (!types || attrs_sz == 0) return fail(HDX_E_INVALID, "empty schema");
+    (void)attrs_sz;
+    return hdx_hash_object(types, 1, key, key_len, nullptr, nullptr, h);
+}
+
+HDX_EXPORT hdx_status hdx_hash_value(uint32_t type, const uint8_t* data, size_t len, uint64_t* out) {
+    return hdx_hash_object(&type, 1, data, len, nullptr, nullptr, out);
+}
+
+HDX_EXPORT hdx_status hdx_alloc_pinned(size_t bytes, void** out) {
+    if (!out) return fail(HDX_E_INVALID, "out is NULL");
+    hdx_status st = bind_device(-1);
+    if (st != HDX_OK) return st;
+    if (hipHostMalloc(out, std::max<size_t>(bytes, 1), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(HDX_E_NOMEM, "hipHostMalloc(%zu) failed", bytes);
+    }
+    return HDX_OK;
+}
+
+HDX_EXPORT hdx_status hdx_free_pinned(void* p) {
+    HIP_TRY(hipHostFree(p));
+    return HDX_OK;
+}
+
+static hdx_status synth_args(const hdx_synth_rule* rules, uint32_t A, uint64_t seed, uint64_t first,
+                             uint64_t n, SynthArgs* a) {
+    if (!rules || A == 0 || A > 64) return fail(HDX_E_INVALID, "synth: 1 <= attrs_sz <= 64");
+    *a = SynthArgs{};
+    a->seed = seed;
+    a->first = first;
+    a->n = n;
+    a->A = A;
+    for (uint32_t j = 0; j < A; ++j) {
+        if (type_code(rules[j].type) < 0) return fail(HDX_E_BADTYPE, "synth: type %u", rules[j].type);
+        if (rules[j].kind > 2 || (rules[j].kind == 1 && rules[j].hi < rules[j].lo))
+            return fail(HDX_E_INVALID, "synth: bad rule at %u", j);
+        a->rules[j] = rules[j];
+    }
+    return HDX_OK;
+}
+
+HDX_EXPORT hdx_status hdx_synth_lengths(const hdx_synth_rule* rules, uint32_t attrs_sz, uint64_t seed,
+                                        uint64_t first, uint64_t n, uint32_t* attr_len_dev,
+                                        hdx_stream stream) {
+    SynthArgs a;
+    hdx_status st = synth_args(rules, attrs_sz, seed, first, n, &a);
+    if (st != HDX_OK) return st;
+    if ((st = bind_device(-1)) != HDX_OK) return st;
+    hipStream_t s = (hipStream_t)stream;
+    if (!s && (st = thread_stream(&s)) != HDX_OK) return st;
+    HIP_TRY(launch_synth_lengths(a, attr_len_dev, s));
+    return HDX_OK;
+}
+
+HDX_EXPORT hdx_status hdx_synth_fill(const hdx_synth_rule* rules, uint32_t attrs_sz, uint64_t seed,
+                                     uint64_t first, uint64_t n, const uint64_t* obj_base_dev,
+                                     const uint32_t* attr_len_dev, uint8_t* blob_dev, uint64_t bytes,
+                                     hdx_stream stream) {
+    SynthArgs a;
+    hdx_status st = synth_args(rules, attrs_sz, seed, first, n, &a);
+    if (st != HDX_OK) return st;
+    if ((st = bind_device(-1)) != HDX_OK) return st;
+    hipStream_t s = (hipStream_t)stream;
+    if (!s && (st = thread_stream(&s)) != HDX_OK) return st;
+    HIP_TRY(launch_synth_fill(a, obj_base_dev, attr_len_dev, blob_dev, bytes, s));
+    return HDX_OK;
+}

@@ -1,0 +1,54 @@
+// hdx_internal.h — declarations shared by the kernels and the C-ABI layer.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/hdxhash.h"
+
+namespace hdx {
+
+// Attribute classes the kernel dispatches on (host maps hyperdatatype -> code).
+enum : uint32_t {
+    CODE_ZERO = 0,     // not hashable: document/list/set/map/macaroon -> 0
+    CODE_STRING = 1,
+    CODE_INT64 = 2,
+    CODE_FLOAT = 3,
+    CODE_TS_SECOND = 4,  // .. CODE_TS_MONTH = 9, in hyperdatatype order
+    CODE_TS_MONTH = 9,
+};
+
+
+// Kernel arguments, passed by value (kernarg segment).  codes[] holds the
+// per-attribute dispatch class (hdx_device_hash.h CODE_*).
+struct BatchArgs {
+    const uint8_t* blob;
+    const uint64_t* obj_base;
+    const uint32_t* attr_len;
+    uint64_t* coords;
+    uint32_t* status;
+    uint64_t n;
+    uint32_t A;
+    uint32_t pad_;
+    uint8_t codes[HDX_MAX_ATTRS];
+};
+
+hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream);
+
+struct SynthArgs {
+    uint64_t seed;
+    uint64_t first;
+    uint64_t n;
+    uint32_t A;
+    uint32_t pad_;
+    hdx_synth_rule rules[64];
+};
+
+hipError_t launch_synth_lengths(const SynthArgs& a, uint32_t* attr_len, hipStream_t s);
+hipError_t launch_synth_fill(const SynthArgs& a, const uint64_t* obj_base, const uint32_t* attr_len,
+                             uint8_t* blob, uint64_t bytes, hipStream_t s);
+
+// hyperdatatype -> dispatch code; -1 for an id datatype_info::lookup rejects.
+int type_code(uint32_t type);
+
+}  // namespace hdx

@@ -1,0 +1,112 @@
+"""Python mirror of the reference hashing interface (common/hash.h:43-55).
+
+    hash(type, value)               -> uint64_t hash(hyperdatatype, const e::slice&)
+    hash_key(schema, key)           -> void hash(const schema&, const e::slice& key, uint64_t* h)
+    hash_object(schema, key, vals)  -> void hash(const schema&, key, std::vector<e::slice>, uint64_t* hs)
+
+plus the batched GPU path over the packed layout of include/hdxhash.h:
+
+    hash_batch(types, blob, obj_base, attr_len)       device-resident (torch HIP tensors)
+    hash_batch_host(types, blob, obj_base, attr_len)  host-resident (numpy), pipelined H2D/D2H
+
+All of them run the gfx950 kernels in libhdxhash.so.  Where the reference
+asserts (unknown type, mis-sized numeric value) these raise HdxError.
+"""
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import HdxError, check, lib
+from .datatypes import Schema
+
+
+def _u32_array(xs):
+    arr = np.ascontiguousarray(np.asarray(xs, dtype=np.uint32))
+    return arr
+
+
+def schema_check(types) -> None:
+    t = _u32_array(types)
+    check(lib().hdx_schema_check(t.ctypes.data, len(t)))
+
+
+def hashable(type_id: int) -> bool:
+    return bool(lib().hdx_type_hashable(type_id))
+
+
+def hash(type_id: int, value: bytes) -> int:  # noqa: A001 (mirrors hyperdex::hash)
+    out = ctypes.c_uint64(0)
+    buf = ctypes.create_string_buffer(bytes(value), max(len(value), 1))
+    check(lib().hdx_hash_value(type_id, buf, len(value), ctypes.byref(out)))
+    return out.value
+
+
+def _types_of(sc):
+    return sc.types() if isinstance(sc, Schema) else list(sc)
+
+
+def hash_key(sc, key: bytes) -> int:
+    t = _u32_array(_types_of(sc))
+    out = ctypes.c_uint64(0)
+    buf = ctypes.create_string_buffer(bytes(key), max(len(key), 1))
+    check(lib().hdx_hash_key(t.ctypes.data, len(t), buf, len(key), ctypes.byref(out)))
+    return out.value
+
+
+def hash_object(sc, key: bytes, values: Sequence[bytes]):
+    t = _u32_array(_types_of(sc))
+    A = len(t)
+    if len(values) < A - 1:
+        raise HdxError(_lib.HDX_E_INVALID, "need %d values, got %d" % (A - 1, len(values)))
+    bufs = [ctypes.create_string_buffer(bytes(v), max(len(v), 1)) for v in values[:A - 1]]
+    ptrs = (ctypes.c_void_p * max(A - 1, 1))(*[ctypes.addressof(b) for b in bufs])
+    lens = (ctypes.c_size_t * max(A - 1, 1))(*[len(v) for v in values[:A - 1]])
+    out = (ctypes.c_uint64 * A)()
+    kbuf = ctypes.create_string_buffer(bytes(key), max(len(key), 1))
+    check(lib().hdx_hash_object(t.ctypes.data, A, kbuf, len(key), ptrs, lens, out))
+    return list(out)
+
+
+def hash_batch(types, blob, obj_base, attr_len, coords=None, status=None, stream=None):
+    """Device-resident batch.  blob/obj_base/attr_len/coords are torch tensors on
+    a HIP device (any integer dtype of the right width); returns coords (n, A)
+    as an int64 tensor holding the uint64 bit patterns.  Asynchronous on
+    `stream` (default: torch's current stream)."""
+    import torch
+
+    t = _u32_array(types)
+    A = len(t)
+    n = obj_base.numel()
+    assert attr_len.numel() == n * A, "attr_len must hold n*A lengths"
+    assert blob.element_size() == 1 and obj_base.element_size() == 8 and attr_len.element_size() == 4
+    for x in (blob, obj_base, attr_len):
+        assert x.is_cuda and x.is_contiguous()
+    if coords is None:
+        coords = torch.empty((n, A), dtype=torch.int64, device=obj_base.device)
+    assert coords.is_cuda and coords.is_contiguous() and coords.element_size() == 8
+    if stream is None:
+        stream = torch.cuda.current_stream(obj_base.device)
+    handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+    check(lib().hdx_hash_batch_device(
+        t.ctypes.data, A, blob.data_ptr(), obj_base.data_ptr(), attr_len.data_ptr(), n,
+        coords.data_ptr(), status.data_ptr() if status is not None else None, handle))
+    return coords
+
+
+def hash_batch_host(types, blob, obj_base, attr_len, out: Optional[np.ndarray] = None):
+    """Host-resident batch (numpy in, numpy (n, A) uint64 out), synchronous."""
+    t = _u32_array(types)
+    A = len(t)
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    obj_base = np.ascontiguousarray(obj_base, dtype=np.uint64)
+    attr_len = np.ascontiguousarray(attr_len, dtype=np.uint32)
+    n = len(obj_base)
+    assert attr_len.size == n * A
+    if out is None:
+        out = np.empty((n, A), dtype=np.uint64)
+    check(lib().hdx_hash_batch_host(t.ctypes.data, A, blob.ctypes.data if blob.size else None,
+                                    blob.size, obj_base.ctypes.data, attr_len.ctypes.data, n,
+                                    out.ctypes.data))
+    return out

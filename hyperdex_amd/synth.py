@@ -1,0 +1,193 @@
+"""Synthetic object batches (SURVEY §8d shapes), on the host (numpy) or in HBM.
+
+The device generator is hyperdex_amd/csrc/hdx_synth.hip; this module restates
+the same counter-based rules in numpy so tests can rebuild any batch on the
+host.  RNG: splitmix64 finaliser over
+    R(stream, k) = mix64(seed + stream * 0xd1b54a32d192ed03 + (k + 1) * 0x9e3779b97f4a7c15)
+Streams: 1 uniform lengths, 2(+first<<8) blob bytes, 3 numeric values,
+4 numeric special-value selector.  Default seed 0x4859504552444558 ("HYPERDEX").
+"""
+import ctypes
+from dataclasses import dataclass
+from typing import List, Tuple
+
+import numpy as np
+
+from . import datatypes as dt
+
+SEED = 0x4859504552444558
+GOLD = np.uint64(0x9e3779b97f4a7c15)
+SALT = np.uint64(0xd1b54a32d192ed03)
+
+FIXED, UNIFORM, NUMERIC = 0, 1, 2
+
+
+@dataclass(frozen=True)
+class Rule:
+    type: int
+    kind: int
+    lo: int = 0
+    hi: int = 0
+
+
+def _s(L):  # key STRING fixed 64 B
+    return Rule(dt.HYPERDATATYPE_STRING, FIXED, L, L)
+
+
+def _n(t):
+    return Rule(t, NUMERIC, 8, 8)
+
+
+# SURVEY §8d configs (config 4 = 3b sharded; config 5 reuses 3b).
+CONFIGS = {
+    "cfg1": [_s(64)],
+    "cfg2": [_s(64)] + [_n(dt.HYPERDATATYPE_INT64)] * 4,
+    "cfg3a": [_s(64)] * 17,
+    "cfg3b": ([_s(64)] + [Rule(dt.HYPERDATATYPE_STRING, UNIFORM, 0, 195)] * 10
+              + [_n(dt.HYPERDATATYPE_INT64)] * 3 + [_n(dt.HYPERDATATYPE_FLOAT)] * 3),
+    # test-only: every hashable type, non-hashable containers, every CityHash regime
+    "mixed": ([Rule(dt.HYPERDATATYPE_STRING, UNIFORM, 0, 300)]
+              + [Rule(dt.HYPERDATATYPE_STRING, UNIFORM, 0, 20)]
+              + [_n(dt.HYPERDATATYPE_INT64), _n(dt.HYPERDATATYPE_FLOAT)]
+              + [_n(t) for t in dt.TIMESTAMPS]
+              + [Rule(dt.HYPERDATATYPE_LIST_STRING, UNIFORM, 0, 40),
+                 Rule(dt.HYPERDATATYPE_DOCUMENT, UNIFORM, 0, 24),
+                 Rule(dt.HYPERDATATYPE_MAP_INT64_FLOAT, FIXED, 16, 16),
+                 Rule(dt.HYPERDATATYPE_STRING, UNIFORM, 60, 140)]),
+    # test-only: many attributes, all strings of every length class
+    "wide": [Rule(dt.HYPERDATATYPE_STRING, UNIFORM, 0, 130)] * 70,
+    "keyonly_long": [Rule(dt.HYPERDATATYPE_STRING, UNIFORM, 200, 4000)],
+}
+
+
+def payload_bytes_per_object(name: str) -> float:
+    tot = 0.0
+    for r in CONFIGS[name]:
+        tot += (r.lo + r.hi) / 2 if r.kind == UNIFORM else (8 * 0.99 if r.kind == NUMERIC else r.lo)
+    return tot
+
+
+def mix64(z: np.ndarray) -> np.ndarray:
+    z = z.astype(np.uint64, copy=True)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+    return z ^ (z >> np.uint64(31))
+
+
+def rnd(seed: int, stream: int, k: np.ndarray) -> np.ndarray:
+    k = np.asarray(k, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        base = np.uint64(seed) + np.uint64(stream & 0xffffffffffffffff) * SALT
+        return mix64(base + (k + np.uint64(1)) * GOLD)
+
+
+def lengths(rules: List[Rule], n: int, seed: int = SEED, first: int = 0) -> np.ndarray:
+    A = len(rules)
+    f = (np.uint64(first) * np.uint64(A)) + np.arange(n * A, dtype=np.uint64)
+    out = np.empty(n * A, dtype=np.uint32)
+    j = np.arange(n * A) % A
+    for jj, r in enumerate(rules):
+        m = j == jj
+        if r.kind == FIXED:
+            out[m] = r.lo
+        elif r.kind == UNIFORM:
+            out[m] = (r.lo + rnd(seed, 1, f[m]) % np.uint64(r.hi - r.lo + 1)).astype(np.uint32)
+        else:
+            out[m] = np.where(rnd(seed, 4, f[m]) % np.uint64(100) == 0, 0, 8).astype(np.uint32)
+    return out
+
+
+def numeric_values(t: int, seed: int, f: np.ndarray) -> np.ndarray:
+    """Mirror of synth_numeric() in hdx_synth.hip (uint64 bit patterns)."""
+    sel = rnd(seed, 4, f) % np.uint64(100)
+    v = rnd(seed, 3, f)
+    FRAC, SIGN = np.uint64(0x000fffffffffffff), np.uint64(0x8000000000000000)
+    if t == dt.HYPERDATATYPE_INT64:
+        mm = np.where(v & np.uint64(1), np.uint64(0x7fffffffffffffff), SIGN)
+        return np.where(sel == 1, mm, v)
+    if t == dt.HYPERDATATYPE_FLOAT:
+        e = np.uint64(963) + ((v >> np.uint64(52)) & np.uint64(0x7f)) % np.uint64(121)
+        out = (v & SIGN) | (e << np.uint64(52)) | (v & FRAC)
+        spec = {1: np.zeros_like(v), 2: np.full_like(v, SIGN),
+                3: np.full_like(v, 0x7ff0000000000000), 4: np.full_like(v, 0xfff0000000000000),
+                5: np.uint64(0x7ff8000000000000) | (v & np.uint64(0x8007ffffffffffff)),
+                6: (v & FRAC) | np.uint64(1), 7: SIGN | (v & FRAC) | np.uint64(1)}
+        for s, val in spec.items():
+            out = np.where(sel == s, val, out)
+        return out
+    return np.where(sel < 50, v & np.uint64((1 << 51) - 1), v)
+
+
+def object_bases(attr_len: np.ndarray, A: int) -> Tuple[np.ndarray, int]:
+    sizes = attr_len.reshape(-1, A).astype(np.uint64).sum(axis=1)
+    base = np.zeros(len(sizes), dtype=np.uint64)
+    if len(sizes) > 1:
+        base[1:] = np.cumsum(sizes[:-1], dtype=np.uint64)
+    total = int(sizes.sum()) if len(sizes) else 0
+    return base, total
+
+
+def blob_bytes(seed: int, first: int, nbytes: int) -> np.ndarray:
+    words = rnd(seed, 2 + (first << 8), np.arange((nbytes + 7) // 8, dtype=np.uint64))
+    return words.view(np.uint8)[:nbytes].copy()
+
+
+def make_batch_host(name_or_rules, n: int, seed: int = SEED, first: int = 0):
+    """(types u32[A], blob u8, obj_base u64[n], attr_len u32[n*A]) on the host,
+    byte-identical to make_batch_device(..) of the same arguments."""
+    rules = CONFIGS[name_or_rules] if isinstance(name_or_rules, str) else list(name_or_rules)
+    A = len(rules)
+    L = lengths(rules, n, seed, first)
+    base, total = object_bases(L, A)
+    blob = blob_bytes(seed, first, total)
+    Lm = L.reshape(n, A)
+    offs = base[:, None] + np.concatenate(
+        [np.zeros((n, 1), np.uint64), np.cumsum(Lm, axis=1, dtype=np.uint64)[:, :-1]], axis=1)
+    for j, r in enumerate(rules):
+        if r.kind != NUMERIC:
+            continue
+        rows = np.nonzero(Lm[:, j] == 8)[0]
+        f = (np.uint64(first) + rows.astype(np.uint64)) * np.uint64(A) + np.uint64(j)
+        vals = numeric_values(r.type, seed, f).astype("<u8").view(np.uint8).reshape(-1, 8)
+        idx = offs[rows, j].astype(np.int64)[:, None] + np.arange(8)[None, :]
+        blob[idx] = vals
+    types = np.array([r.type for r in rules], dtype=np.uint32)
+    return types, blob, base, L
+
+
+def c_rules(rules: List[Rule]):
+    from ._lib import SynthRule
+    arr = (SynthRule * len(rules))()
+    for i, r in enumerate(rules):
+        arr[i] = SynthRule(r.type, r.kind, r.lo, r.hi)
+    return arr
+
+
+def make_batch_device(name_or_rules, n: int, seed: int = SEED, first: int = 0, device=None,
+                      pad: int = 0):
+    """Generate the batch directly in HBM (torch tensors on `device`).
+
+    Returns (types np.u32[A], blob u8, obj_base i64[n], attr_len i32[n*A]);
+    obj_base/attr_len are int64/int32 tensors holding the u64/u32 values."""
+    import torch
+
+    from ._lib import check, lib
+
+    rules = CONFIGS[name_or_rules] if isinstance(name_or_rules, str) else list(name_or_rules)
+    A = len(rules)
+    device = device or torch.device("cuda", torch.cuda.current_device())
+    cr = c_rules(rules)
+    stream = torch.cuda.current_stream(device).cuda_stream
+    attr_len = torch.empty(n * A, dtype=torch.int32, device=device)
+    check(lib().hdx_synth_lengths(cr, A, seed, first, n, attr_len.data_ptr(), stream))
+    sizes = attr_len.view(n, A).to(torch.int64).sum(dim=1)
+    obj_base = torch.zeros(n, dtype=torch.int64, device=device)
+    if n > 1:
+        obj_base[1:] = torch.cumsum(sizes[:-1], dim=0)
+    total = int(sizes.sum().item()) if n else 0
+    blob = torch.empty(total + pad, dtype=torch.uint8, device=device)
+    check(lib().hdx_synth_fill(cr, A, seed, first, n, obj_base.data_ptr(), attr_len.data_ptr(),
+                               blob.data_ptr(), total, stream))
+    types = np.array([r.type for r in rules], dtype=np.uint32)
+    return types, blob, obj_base, attr_len

@@ -1,0 +1,164 @@
+/*
+ * hdxhash.h — C-ABI of the MI355X hyperspace-hashing engine (libhdxhash.so).
+ *
+ * Replaces the per-object attribute hashing of HyperDex:
+ *   uint64_t hyperdex::hash(hyperdatatype, const e::slice&)          common/hash.h:43-44, hash.cc:34-46
+ *   void     hyperdex::hash(const schema&, const e::slice& key, uint64_t* h)
+ *                                                                  common/hash.h:46-49, hash.cc:48-54
+ *   void     hyperdex::hash(const schema&, const e::slice& key,
+ *                           const std::vector<e::slice>& value, uint64_t* hs)
+ *                                                                  common/hash.h:51-55, hash.cc:56-68
+ * with (a) C entry points of the same meaning (hdx_hash_value / hdx_hash_key /
+ * hdx_hash_object) and (b) a batched entry point over a packed layout that
+ * runs the hand-written gfx950 kernels (hdx_hash_batch_device / _host).
+ * The C++ signatures themselves are provided header-only by
+ * include/hyperdex_amd/hash.h on top of these functions.
+ *
+ * Plain pointers and sizes only.  Type ids are the reference's
+ * enum hyperdatatype values (include/hyperdex.h:53-102).
+ *
+ * Packed batch layout (all arrays caller-owned):
+ *   types[A]        u32 hyperdatatype per attribute position; attr 0 = key
+ *                   (schema.attrs[i].type, common/schema.h:40-51)
+ *   blob            bytes; object i's attributes are stored back to back
+ *                   starting at blob + obj_base[i] (any alignment)
+ *   obj_base[n]     u64 byte offset of object i in blob (objects may have gaps
+ *                   between them and may appear in any order)
+ *   attr_len[n*A]   u32 length of attribute j of object i at [i*A + j]
+ *   coords[n*A]     u64 output, row-major: coords[i*A + j] = hash of attr j
+ *                   (= hs[j] of the reference's whole-object hash)
+ * Limits: 1 <= A <= HDX_MAX_ATTRS; each object's attributes total < 4 GiB.
+ *
+ * Errors: the reference asserts on an unknown type (hash.cc:38) and on an
+ * int64/float/timestamp value whose size is not 0 or 8
+ * (datatype_int64.cc:233, datatype_float.cc:204, datatype_timestamp.cc:46);
+ * this library returns HDX_E_BADTYPE / HDX_E_BADSIZE instead and never
+ * aborts.  Non-hashable types (document, list, set, map, macaroon) hash to 0
+ * exactly as in the reference (hash.cc:40-43).
+ *
+ * Threading: every entry point is thread-safe.  Device work is issued on the
+ * caller's stream (batch API) or on a per-thread library stream (host and
+ * per-object API).  There is no CPU implementation behind any entry point:
+ * without a usable gfx950 device every compute call returns HDX_E_DEVICE.
+ */
+#ifndef HDXHASH_H
+#define HDXHASH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HDX_ABI_VERSION 1
+#define HDX_MAX_ATTRS 256
+
+typedef enum hdx_status {
+    HDX_OK = 0,
+    HDX_E_BADTYPE = 1,     /* unknown hyperdatatype (reference: assert(di)) */
+    HDX_E_BADSIZE = 2,     /* int64/float/timestamp value of size not in {0, 8} */
+    HDX_E_DEVICE = 3,      /* no usable device, or a HIP runtime error */
+    HDX_E_INVALID = 4,     /* bad argument: NULL pointer, A == 0, A > HDX_MAX_ATTRS */
+    HDX_E_NOMEM = 5        /* device or pinned allocation failed */
+} hdx_status;
+
+/* An opaque hipStream_t.  NULL means the library's per-thread stream. */
+typedef void* hdx_stream;
+
+/* ---- library state ---------------------------------------------------- */
+
+/* ABI version and a human-readable build string. */
+int hdx_abi_version(void);
+const char* hdx_version(void);
+/* Binds the calling thread to `device` (a HIP ordinal) and checks it is a
+ * gfx950 part.  Optional: every entry point initialises lazily on device 0
+ * or on the thread's current HIP device. */
+hdx_status hdx_init(int device);
+/* Number of HIP devices visible (0 without a GPU; never initialises one). */
+int hdx_device_count(void);
+/* Message for the last non-OK status returned on this thread. */
+const char* hdx_last_error(void);
+/* hipStreamSynchronize on `stream` (NULL: this thread's library stream). */
+hdx_status hdx_sync(hdx_stream stream);
+
+/* ---- schema ------------------------------------------------------------ */
+
+/* HDX_OK if every type id is a hyperdatatype the reference's
+ * datatype_info::lookup accepts (datatype_info.cc:72-141), else
+ * HDX_E_BADTYPE.  Host only; no device needed. */
+hdx_status hdx_schema_check(const uint32_t* types, uint32_t attrs_sz);
+/* 1 if datatype_info::lookup(type)->hashable() (string, int64, float,
+ * timestamp second..month), 0 otherwise (including unknown). */
+int hdx_type_hashable(uint32_t type);
+
+/* ---- batched hashing (the GPU path) -------------------------------------- */
+
+/* All of blob, obj_base, attr_len, coords are DEVICE pointers; `types` is a
+ * HOST array.  Asynchronous on `stream`: returns after the launch.  If
+ * `status_dev` (a device u32, may be NULL) is given, the kernel ORs
+ * (1u << HDX_E_BADSIZE) into it for any mis-sized numeric attribute (whose
+ * coordinate is then written as 0).  Returns HDX_E_BADTYPE / HDX_E_INVALID
+ * before launching anything. */
+hdx_status hdx_hash_batch_device(const uint32_t* types, uint32_t attrs_sz,
+                                 const uint8_t* blob, const uint64_t* obj_base,
+                                 const uint32_t* attr_len, uint64_t n,
+                                 uint64_t* coords, uint32_t* status_dev,
+                                 hdx_stream stream);
+
+/* Same batch with every array in HOST memory (pageable or pinned).
+ * Synchronous.  The library validates numeric sizes on the host, then
+ * streams the batch through the device in chunks, overlapping H2D copies,
+ * kernels and D2H copies on two streams.  blob_bytes is the size of the
+ * blob allocation (every object must lie inside it). */
+hdx_status hdx_hash_batch_host(const uint32_t* types, uint32_t attrs_sz,
+                               const uint8_t* blob, uint64_t blob_bytes,
+                               const uint64_t* obj_base, const uint32_t* attr_len,
+                               uint64_t n, uint64_t* coords);
+
+/* ---- per-value / per-object (the reference signatures, C form) ---------- */
+
+/* hash(hyperdatatype, slice)  — common/hash.cc:34-46 */
+hdx_status hdx_hash_value(uint32_t type, const uint8_t* data, size_t len, uint64_t* out);
+/* hash(schema, key, &h)       — common/hash.cc:48-54 (uses types[0] only) */
+hdx_status hdx_hash_key(const uint32_t* types, uint32_t attrs_sz,
+                        const uint8_t* key, size_t key_len, uint64_t* h);
+/* hash(schema, key, value, hs) — common/hash.cc:56-68.  values[k] /
+ * value_lens[k] are attribute k+1, k in [0, attrs_sz-1). */
+hdx_status hdx_hash_object(const uint32_t* types, uint32_t attrs_sz,
+                           const uint8_t* key, size_t key_len,
+                           const uint8_t* const* values, const size_t* value_lens,
+                           uint64_t* hs);
+
+/* ---- pinned host memory ------------------------------------------------- */
+
+hdx_status hdx_alloc_pinned(size_t bytes, void** out);
+hdx_status hdx_free_pinned(void* p);
+
+/* ---- synthetic batches (benchmark tooling; see hyperdex_amd/synth.py) ---- */
+
+/* Per-attribute synthetic rule, one per attribute position. */
+typedef struct hdx_synth_rule {
+    uint32_t type;   /* hyperdatatype */
+    uint32_t kind;   /* 0 fixed len lo; 1 uniform len in [lo, hi]; 2 numeric (8 B, 1% empty) */
+    uint32_t lo;
+    uint32_t hi;
+} hdx_synth_rule;
+
+/* attr_len[n*A] for objects [first, first+n) of the synthetic stream `seed`. */
+hdx_status hdx_synth_lengths(const hdx_synth_rule* rules, uint32_t attrs_sz, uint64_t seed,
+                             uint64_t first, uint64_t n, uint32_t* attr_len_dev,
+                             hdx_stream stream);
+/* Fills blob_dev[0, bytes) with the seed's byte stream (position-keyed), then
+ * writes the numeric attributes (int64/float/timestamp values incl. special
+ * values) at their offsets.  obj_base_dev must already hold the offsets. */
+hdx_status hdx_synth_fill(const hdx_synth_rule* rules, uint32_t attrs_sz, uint64_t seed,
+                          uint64_t first, uint64_t n, const uint64_t* obj_base_dev,
+                          const uint32_t* attr_len_dev, uint8_t* blob_dev, uint64_t bytes,
+                          hdx_stream stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HDXHASH_H */

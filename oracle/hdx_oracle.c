@@ -1,0 +1,316 @@
+/*
+ * hdx_oracle.c — plain-C restatement of the reference hashing path.
+ *
+ * TEST INFRASTRUCTURE ONLY (see hdx_oracle.h).  Compiled -O2 without
+ * -ffast-math so the IEEE comparisons and the timestamp's double division
+ * behave exactly as in the reference build.
+ *
+ * Each function names the reference file:line it restates.
+ */
+#define _GNU_SOURCE
+#include "hdx_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* include/hyperdex.h:53-102 */
+enum {
+    T_GENERIC = 9216, T_STRING = 9217, T_INT64 = 9218, T_FLOAT = 9219,
+    T_DOCUMENT = 9223,
+    T_LIST_GENERIC = 9280, T_LIST_STRING = 9281, T_LIST_INT64 = 9282, T_LIST_FLOAT = 9283,
+    T_SET_GENERIC = 9344, T_SET_STRING = 9345, T_SET_INT64 = 9346, T_SET_FLOAT = 9347,
+    T_MAP_GENERIC = 9408,
+    T_MAP_SS = 9417, T_MAP_SI = 9418, T_MAP_SF = 9419,
+    T_MAP_IS = 9425, T_MAP_II = 9426, T_MAP_IF = 9427,
+    T_MAP_FS = 9433, T_MAP_FI = 9434, T_MAP_FF = 9435,
+    T_TS_GENERIC = 9472,
+    T_TS_SECOND = 9473, T_TS_MINUTE = 9474, T_TS_HOUR = 9475,
+    T_TS_DAY = 9476, T_TS_WEEK = 9477, T_TS_MONTH = 9478,
+    T_MACAROON = 9664
+};
+
+/* ---- CityHash v1.1 (cityhash/city.cc) --------------------------------- */
+
+#define K0 0xc3a5c85c97cb3127ULL /* city.cc:116 */
+#define K1 0xb492b66fbe98f273ULL /* city.cc:117 */
+#define K2 0x9ae16a3b2f90404fULL /* city.cc:118 */
+#define KMUL 0x9ddfea08eb382d69ULL /* city.h:102 */
+
+/* city.cc:45-55,107-113: unaligned little-endian loads */
+static inline uint64_t ld64(const uint8_t* p) { uint64_t v; memcpy(&v, p, 8); return v; }
+static inline uint32_t ld32(const uint8_t* p) { uint32_t v; memcpy(&v, p, 4); return v; }
+
+/* city.cc:255-258 (never called with r == 0 on this path) */
+static inline uint64_t ror64(uint64_t v, int r) { return r == 0 ? v : (v >> r) | (v << (64 - r)); }
+/* city.cc:260-262 */
+static inline uint64_t smix(uint64_t v) { return v ^ (v >> 47); }
+
+/* city.cc:268-276: murmur-style 128->64 with an explicit multiplier */
+static uint64_t mix2(uint64_t u, uint64_t v, uint64_t mul) {
+    uint64_t a = (u ^ v) * mul;
+    a ^= a >> 47;
+    uint64_t b = (v ^ a) * mul;
+    b ^= b >> 47;
+    return b * mul;
+}
+/* city.cc:264-266 -> city.h:100-109 (Hash128to64) */
+static uint64_t mix2k(uint64_t u, uint64_t v) { return mix2(u, v, KMUL); }
+
+/* city.cc:278-301 */
+static uint64_t city_0to16(const uint8_t* s, size_t n) {
+    if (n >= 8) {
+        uint64_t m = K2 + (uint64_t)n * 2;
+        uint64_t a = ld64(s) + K2;
+        uint64_t b = ld64(s + n - 8);
+        uint64_t c = ror64(b, 37) * m + a;
+        uint64_t d = (ror64(a, 25) + b) * m;
+        return mix2(c, d, m);
+    }
+    if (n >= 4) {
+        uint64_t m = K2 + (uint64_t)n * 2;
+        uint64_t a = ld32(s);
+        return mix2((uint64_t)n + (a << 3), ld32(s + n - 4), m);
+    }
+    if (n > 0) {
+        uint32_t y = (uint32_t)s[0] + ((uint32_t)s[n >> 1] << 8);
+        uint32_t z = (uint32_t)n + ((uint32_t)s[n - 1] << 2);
+        return smix((uint64_t)y * K2 ^ (uint64_t)z * K0) * K2;
+    }
+    return K2;
+}
+
+/* city.cc:305-313 */
+static uint64_t city_17to32(const uint8_t* s, size_t n) {
+    uint64_t m = K2 + (uint64_t)n * 2;
+    uint64_t a = ld64(s) * K1;
+    uint64_t b = ld64(s + 8);
+    uint64_t c = ld64(s + n - 8) * m;
+    uint64_t d = ld64(s + n - 16) * K2;
+    return mix2(ror64(a + b, 43) + ror64(c, 30) + d, a + ror64(b + K2, 18) + c, m);
+}
+
+/* city.cc:317-337: weak 32-byte mix with two seeds, returns (lo, hi) */
+static void weak32(const uint8_t* s, uint64_t a, uint64_t b, uint64_t* lo, uint64_t* hi) {
+    uint64_t w = ld64(s), x = ld64(s + 8), y = ld64(s + 16), z = ld64(s + 24);
+    a += w;
+    b = ror64(b + a + z, 21);
+    uint64_t c = a;
+    a += x;
+    a += y;
+    b += ror64(a, 44);
+    *lo = a + z;
+    *hi = b + c;
+}
+
+/* city.cc:340-359 */
+static uint64_t city_33to64(const uint8_t* s, size_t n) {
+    uint64_t m = K2 + (uint64_t)n * 2;
+    uint64_t a = ld64(s) * K2;
+    uint64_t b = ld64(s + 8);
+    uint64_t c = ld64(s + n - 24);
+    uint64_t d = ld64(s + n - 32);
+    uint64_t e = ld64(s + 16) * K2;
+    uint64_t f = ld64(s + 24) * 9;
+    uint64_t g = ld64(s + n - 8);
+    uint64_t h = ld64(s + n - 16) * m;
+    uint64_t u = ror64(a + g, 43) + (ror64(b, 30) + c) * 9;
+    uint64_t v = ((a + g) ^ d) + f + 1;
+    uint64_t w = __builtin_bswap64((u + v) * m) + h;
+    uint64_t x = ror64(e + f, 42) + c;
+    uint64_t y = (__builtin_bswap64((v + w) * m) + g) * m;
+    uint64_t z = e + f + c;
+    a = __builtin_bswap64((x + z) * m + y) + b;
+    b = smix((z + a) * m + d + h) * m;
+    return b + x;
+}
+
+/* city.cc:361-397 */
+uint64_t hdxo_cityhash64(const uint8_t* s, size_t n) {
+    if (n <= 16) return city_0to16(s, n);
+    if (n <= 32) return city_17to32(s, n);
+    if (n <= 64) return city_33to64(s, n);
+
+    uint64_t x = ld64(s + n - 40);
+    uint64_t y = ld64(s + n - 16) + ld64(s + n - 56);
+    uint64_t z = mix2k(ld64(s + n - 48) + n, ld64(s + n - 24));
+    uint64_t v0, v1, w0, w1;
+    weak32(s + n - 64, n, z, &v0, &v1);
+    weak32(s + n - 32, y + K1, x, &w0, &w1);
+    x = x * K1 + ld64(s);
+
+    size_t left = (n - 1) & ~(size_t)63;
+    do {
+        x = ror64(x + y + v0 + ld64(s + 8), 37) * K1;
+        y = ror64(y + v1 + ld64(s + 48), 42) * K1;
+        x ^= w1;
+        y += v0 + ld64(s + 40);
+        z = ror64(z + w0, 33) * K1;
+        uint64_t nv0, nv1, nw0, nw1;
+        weak32(s, v1 * K1, x + w0, &nv0, &nv1);
+        weak32(s + 32, z + w1, y + ld64(s + 16), &nw0, &nw1);
+        v0 = nv0; v1 = nv1; w0 = nw0; w1 = nw1;
+        uint64_t t = z; z = x; x = t;
+        s += 64;
+        left -= 64;
+    } while (left != 0);
+    return mix2k(mix2k(v0, w0) + smix(y) * K1 + z, mix2k(v1, w1) + x);
+}
+
+/* ---- ordered encodings (common/ordered_encoding.cc) ------------------- */
+
+/* ordered_encoding.cc:43-49 */
+uint64_t hdxo_encode_int64(int64_t x) {
+    uint64_t out = (uint64_t)x;
+    out += x >= 0 ? 0x8000000000000000ULL : (uint64_t)INT64_MIN;
+    return out;
+}
+
+/* ordered_encoding.cc:114-161 (ieee_double bitfields: common/ieee.h:107) */
+uint64_t hdxo_encode_double(double x) {
+    if (isinf(x)) return x > 0 ? 0xfff0000000000000ULL + 2 : 0;
+    if (isnan(x)) return 0xfff0000000000000ULL + 3;
+    if (x == 0) return 0x8000000000000000ULL + 1;
+    uint64_t bits;
+    memcpy(&bits, &x, 8);
+    uint64_t sign = (bits >> 63) ^ 1;
+    uint64_t ex = (bits >> 52) & 0x7ff;
+    uint64_t frac = bits & 0xfffffffffffffULL;
+    uint64_t shift = 2;
+    if (x < 0) {
+        ex ^= 0x7ff;
+        frac ^= 0xfffffffffffffULL;
+        shift = 1;
+    }
+    return ((sign << 63) | (ex << 52) | frac) + shift;
+}
+
+/* ---- timestamp (common/datatype_timestamp.cc:117-219) ----------------- */
+
+static const uint64_t TS_INTERVALS[6] = {60, 60, 24, 7, 4, 12};
+/* datatype_timestamp.cc:131-136: permutation per granularity */
+static const unsigned TS_ORDER[6][7] = {
+    {0, 1, 2, 3, 4, 5, 6}, /* second */
+    {1, 0, 2, 3, 4, 5, 6}, /* minute */
+    {2, 1, 0, 3, 4, 5, 6}, /* hour */
+    {3, 2, 1, 0, 4, 5, 6}, /* day */
+    {4, 3, 2, 1, 0, 5, 6}, /* week */
+    {5, 4, 3, 2, 1, 0, 6}, /* month */
+};
+
+uint64_t hdxo_hash_timestamp(uint32_t type, int64_t ts) {
+    uint64_t t = (uint64_t)ts; /* :141 unsigned view of the signed value */
+    if (type < T_TS_SECOND || type > T_TS_MONTH) return t; /* :174-176 default */
+    const unsigned* ord = TS_ORDER[type - T_TS_SECOND];
+    uint64_t x = (uint64_t)((double)t / 1000000.); /* :198 */
+    uint64_t digit[7];
+    for (int i = 0; i < 6; ++i) {
+        digit[i] = x % TS_INTERVALS[i];
+        x /= TS_INTERVALS[i];
+    }
+    digit[6] = x;
+    uint64_t y = UINT64_MAX, h = 0;
+    for (int i = 0; i < 6; ++i) {
+        y /= TS_INTERVALS[ord[i]];
+        h += digit[ord[i]] * y;
+    }
+    return h + digit[ord[6]];
+}
+
+/* ---- dispatch (common/hash.cc:34-46, datatype_info.cc:72-141,169-180) -- */
+
+static int known_type(uint32_t t) {
+    switch (t) {
+        case T_STRING: case T_INT64: case T_FLOAT: case T_DOCUMENT:
+        case T_LIST_STRING: case T_LIST_INT64: case T_LIST_FLOAT:
+        case T_SET_STRING: case T_SET_INT64: case T_SET_FLOAT:
+        case T_MAP_SS: case T_MAP_SI: case T_MAP_SF:
+        case T_MAP_IS: case T_MAP_II: case T_MAP_IF:
+        case T_MAP_FS: case T_MAP_FI: case T_MAP_FF:
+        case T_TS_SECOND: case T_TS_MINUTE: case T_TS_HOUR:
+        case T_TS_DAY: case T_TS_WEEK: case T_TS_MONTH:
+        case T_MACAROON:
+            return 1;
+        default:
+            return 0;
+    }
+}
+
+uint64_t hdxo_hash_value(uint32_t type, const uint8_t* p, size_t len, int* err) {
+    *err = 0;
+    if (!known_type(type)) { *err = 1; return 0; }
+    switch (type) {
+        case T_STRING: /* datatype_string.cc:181-185 */
+            return hdxo_cityhash64(p, len);
+        case T_INT64: { /* datatype_int64.cc:46-59,230-235 */
+            if (len != 0 && len != 8) { *err = 2; return 0; }
+            int64_t v = 0;
+            if (len) memcpy(&v, p, 8);
+            return hdxo_encode_int64(v);
+        }
+        case T_FLOAT: { /* datatype_float.cc:44-57,201-207 */
+            if (len != 0 && len != 8) { *err = 2; return 0; }
+            double v = 0;
+            if (len) memcpy(&v, p, 8);
+            return hdxo_encode_double(v);
+        }
+        case T_TS_SECOND: case T_TS_MINUTE: case T_TS_HOUR:
+        case T_TS_DAY: case T_TS_WEEK: case T_TS_MONTH: { /* datatype_timestamp.cc:43-56 */
+            if (len != 0 && len != 8) { *err = 2; return 0; }
+            int64_t v = 0;
+            if (len) memcpy(&v, p, 8);
+            return hdxo_hash_timestamp(type, v);
+        }
+        default: /* hashable() == false */
+            return 0;
+    }
+}
+
+/* ---- batch over the packed layout ------------------------------------- */
+
+struct job {
+    const uint32_t* types; uint32_t A; const uint8_t* blob;
+    const uint64_t* obj_base; const uint32_t* attr_len;
+    uint64_t lo, hi; uint64_t* coords; int err;
+};
+
+static void* run_job(void* arg) {
+    struct job* jb = (struct job*)arg;
+    for (uint64_t i = jb->lo; i < jb->hi; ++i) {
+        const uint8_t* p = jb->blob + jb->obj_base[i];
+        const uint32_t* lens = jb->attr_len + i * jb->A;
+        uint64_t* out = jb->coords + i * jb->A;
+        for (uint32_t j = 0; j < jb->A; ++j) {
+            int e;
+            out[j] = hdxo_hash_value(jb->types[j], p, lens[j], &e);
+            if (e && !jb->err) jb->err = e;
+            p += lens[j];
+        }
+    }
+    return NULL;
+}
+
+int hdxo_hash_batch(const uint32_t* types, uint32_t A, const uint8_t* blob,
+                    const uint64_t* obj_base, const uint32_t* attr_len,
+                    uint64_t n, uint64_t* coords, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    if ((uint64_t)nthreads > n) nthreads = n ? (int)n : 1;
+    struct job* jobs = (struct job*)calloc((size_t)nthreads, sizeof(struct job));
+    pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+    for (int t = 0; t < nthreads; ++t) {
+        jobs[t] = (struct job){types, A, blob, obj_base, attr_len,
+                               n * (uint64_t)t / nthreads, n * (uint64_t)(t + 1) / nthreads,
+                               coords, 0};
+    }
+    for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], NULL, run_job, &jobs[t]);
+    run_job(&jobs[0]);
+    int err = jobs[0].err;
+    for (int t = 1; t < nthreads; ++t) {
+        pthread_join(th[t], NULL);
+        if (!err) err = jobs[t].err;
+    }
+    free(jobs);
+    free(th);
+    return err;
+}

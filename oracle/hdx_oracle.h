@@ -1,0 +1,53 @@
+/*
+ * hdx_oracle.h — CPU restatement of HyperDex's attribute-hashing path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in hyperdex_amd/ may include, link or
+ * call this.  It is the parity checker for the HIP kernels (tests/,
+ * __graft_entry__.smoke()) and the timed CPU baseline in bench.py
+ * ("cpu_baseline.kind" = "port").
+ *
+ * Pinning:
+ *   - CityHash64 v1.1: every column-0 vector of the reference KAT
+ *     cityhash/test/city.cc:63-1265 (tests/golden/cityhash64_kat.json).
+ *   - ordered encodings: exact cases of common/test/ordered_encoding.cc:42-69
+ *     and, when oracle/_ref is built, 2^20+ random inputs against the
+ *     reference's own ordered_encoding.cc compiled unmodified.
+ *   - timestamp hash and whole-object hash: the reference-produced values
+ *     recorded in SURVEY.md §8c (survey-time reference build).
+ */
+#ifndef HDX_ORACLE_H
+#define HDX_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* CityHash v1.1 CityHash64 (reference cityhash/city.cc:361-397). */
+uint64_t hdxo_cityhash64(const uint8_t* s, size_t len);
+
+/* common/ordered_encoding.cc:43-49 */
+uint64_t hdxo_encode_int64(int64_t x);
+/* common/ordered_encoding.cc:114-161 */
+uint64_t hdxo_encode_double(double x);
+/* common/datatype_timestamp.cc:138-219; type = HYPERDATATYPE_TIMESTAMP_* */
+uint64_t hdxo_hash_timestamp(uint32_t type, int64_t ts);
+
+/* common/hash.cc:34-46.  *err: 0 ok, 1 unknown type (reference asserts),
+ * 2 bad size for int64/float/timestamp (reference asserts). */
+uint64_t hdxo_hash_value(uint32_t type, const uint8_t* p, size_t len, int* err);
+
+/* Whole batch in the packed layout of include/hdxhash.h:
+ *   attr i,j lives at blob + obj_base[i] + sum_{k<j} attr_len[i*A+k].
+ * Returns 0, or the first error code.  nthreads <= 1 runs on the caller. */
+int hdxo_hash_batch(const uint32_t* types, uint32_t A, const uint8_t* blob,
+                    const uint64_t* obj_base, const uint32_t* attr_len,
+                    uint64_t n, uint64_t* coords, int nthreads);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,90 @@
+"""ctypes view of oracle/liboracle.so (TEST INFRASTRUCTURE ONLY).
+
+The CPU restatement of the reference hashing path (oracle/hdx_oracle.c).
+Used as the parity checker and as bench.py's cpu_baseline ("port").
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+_REF = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE, "liboracle.so"])
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        u64, u32, i64, sz = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int64, ctypes.c_size_t
+        vp = ctypes.c_void_p
+        L.hdxo_cityhash64.argtypes = [vp, sz]
+        L.hdxo_cityhash64.restype = u64
+        L.hdxo_encode_int64.argtypes = [i64]
+        L.hdxo_encode_int64.restype = u64
+        L.hdxo_encode_double.argtypes = [ctypes.c_double]
+        L.hdxo_encode_double.restype = u64
+        L.hdxo_hash_timestamp.argtypes = [u32, i64]
+        L.hdxo_hash_timestamp.restype = u64
+        L.hdxo_hash_value.argtypes = [u32, vp, sz, ctypes.POINTER(ctypes.c_int)]
+        L.hdxo_hash_value.restype = u64
+        L.hdxo_hash_batch.argtypes = [vp, u32, vp, vp, vp, u64, vp, ctypes.c_int]
+        L.hdxo_hash_batch.restype = ctypes.c_int
+        _LIB = L
+    return _LIB
+
+
+def ref_lib():
+    """oracle/_ref/libref_ordered.so (reference ordered_encoding.cc), or None."""
+    global _REF
+    if _REF is None:
+        path = os.path.join(_HERE, "_ref", "libref_ordered.so")
+        if not os.path.exists(path):
+            return None
+        R = ctypes.CDLL(path)
+        R.ref_ordered_encode_int64.argtypes = [ctypes.c_int64]
+        R.ref_ordered_encode_int64.restype = ctypes.c_uint64
+        R.ref_ordered_encode_double.argtypes = [ctypes.c_double]
+        R.ref_ordered_encode_double.restype = ctypes.c_uint64
+        _REF = R
+    return _REF
+
+
+def cityhash64(data: bytes) -> int:
+    buf = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+    return lib().hdxo_cityhash64(buf, len(data))
+
+
+def hash_value(type_id: int, data: bytes):
+    """hash(hyperdatatype, slice) -> (u64, err)  (common/hash.cc:34-46)."""
+    buf = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+    err = ctypes.c_int(0)
+    h = lib().hdxo_hash_value(type_id, buf, len(data), ctypes.byref(err))
+    return h, err.value
+
+
+def hash_batch(types, blob, obj_base, attr_len, nthreads=1):
+    """Whole-batch oracle over the packed layout.  numpy in, numpy out."""
+    types = np.ascontiguousarray(types, dtype=np.uint32)
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    obj_base = np.ascontiguousarray(obj_base, dtype=np.uint64)
+    attr_len = np.ascontiguousarray(attr_len, dtype=np.uint32)
+    A = len(types)
+    n = len(obj_base)
+    assert attr_len.size == n * A
+    coords = np.zeros(n * A, dtype=np.uint64)
+    if blob.size == 0:
+        blob = np.zeros(1, dtype=np.uint8)
+    err = lib().hdxo_hash_batch(types.ctypes.data, A, blob.ctypes.data,
+                                obj_base.ctypes.data, attr_len.ctypes.data, n,
+                                coords.ctypes.data, nthreads)
+    return coords.reshape(n, A), err

@@ -1,0 +1,94 @@
+"""libhdxhash.so loads on any host and exports exactly what include/hdxhash.h
+declares.  Host-only checks here; no compute call needs (or may fake) a GPU."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import hyperdex_amd as hdx
+from hyperdex_amd import _lib, datatypes as dt
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    text = open(os.path.join(ROOT, "include", "hdxhash.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(hdx_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_matches_binding_table():
+    assert declared_symbols() == sorted(name for name, _, _ in _lib.SIGNATURES)
+
+
+def test_library_exports_every_declared_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH],
+                         capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (hdx_\w+)", out))
+    assert set(declared_symbols()) <= exported
+    # nothing else leaks out of the C-ABI (hidden visibility for internals)
+    assert {s for s in exported if s.startswith("hdx_")} == set(declared_symbols())
+    lib = hdx.lib()
+    for name in declared_symbols():
+        assert getattr(lib, name) is not None
+
+
+def test_version_and_abi():
+    assert hdx.lib().hdx_abi_version() == 1
+    assert b"gfx950" in hdx.lib().hdx_version()
+
+
+@pytest.mark.parametrize("t", dt.KNOWN)
+def test_known_types_accepted(t):
+    hdx.schema_check([dt.HYPERDATATYPE_STRING, t])
+
+
+@pytest.mark.parametrize("t", [dt.HYPERDATATYPE_GENERIC, dt.HYPERDATATYPE_TIMESTAMP_GENERIC,
+                               dt.HYPERDATATYPE_LIST_GENERIC, dt.HYPERDATATYPE_SET_GENERIC,
+                               dt.HYPERDATATYPE_MAP_GENERIC, dt.HYPERDATATYPE_MAP_STRING_KEYONLY,
+                               dt.HYPERDATATYPE_MAP_INT64_KEYONLY, dt.HYPERDATATYPE_MAP_FLOAT_KEYONLY,
+                               dt.HYPERDATATYPE_GARBAGE, 0, 12345])
+def test_unknown_types_rejected(t):
+    """datatype_info::lookup returns NULL -> reference asserts (hash.cc:38)."""
+    with pytest.raises(hdx.HdxError) as e:
+        hdx.schema_check([dt.HYPERDATATYPE_STRING, t])
+    assert e.value.status == _lib.HDX_E_BADTYPE
+
+
+def test_hashable_matches_reference():
+    for t in dt.KNOWN:
+        assert hdx.hashable(t) == (t in dt.HASHABLE), t
+    assert not hdx.hashable(dt.HYPERDATATYPE_GENERIC)
+
+
+def test_schema_limits():
+    with pytest.raises(hdx.HdxError) as e:
+        hdx.schema_check([])
+    assert e.value.status == _lib.HDX_E_INVALID
+    hdx.schema_check([dt.HYPERDATATYPE_STRING] * _lib.HDX_MAX_ATTRS)
+    with pytest.raises(hdx.HdxError):
+        hdx.schema_check([dt.HYPERDATATYPE_STRING] * (_lib.HDX_MAX_ATTRS + 1))
+
+
+def test_no_cpu_fallback_without_device():
+    """Without a GPU every compute entry point fails loudly with HDX_E_DEVICE."""
+    if hdx.lib().hdx_device_count() > 0:
+        pytest.skip("a device is present")
+    with pytest.raises(hdx.HdxError) as e:
+        hdx.hash(dt.HYPERDATATYPE_STRING, b"x")
+    assert e.value.status == _lib.HDX_E_DEVICE
+    with pytest.raises(hdx.HdxError) as e:
+        hdx.hash_batch_host([dt.HYPERDATATYPE_STRING], np.zeros(4, np.uint8),
+                            np.zeros(1, np.uint64), np.array([4], np.uint32))
+    assert e.value.status == _lib.HDX_E_DEVICE
+
+
+def test_product_does_not_reference_oracle():
+    """hyperdex_amd/ never imports or links the test oracle."""
+    for dirpath, _, files in os.walk(os.path.join(ROOT, "hyperdex_amd")):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h", "Makefile")):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in src.replace("no CPU", ""), f

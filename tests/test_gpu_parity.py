@@ -1,0 +1,269 @@
+"""GPU parity: the gfx950 kernels (through the C-ABI) vs the CPU oracle.
+
+Bit-exact equality on every coordinate: integer/byte work has no tolerance.
+Inputs: the reference KAT, the SURVEY §8c reference-produced values, seeded
+synthetic batches of every config at oracle-friendly sizes, edge cases (empty
+and ragged batches, wave boundaries, attribute-count extremes, gaps and
+shuffled object order, unaligned strings), and a full BASELINE-size batch
+checked by sampling + determinism.
+"""
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+
+import hyperdex_amd as hdx
+from hyperdex_amd import _lib, datatypes as dt, synth
+from kat_data import kat_array
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    assert torch.cuda.is_available()
+    return torch, torch.device("cuda", 0)
+
+
+def to_dev(torch, dev, blob, base, lens):
+    b = torch.from_numpy(np.ascontiguousarray(blob).view(np.uint8).copy()).to(dev)
+    o = torch.from_numpy(np.ascontiguousarray(base, np.uint64).view(np.int64).copy()).to(dev)
+    L = torch.from_numpy(np.ascontiguousarray(lens, np.uint32).view(np.int32).copy()).to(dev)
+    return b, o, L
+
+
+def gpu_hash(torch, dev, types, blob, base, lens, status=None):
+    if len(blob) == 0:
+        blob = np.zeros(1, np.uint8)
+    b, o, L = to_dev(torch, dev, blob, base, lens)
+    c = hdx.hash_batch(types, b, o, L, status=status)
+    torch.cuda.synchronize()
+    return c.cpu().numpy().view(np.uint64)
+
+
+def check_batch(oracle, torch, dev, types, blob, base, lens):
+    want, err = oracle.hash_batch(types, blob, base, lens)
+    assert err == 0
+    got = gpu_hash(torch, dev, types, blob, base, lens)
+    bad = np.argwhere(got != want)
+    assert bad.size == 0, "first mismatch at (obj, attr) %s: got %x want %x" % (
+        tuple(bad[0]), got[tuple(bad[0])], want[tuple(bad[0])])
+    return got
+
+
+def test_kat_on_gpu(oracle, torch_dev):
+    """All 300 reference CityHash64 vectors hashed in one device batch (A=1)."""
+    torch, dev = torch_dev
+    kat = json.load(open(os.path.join(GOLD, "cityhash64_kat.json")))["cases"]
+    data = kat_array()
+    base = np.array([c["offset"] for c in kat], np.uint64)
+    lens = np.array([c["len"] for c in kat], np.uint32)
+    got = gpu_hash(torch, dev, [dt.HYPERDATATYPE_STRING], data, base, lens)[:, 0]
+    want = np.array([int(c["cityhash64"], 16) for c in kat], np.uint64)
+    assert np.array_equal(got, want), np.nonzero(got != want)
+
+
+def _enc(kind, value):
+    if kind == "empty":
+        return b""
+    if kind == "bytes":
+        return value.encode()
+    if kind == "int64":
+        return struct.pack("<q", value)
+    return struct.pack("<Q", int(value, 16))
+
+
+def test_reference_values_per_object_api(torch_dev):
+    """hash(type, slice) and hash(schema, key, value, hs) through the C-ABI."""
+    rv = json.load(open(os.path.join(GOLD, "reference_values.json")))
+    for s in rv["scalars"]:
+        assert hdx.hash(s["type"], _enc(s["kind"], s["value"])) == int(s["hash"], 16), s
+    for o in rv["objects"]:
+        sc = dt.Schema.of(*o["types"])
+        hs = hdx.hash_object(sc, o["key"].encode(), [_enc(v["kind"], v["value"]) for v in o["values"]])
+        assert ["%016x" % h for h in hs] == o["hashes"]
+        assert hdx.hash_key(sc, o["key"].encode()) == int(o["hashes"][0], 16)
+
+
+@pytest.mark.parametrize("cfg,n", [("cfg1", 5000), ("cfg2", 5000), ("cfg3a", 3000), ("cfg3b", 4000),
+                                   ("mixed", 6000), ("wide", 500), ("keyonly_long", 700)])
+def test_configs_match_oracle(oracle, torch_dev, cfg, n):
+    torch, dev = torch_dev
+    types, blob, base, lens = synth.make_batch_host(cfg, n, seed=synth.SEED + n)
+    check_batch(oracle, torch, dev, types, blob, base, lens)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 63, 64, 65, 127, 129, 1000])
+def test_ragged_object_counts(oracle, torch_dev, n):
+    torch, dev = torch_dev
+    types, blob, base, lens = synth.make_batch_host("mixed", n, seed=1000 + n)
+    if n == 0:
+        b, o, L = to_dev(torch, dev, np.zeros(1, np.uint8), np.zeros(0, np.uint64),
+                         np.zeros(0, np.uint32))
+        c = hdx.hash_batch(types, b, o, L)
+        assert c.shape == (0, len(types))
+        return
+    check_batch(oracle, torch, dev, types, blob, base, lens)
+
+
+@pytest.mark.parametrize("A", [1, 2, 3, 5, 31, 32, 33, 63, 64, 65, 100, 128, 255, 256])
+def test_attribute_counts(oracle, torch_dev, A):
+    torch, dev = torch_dev
+    rules = [synth.Rule(dt.HYPERDATATYPE_STRING, synth.UNIFORM, 0, 80)] * A
+    types, blob, base, lens = synth.make_batch_host(rules, 150, seed=77 + A)
+    check_batch(oracle, torch, dev, types, blob, base, lens)
+
+
+def test_every_string_length_and_alignment(oracle, torch_dev):
+    """Lengths 0..520 at every byte alignment 0..15 (all CityHash regimes and
+    1..8 iterations of the 64-byte loop)."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(5)
+    lens = np.repeat(np.arange(521, dtype=np.uint32), 16)
+    align = np.tile(np.arange(16, dtype=np.uint64), 521)
+    stride = 544
+    base = np.arange(len(lens), dtype=np.uint64) * stride + align
+    blob = rng.integers(0, 256, int(base[-1]) + stride, dtype=np.uint8)
+    check_batch(oracle, torch, dev, [dt.HYPERDATATYPE_STRING], blob, base, lens)
+
+
+def test_gaps_and_shuffled_objects(oracle, torch_dev):
+    torch, dev = torch_dev
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 3000, seed=99)
+    n, A = len(base), len(types)
+    rng = np.random.default_rng(3)
+    perm = rng.permutation(n)
+    sizes = lens.reshape(n, A).astype(np.uint64).sum(axis=1)
+    gaps = rng.integers(0, 37, n).astype(np.uint64)
+    new_base = np.zeros(n, np.uint64)
+    pos = np.uint64(5)
+    out = np.zeros(int(sizes.sum() + gaps.sum()) + 64, np.uint8)
+    for k in perm:  # write objects in shuffled order with random gaps
+        pos += gaps[k]
+        new_base[k] = pos
+        out[int(pos):int(pos + sizes[k])] = blob[int(base[k]):int(base[k] + sizes[k])]
+        pos += sizes[k]
+    got = check_batch(oracle, torch, dev, types, out, new_base, lens)
+    want, _ = oracle.hash_batch(types, blob, base, lens)
+    assert np.array_equal(got, want)
+
+
+def test_float_and_int_specials(oracle, torch_dev):
+    torch, dev = torch_dev
+    vals = [0, 1 << 63, 0x7ff0000000000000, 0xfff0000000000000, 0x7ff8000000000000,
+            0xfff8000000000001, 0x7ff0000000000001, 0xfff0000000000001, 1, (1 << 63) | 1,
+            0x000fffffffffffff, 0x800fffffffffffff, 0x0010000000000000, 0x8010000000000000,
+            0x7fefffffffffffff, 0xffefffffffffffff, 0x3ff0000000000000, 0xbff0000000000000,
+            0x7fffffffffffffff, 0xffffffffffffffff]
+    types = [dt.HYPERDATATYPE_FLOAT, dt.HYPERDATATYPE_INT64] + list(dt.TIMESTAMPS)
+    A = len(types)
+    blob = np.frombuffer(b"".join(struct.pack("<Q", v) for v in vals for _ in range(A)), np.uint8)
+    base = np.arange(len(vals), dtype=np.uint64) * (8 * A)
+    lens = np.full(len(vals) * A, 8, np.uint32)
+    check_batch(oracle, torch, dev, types, blob, base, lens)
+
+
+def test_timestamps_random(oracle, torch_dev):
+    torch, dev = torch_dev
+    rng = np.random.default_rng(11)
+    n = 20000
+    ts = np.concatenate([rng.integers(-2**63, 2**63 - 1, n // 2, dtype=np.int64),
+                         rng.integers(0, 2**53, n // 2, dtype=np.int64)])
+    types = list(dt.TIMESTAMPS)
+    blob = np.repeat(ts.astype("<i8"), len(types)).view(np.uint8)
+    base = np.arange(n, dtype=np.uint64) * (8 * len(types))
+    lens = np.full(n * len(types), 8, np.uint32)
+    check_batch(oracle, torch, dev, types, blob, base, lens)
+
+
+def test_bad_size_sets_status(torch_dev):
+    torch, dev = torch_dev
+    types = [dt.HYPERDATATYPE_STRING, dt.HYPERDATATYPE_INT64]
+    blob = np.zeros(64, np.uint8)
+    base = np.array([0, 16], np.uint64)
+    lens = np.array([4, 8, 4, 5], np.uint32)  # object 1 attr 1 is 5 bytes
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    got = gpu_hash(torch, dev, types, blob, base, lens, status=status)
+    assert int(status.item()) == 1 << _lib.HDX_E_BADSIZE
+    assert got[1, 1] == 0
+    with pytest.raises(hdx.HdxError) as e:
+        hdx.hash_batch_host(types, blob, base, lens)
+    assert e.value.status == _lib.HDX_E_BADSIZE
+    with pytest.raises(hdx.HdxError) as e:
+        hdx.hash(dt.HYPERDATATYPE_FLOAT, b"\0" * 7)
+    assert e.value.status == _lib.HDX_E_BADSIZE
+
+
+def test_bad_type_rejected_before_launch(torch_dev):
+    torch, dev = torch_dev
+    b, o, L = to_dev(torch, dev, np.zeros(8, np.uint8), np.zeros(1, np.uint64),
+                     np.array([8], np.uint32))
+    with pytest.raises(hdx.HdxError) as e:
+        hdx.hash_batch([dt.HYPERDATATYPE_GENERIC], b, o, L)
+    assert e.value.status == _lib.HDX_E_BADTYPE
+
+
+def test_host_path_matches_device_path(oracle, torch_dev):
+    torch, dev = torch_dev
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 20000, seed=4)
+    want, _ = oracle.hash_batch(types, blob, base, lens)
+    assert np.array_equal(hdx.hash_batch_host(types, blob, base, lens), want)
+
+
+def test_host_path_multichunk(oracle, torch_dev):
+    """> 2 pipeline chunks (128 MiB each) through the two-stream host path."""
+    torch, dev = torch_dev
+    types, blob, base, lens = synth.make_batch_host("cfg3a", 300000, seed=8)  # ~326 MB
+    got = hdx.hash_batch_host(types, blob, base, lens)
+    idx = np.random.default_rng(0).choice(len(base), 3000, replace=False)
+    idx.sort()
+    sub_base = base[idx]
+    sub_lens = lens.reshape(len(base), -1)[idx].ravel()
+    want, _ = oracle.hash_batch(types, blob, sub_base, sub_lens)
+    assert np.array_equal(got[idx], want)
+
+
+def test_device_generator_matches_host_generator(torch_dev):
+    torch, dev = torch_dev
+    for cfg in ("cfg2", "cfg3b", "mixed"):
+        t1, b1, o1, L1 = synth.make_batch_host(cfg, 2000, seed=21, first=12345)
+        t2, b2, o2, L2 = synth.make_batch_device(cfg, 2000, seed=21, first=12345, device=dev)
+        assert np.array_equal(t1, t2)
+        assert np.array_equal(L1, L2.cpu().numpy().view(np.uint32))
+        assert np.array_equal(o1, o2.cpu().numpy().view(np.uint64))
+        assert np.array_equal(b1, b2.cpu().numpy())
+
+
+@pytest.mark.parametrize("cfg", ["cfg3a", "cfg3b"])
+def test_full_size_sampled(oracle, torch_dev, cfg):
+    """BASELINE size (10M objects, ~10.9 GB in HBM): sampled parity + determinism."""
+    torch, dev = torch_dev
+    n = 10_000_000
+    types, blob, base, lens = synth.make_batch_device(cfg, n, device=dev)
+    c1 = hdx.hash_batch(types, blob, base, lens)
+    c2 = hdx.hash_batch(types, blob, base, lens)
+    torch.cuda.synchronize()
+    assert torch.equal(c1, c2)
+    A = len(types)
+    idx = np.unique(np.concatenate([np.arange(64), n - 1 - np.arange(64),
+                                    np.random.default_rng(1).choice(n, 4000, replace=False)]))
+    ti = torch.from_numpy(idx).to(dev)
+    sb = base[ti].cpu().numpy().view(np.uint64)
+    sl = lens.view(n, A)[ti].cpu().numpy().view(np.uint32)
+    sizes = sl.astype(np.uint64).sum(axis=1)
+    # gather the sampled objects into a compact host blob
+    parts, nb, pos = [], np.zeros(len(idx), np.uint64), 0
+    for k in range(len(idx)):
+        parts.append(blob[int(sb[k]):int(sb[k] + sizes[k])].cpu().numpy())
+        nb[k] = pos
+        pos += int(sizes[k])
+    want, err = oracle.hash_batch(types, np.concatenate(parts), nb, sl.ravel())
+    assert err == 0
+    got = c1[ti].cpu().numpy().view(np.uint64)
+    assert np.array_equal(got, want)
+    del blob, base, lens, c1, c2
+    torch.cuda.empty_cache()
