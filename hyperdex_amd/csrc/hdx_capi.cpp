@@ -338,11 +338,9 @@ HDX_EXPORT hdx_status hdx_init(int device) {
 }
 
 HDX_EXPORT hdx_status hdx_sync(hdx_stream stream) {
+    hdx_status st = bind_device(-1);
+    if (st != HDX_OK) return st;
     hipStream_t s = (hipStream_t)stream;
-    if (!s) {
-        hdx_status st = thread_stream(&s);
-        if (st != HDX_OK) return st;
-    }
     HIP_TRY(hipStreamSynchronize(s));
     return HDX_OK;
 }
@@ -365,8 +363,7 @@ HDX_EXPORT hdx_status hdx_hash_batch_device(const uint32_t* types, uint32_t attr
     if (!blob || !obj_base || !attr_len || !coords)
         return fail(HDX_E_INVALID, "NULL device pointer");
     if ((st = bind_device(-1)) != HDX_OK) return st;
-    hipStream_t s = (hipStream_t)stream;
-    if (!s && (st = thread_stream(&s)) != HDX_OK) return st;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
     args.blob = blob;
     args.obj_base = obj_base;
     args.attr_len = attr_len;
@@ -476,7 +473,6 @@ HDX_EXPORT hdx_status hdx_synth_lengths(const hdx_synth_rule* rules, uint32_t at
     if (st != HDX_OK) return st;
     if ((st = bind_device(-1)) != HDX_OK) return st;
     hipStream_t s = (hipStream_t)stream;
-    if (!s && (st = thread_stream(&s)) != HDX_OK) return st;
     HIP_TRY(launch_synth_lengths(a, attr_len_dev, s));
     return HDX_OK;
 }
@@ -490,7 +486,6 @@ HDX_EXPORT hdx_status hdx_synth_fill(const hdx_synth_rule* rules, uint32_t attrs
     if (st != HDX_OK) return st;
     if ((st = bind_device(-1)) != HDX_OK) return st;
     hipStream_t s = (hipStream_t)stream;
-    if (!s && (st = thread_stream(&s)) != HDX_OK) return st;
     HIP_TRY(launch_synth_fill(a, obj_base_dev, attr_len_dev, blob_dev, bytes, s));
     return HDX_OK;
 }

@@ -37,8 +37,8 @@
  * exactly as in the reference (hash.cc:40-43).
  *
  * Threading: every entry point is thread-safe.  Device work is issued on the
- * caller's stream (batch API) or on a per-thread library stream (host and
- * per-object API).  There is no CPU implementation behind any entry point:
+ * caller's stream (batch API; NULL = null stream) or on per-thread library
+ * streams (host-resident and per-object API).  There is no CPU implementation behind any entry point:
  * without a usable gfx950 device every compute call returns HDX_E_DEVICE.
  */
 #ifndef HDXHASH_H
@@ -63,7 +63,7 @@ typedef enum hdx_status {
     HDX_E_NOMEM = 5        /* device or pinned allocation failed */
 } hdx_status;
 
-/* An opaque hipStream_t.  NULL means the library's per-thread stream. */
+/* An opaque hipStream_t.  NULL is the HIP null (default) stream. */
 typedef void* hdx_stream;
 
 /* ---- library state ---------------------------------------------------- */
@@ -79,7 +79,7 @@ hdx_status hdx_init(int device);
 int hdx_device_count(void);
 /* Message for the last non-OK status returned on this thread. */
 const char* hdx_last_error(void);
-/* hipStreamSynchronize on `stream` (NULL: this thread's library stream). */
+/* hipStreamSynchronize on `stream` (NULL: the null stream). */
 hdx_status hdx_sync(hdx_stream stream);
 
 /* ---- schema ------------------------------------------------------------ */
