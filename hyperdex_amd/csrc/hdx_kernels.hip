@@ -9,12 +9,19 @@
 //   * one wave64 owns 64 consecutive objects and walks their 64*A attributes
 //     in A rounds of 64 consecutive (object, attr) slots, so every attr_len
 //     load and every coords store is one coalesced 256 B / 512 B access;
-//   * a lane's byte offset inside its object is a wave-wide segmented prefix
-//     sum of the round's lengths (DPP scan) plus a carry from the previous round;
+//   * a lane's byte offset inside its object is a wave-wide prefix sum of the
+//     round's lengths plus a carry from the previous round;
 //   * each lane hashes one attribute: type dispatch through an LDS code table,
 //     strings read as 16 B vectors straight from HBM.
+// Software pipelining (template flags, A/B-able through launch_hash_batch_variant):
+//   PF_LEN  — round r+1's lengths are loaded while round r is hashed;
+//   BASE_RF — the wave's 64 obj_base values live in one VGPR (lane l = object
+//             o0+l) and are fetched per round by ds_bpermute, not by a load;
+//   PF_STR  — round r+1's first string block (up to 64 B, regime-dependent)
+//             is loaded before round r is hashed.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "hdx_device_hash.h"
 #include "hdx_internal.h"
@@ -31,6 +38,12 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v, int lane) {
     return v;
 }
 
+__device__ __forceinline__ uint64_t hash_numeric(uint32_t code, uint64_t bits) {
+    if (code == CODE_INT64) return encode_int64(bits);
+    if (code == CODE_FLOAT) return encode_double(bits);
+    return hash_timestamp(code - CODE_TS_SECOND, bits);
+}
+
 __device__ __forceinline__ uint64_t hash_attr(uint32_t code, const uint8_t* p, uint32_t len,
                                               bool& bad) {
     if (code == CODE_STRING) return cityhash64(p, len);
@@ -43,11 +56,74 @@ __device__ __forceinline__ uint64_t hash_attr(uint32_t code, const uint8_t* p, u
         bad = true;
         return 0;
     }
-    if (code == CODE_INT64) return encode_int64(bits);
-    if (code == CODE_FLOAT) return encode_double(bits);
-    return hash_timestamp(code - CODE_TS_SECOND, bits);
+    return hash_numeric(code, bits);
 }
 
+// Prefetched first block of a string attribute (PF_STR):
+//   17..32 B: v0 = s[0,16),   v3 = s[n-16,n)
+//   33..64 B: v0..v1 = s[0,32), v2..v3 = s[n-32,n)
+//   > 64 B  : v0..v3 = s[n-64,n) (the tail block the long path starts with)
+//   <= 16 B and non-strings load at use.
+struct StrBlock {
+    u64x2 v0, v1, v2, v3;
+};
+
+__device__ __forceinline__ void prefetch_block(uint32_t code, const uint8_t* s, uint32_t n, StrBlock& b) {
+    if (code != CODE_STRING || n <= 16) return;
+    if (n > 64) {
+        b.v0 = ld16(s + n - 64);
+        b.v1 = ld16(s + n - 48);
+        b.v2 = ld16(s + n - 32);
+        b.v3 = ld16(s + n - 16);
+        return;
+    }
+    b.v0 = ld16(s);
+    b.v3 = ld16(s + n - 16);
+    if (n > 32) {
+        b.v1 = ld16(s + 16);
+        b.v2 = ld16(s + n - 32);
+    }
+}
+
+// city_gt64 with the tail block already in registers.
+__device__ __forceinline__ uint64_t city_gt64_tail(const uint8_t* s, uint32_t n, const StrBlock& t) {
+    const u64x2 e0 = t.v0, e1 = t.v1, e2 = t.v2, e3 = t.v3;
+    uint64_t x = e1.y;
+    uint64_t y = e3.x + e0.y;
+    uint64_t z = mix16(e1.x + n, e2.y, KMUL);
+    uint64_t v0, v1, w0, w1;
+    weak32(e0.x, e0.y, e1.x, e1.y, n, z, v0, v1);
+    weak32(e2.x, e2.y, e3.x, e3.y, y + K1, x, w0, w1);
+    x = x * K1 + ld8(s);
+    uint32_t blocks = (n - 1) >> 6;
+    for (uint32_t k = 0; k < blocks; ++k, s += 64) {
+        const u64x2 b0 = ld16(s), b1 = ld16(s + 16), b2 = ld16(s + 32), b3 = ld16(s + 48);
+        x = ror(x + y + v0 + b0.y, 37) * K1;
+        y = ror(y + v1 + b3.x, 42) * K1;
+        x ^= w1;
+        y += v0 + b2.y;
+        z = ror(z + w0, 33) * K1;
+        uint64_t nv0, nv1, nw0, nw1;
+        weak32(b0.x, b0.y, b1.x, b1.y, v1 * K1, x + w0, nv0, nv1);
+        weak32(b2.x, b2.y, b3.x, b3.y, z + w1, y + b1.x, nw0, nw1);
+        v0 = nv0; v1 = nv1; w0 = nw0; w1 = nw1;
+        uint64_t tt = z; z = x; x = tt;
+    }
+    return mix16(mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z, mix16(v1, w1, KMUL) + x, KMUL);
+}
+
+__device__ __forceinline__ uint64_t hash_attr_pf(uint32_t code, const uint8_t* p, uint32_t n,
+                                                 const StrBlock& b, bool& bad) {
+    if (code == CODE_STRING) {
+        if (n <= 16) return city_le16(p, n);
+        if (n <= 32) return city_17to32(b.v0, b.v3, n);
+        if (n <= 64) return city_33to64(b.v0, b.v1, b.v2, b.v3, n);
+        return city_gt64_tail(p, n, b);
+    }
+    return hash_attr(code, p, n, bad);
+}
+
+template <bool PF_LEN, bool BASE_RF, bool PF_STR>
 __global__ void __launch_bounds__(256)
 hash_batch_kernel(const BatchArgs args) {
     __shared__ uint8_t codes[HDX_MAX_ATTRS];
@@ -60,49 +136,138 @@ hash_batch_kernel(const BatchArgs args) {
     if (o0 >= args.n) return;
     const uint32_t nobj = (uint32_t)min<uint64_t>(64, args.n - o0);
     const uint32_t A = args.A;
-    const uint32_t rounds = A;  // 64*A slots, 64 per round
-
-    // slot q = 64*r + lane  ->  (object il = q / A, attribute j = q % A)
-    uint32_t il = (uint32_t)lane / A;
-    uint32_t j = (uint32_t)lane % A;
     const uint32_t qA = 64 / A, rA = 64 % A;
 
     const uint32_t* lens = args.attr_len + o0 * A;
     uint64_t* out = args.coords + o0 * A;
+    const uint64_t* bases = args.obj_base + o0;
+    uint64_t my_base = 0;
+    if (BASE_RF) my_base = (uint32_t)lane < nobj ? bases[lane] : 0;
+
+    // slot q = 64*r + lane  ->  (object il = q / A, attribute j = q % A)
+    uint32_t il = (uint32_t)lane / A;
+    uint32_t j = (uint32_t)lane % A;
     uint32_t carry = 0;
     bool bad = false;
 
-    for (uint32_t r = 0; r < rounds; ++r) {
-        const uint32_t q = r * 64 + lane;
-        const bool valid = il < nobj;
-        const uint32_t L = valid ? lens[q] : 0;
+    // round state: L, offset, pointer, code (+ prefetched block)
+    auto load_len = [&](uint32_t r, uint32_t il_, uint32_t) -> uint32_t {
+        return il_ < nobj ? lens[r * 64 + lane] : 0u;
+    };
+    auto locate = [&](uint32_t L, uint32_t il_, uint32_t j_, uint32_t& carry_) -> const uint8_t* {
         const uint32_t S = wave_inclusive_scan(L, lane);
         const uint32_t Sx = S - L;
-        const int head = lane - (int)j;  // lane holding this object's attr 0, if in this round
+        const int head = lane - (int)j_;
         const uint32_t head_sx = __shfl(Sx, head < 0 ? 0 : head, 64);
-        const uint32_t off = head >= 0 ? Sx - head_sx : carry + Sx;
-        carry = __shfl(off + L, 63, 64);
+        const uint32_t off = head >= 0 ? Sx - head_sx : carry_ + Sx;
+        carry_ = __shfl(off + L, 63, 64);
+        uint64_t base;
+        if (BASE_RF) {
+            const int src = il_ < 64 ? (int)il_ : 0;
+            const uint32_t lo = __shfl((uint32_t)my_base, src, 64);
+            const uint32_t hi = __shfl((uint32_t)(my_base >> 32), src, 64);
+            base = ((uint64_t)hi << 32) | lo;
+        } else {
+            base = il_ < nobj ? bases[il_] : 0;
+        }
+        return args.blob + base + off;
+    };
+    auto advance = [&](uint32_t& il_, uint32_t& j_) {
+        j_ += rA;
+        il_ += qA;
+        if (j_ >= A) {
+            j_ -= A;
+            ++il_;
+        }
+    };
+
+    uint32_t L = load_len(0, il, j);
+    const uint8_t* p = locate(L, il, j, carry);
+    uint32_t code = codes[j];
+    StrBlock blk;
+    if (PF_STR && il < nobj) prefetch_block(code, p, L, blk);
+    uint32_t Lnext = 0;
+    uint32_t il_n = il, j_n = j;
+    advance(il_n, j_n);
+    if (PF_LEN && A > 1) Lnext = load_len(1, il_n, j_n);
+
+    for (uint32_t r = 0; r < A; ++r) {
+        const bool valid = il < nobj;
+        // next round's lengths / address / first block, issued before this round's hash
+        uint32_t Ln = 0, code_n = 0;
+        const uint8_t* pn = nullptr;
+        StrBlock blk_n;
+        const bool more = r + 1 < A;
+        if (more) {
+            Ln = PF_LEN ? Lnext : 0;
+            if (PF_STR) {
+                if (!PF_LEN) Ln = load_len(r + 1, il_n, j_n);
+                pn = locate(Ln, il_n, j_n, carry);
+                code_n = codes[j_n];
+                if (il_n < nobj) prefetch_block(code_n, pn, Ln, blk_n);
+            }
+            if (PF_LEN && r + 2 < A) {
+                uint32_t il2 = il_n, j2 = j_n;
+                advance(il2, j2);
+                Lnext = load_len(r + 2, il2, j2);
+            }
+        }
         if (valid) {
-            const uint8_t* p = args.blob + args.obj_base[o0 + il] + off;
-            out[q] = hash_attr(codes[j], p, L, bad);
+            const uint64_t h = PF_STR ? hash_attr_pf(code, p, L, blk, bad) : hash_attr(code, p, L, bad);
+            out[r * 64 + lane] = h;
         }
-        j += rA;
-        il += qA;
-        if (j >= A) {
-            j -= A;
-            ++il;
+        if (!more) break;
+        // rotate round state
+        if (PF_STR) {
+            p = pn;
+            code = code_n;
+            blk = blk_n;
+        } else {
+            if (!PF_LEN) Ln = load_len(r + 1, il_n, j_n);
+            p = locate(Ln, il_n, j_n, carry);
+            code = codes[j_n];
         }
+        L = Ln;
+        il = il_n;
+        j = j_n;
+        advance(il_n, j_n);
     }
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream) {
+template <bool A_, bool B_, bool C_>
+static hipError_t launch_t(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n + 63) / 64;
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(hash_batch_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_batch_kernel<A_, B_, C_>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
     return hipGetLastError();
+}
+
+hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, int variant) {
+    switch (variant) {
+        case 0: return launch_t<false, false, false>(args, stream);
+        case 1: return launch_t<true, false, false>(args, stream);
+        case 2: return launch_t<true, true, false>(args, stream);
+        case 3: return launch_t<true, true, true>(args, stream);
+        case 4: return launch_t<false, true, true>(args, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+static constexpr int kDefaultVariant = 3;
+
+int hash_variant() {
+    static const int v = [] {
+        const char* e = getenv("HDX_KERNEL_VARIANT");
+        return e && *e ? atoi(e) : kDefaultVariant;
+    }();
+    return v;
+}
+
+hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream) {
+    return launch_hash_batch_variant(args, stream, hash_variant());
 }
 
 }  // namespace hdx
