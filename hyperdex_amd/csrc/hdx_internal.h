@@ -35,7 +35,8 @@ struct BatchArgs {
 
 hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream);
 // Kernel variants (hdx_kernels.hip): 0 plain, 1 +length prefetch, 2 +obj_base in
-// registers, 3 +string-block prefetch, 4 = 3 without length prefetch.
+// registers, 3 +string-block prefetch, 4 = 3 without length prefetch, 5/6 = 2/3 with
+// non-temporal coordinate stores.
 hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, int variant);
 // The variant launch_hash_batch uses: HDX_KERNEL_VARIANT (tuning knob) or the default.
 int hash_variant();

@@ -18,7 +18,8 @@
 //   BASE_RF — the wave's 64 obj_base values live in one VGPR (lane l = object
 //             o0+l) and are fetched per round by ds_bpermute, not by a load;
 //   PF_STR  — round r+1's first string block (up to 64 B, regime-dependent)
-//             is loaded before round r is hashed.
+//             is loaded before round r is hashed;
+//   NT_STORE — coordinates stored with the non-temporal hint.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -123,7 +124,7 @@ __device__ __forceinline__ uint64_t hash_attr_pf(uint32_t code, const uint8_t* p
     return hash_attr(code, p, n, bad);
 }
 
-template <bool PF_LEN, bool BASE_RF, bool PF_STR>
+template <bool PF_LEN, bool BASE_RF, bool PF_STR, bool NT_STORE>
 __global__ void __launch_bounds__(256)
 hash_batch_kernel(const BatchArgs args) {
     __shared__ uint8_t codes[HDX_MAX_ATTRS];
@@ -214,7 +215,8 @@ hash_batch_kernel(const BatchArgs args) {
         }
         if (valid) {
             const uint64_t h = PF_STR ? hash_attr_pf(code, p, L, blk, bad) : hash_attr(code, p, L, bad);
-            out[r * 64 + lane] = h;
+            if (NT_STORE) __builtin_nontemporal_store(h, out + r * 64 + lane);
+            else out[r * 64 + lane] = h;
         }
         if (!more) break;
         // rotate round state
@@ -235,13 +237,13 @@ hash_batch_kernel(const BatchArgs args) {
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <bool A_, bool B_, bool C_>
+template <bool A_, bool B_, bool C_, bool D_ = false>
 static hipError_t launch_t(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n + 63) / 64;
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_batch_kernel<A_, B_, C_>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_batch_kernel<A_, B_, C_, D_>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
     return hipGetLastError();
 }
 
@@ -252,6 +254,8 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 2: return launch_t<true, true, false>(args, stream);
         case 3: return launch_t<true, true, true>(args, stream);
         case 4: return launch_t<false, true, true>(args, stream);
+        case 5: return launch_t<true, true, false, true>(args, stream);
+        case 6: return launch_t<true, true, true, true>(args, stream);
         default: return hipErrorInvalidValue;
     }
 }

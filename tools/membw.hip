@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
 #include <vector>
 
@@ -82,6 +83,57 @@ __global__ void __launch_bounds__(256) k_stride64_lds(const u32x4* p, size_t chu
     if (x == 0x12345678u) out[0] = x;
 }
 
+
+// read 64 B/lane + 8 B coordinate per lane, stored non-temporally
+__global__ void __launch_bounds__(256) k_stride64_w8nt(const u32x4* p, size_t chunks, uint64_t* out) {
+    const int lane = threadIdx.x & 63;
+    size_t w = blockIdx.x * 4ull + (threadIdx.x >> 6);
+    if (w >= chunks) return;
+    const u32x4* c = p + w * 256 + lane * 4;
+    u32x4 a = c[0] ^ c[1] ^ c[2] ^ c[3];
+    __builtin_nontemporal_store(((uint64_t)(a.x ^ a.y) << 32) | (a.z ^ a.w), out + w * 64 + lane);
+}
+
+// each wave walks R consecutive 4 KiB chunks (like A rounds of one hash wave),
+// keeping its R coordinate vectors in registers and storing them at the end
+template <int R, bool NT>
+__global__ void __launch_bounds__(256) k_rounds_w8(const u32x4* p, size_t chunks, uint64_t* out) {
+    const int lane = threadIdx.x & 63;
+    size_t w0 = (blockIdx.x * 4ull + (threadIdx.x >> 6)) * R;
+    if (w0 >= chunks) return;
+    uint64_t acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const u32x4* c = p + (w0 + r) * 256 + lane * 4;
+        u32x4 a = (w0 + r < chunks) ? (c[0] ^ c[1] ^ c[2] ^ c[3]) : u32x4{0, 0, 0, 0};
+        acc[r] = ((uint64_t)(a.x ^ a.y) << 32) | (a.z ^ a.w);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+        if (w0 + r < chunks) {
+            if (NT) __builtin_nontemporal_store(acc[r], out + (w0 + r) * 64 + lane);
+            else out[(w0 + r) * 64 + lane] = acc[r];
+        }
+}
+
+// the hash kernel's exact traffic without the hash: per round a coalesced u32
+// length load, then 64 B per lane, then an 8 B store; R rounds per wave
+template <int R, bool NT>
+__global__ void __launch_bounds__(256) k_hashshape(const u32x4* p, const uint32_t* lens, size_t chunks, uint64_t* out) {
+    const int lane = threadIdx.x & 63;
+    size_t w0 = (blockIdx.x * 4ull + (threadIdx.x >> 6)) * R;
+    for (int r = 0; r < R; ++r) {
+        size_t w = w0 + r;
+        if (w >= chunks) return;
+        uint32_t L = lens[w * 64 + lane];
+        const u32x4* c = p + w * 256 + lane * 4 + (L >> 31);
+        u32x4 a = c[0] ^ c[1] ^ c[2] ^ c[3];
+        uint64_t h = ((uint64_t)(a.x ^ a.y) << 32) | (a.z ^ a.w) ^ L;
+        if (NT) __builtin_nontemporal_store(h, out + w * 64 + lane);
+        else out[w * 64 + lane] = h;
+    }
+}
+
 // grid-stride streaming read, 2048 blocks, 4 x 16 B in flight per lane
 __global__ void __launch_bounds__(256) k_stream(const u32x4* p, size_t n16, uint32_t* out) {
     u32x4 a = {0, 0, 0, 0};
@@ -147,6 +199,24 @@ int main(int argc, char** argv) {
     timeit("stride64_lds_wave4k", bytes, reps, [&] { k_stride64_lds<<<blocks, 256>>>(p, chunks, out); });
     timeit("stride64_w8_wave4k", bytes + chunks * 64 * 8.0, reps,
            [&] { k_stride64_w8<<<blocks, 256>>>(p, chunks, coords); });
+
+    timeit("stride64_w8nt_wave4k", bytes + chunks * 64 * 8.0, reps,
+           [&] { k_stride64_w8nt<<<blocks, 256>>>(p, chunks, coords); });
+    {
+        const unsigned b17 = (unsigned)((chunks + 4 * 17 - 1) / (4 * 17));
+        timeit("rounds17_w8_deferred", bytes + chunks * 64 * 8.0, reps,
+               [&] { k_rounds_w8<17, false><<<b17, 256>>>(p, chunks, coords); });
+        timeit("rounds17_w8nt_deferred", bytes + chunks * 64 * 8.0, reps,
+               [&] { k_rounds_w8<17, true><<<b17, 256>>>(p, chunks, coords); });
+        uint32_t* lens;
+        CK(hipMalloc(&lens, chunks * 64 * 4));
+        CK(hipMemset(lens, 0, chunks * 64 * 4));
+        timeit("hashshape17_plain", bytes + chunks * 64 * 12.0, reps,
+               [&] { k_hashshape<17, false><<<b17, 256>>>(p, lens, chunks, coords); });
+        timeit("hashshape17_nt", bytes + chunks * 64 * 12.0, reps,
+               [&] { k_hashshape<17, true><<<b17, 256>>>(p, lens, chunks, coords); });
+        CK(hipFree(lens));
+    }
     for (unsigned g : {1024u, 2048u, 4096u, 8192u})
         timeit(g == 1024 ? "stream_gs1024" : g == 2048 ? "stream_gs2048" : g == 4096 ? "stream_gs4096" : "stream_gs8192",
                bytes, reps, [&] { k_stream<<<g, 256>>>(p, n16, out); });
