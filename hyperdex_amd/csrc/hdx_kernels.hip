@@ -237,6 +237,283 @@ hash_batch_kernel(const BatchArgs args) {
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
+// ===========================================================================
+// Software-pipelined kernel (variants 7/8).
+//
+// Every lane issues exactly four 16-byte loads per round, unconditionally, at
+// per-lane addresses chosen by the attribute's regime (unused slots point at
+// a 64-byte zero pad), so the load stream is straight-line code and the
+// compiler's counted s_waitcnt lets round r+1's bytes and round r+2's lengths
+// be in flight while round r is hashed:
+//   string  > 64 B : s[n-64,n) in four pieces (the tail block CityHash starts with)
+//   string 33..64 B: s[0,32) and s[n-32,n)
+//   string 16..32 B: s[0,16) and s[n-16,n)
+//   string  1..15 B, int64/float/timestamp: the aligned 16-byte chunks holding
+//                    the first and last byte — a load never leaves the pages
+//                    the value lives in, so short values at the very end of a
+//                    buffer are read safely — then a funnel shift (v_alignbyte)
+//                    recovers the value's bytes in registers.
+// ===========================================================================
+
+__device__ __attribute__((aligned(64))) uint8_t g_zero_pad[64];
+
+// 16-byte load through an explicit global (addrspace 1) pointer at any
+// alignment: keeps the access a global_load_dwordx4 (never flat_, whose
+// out-of-order completion would force full vmcnt/lgkmcnt drains).
+typedef u64x2 __attribute__((aligned(1))) u64x2_u;
+typedef const __attribute__((address_space(1))) u64x2_u* gvec_ptr;
+__device__ __forceinline__ u64x2 gld16(const uint8_t* p) { return *(gvec_ptr)p; }
+
+struct Blk {
+    u64x2 v0, v1, v2, v3;
+};
+
+__device__ __forceinline__ Blk issue_block(uint32_t code, const uint8_t* p, uint32_t n) {
+    const uint8_t* D = g_zero_pad;
+    const bool str = code == CODE_STRING;
+    const bool shortv = (str && n > 0 && n < 16) || (code >= CODE_INT64 && n == 8);
+    const uint8_t* lo = p - ((uintptr_t)p & 15);  // pointer arithmetic keeps provenance
+    const uint8_t* hi = (p + n - 1) - ((uintptr_t)(p + n - 1) & 15);
+    const bool g64 = str && n > 64, g32 = str && n > 32 && n <= 64, g16 = str && n >= 16 && n <= 32;
+    const uint8_t* a0 = g64 ? p + n - 64 : (g32 || g16) ? p : shortv ? lo : D;
+    const uint8_t* a1 = g64 ? p + n - 48 : g32 ? p + 16 : g16 ? p + n - 16 : shortv ? hi : D;
+    const uint8_t* a2 = g64 || g32 ? p + n - 32 : D;
+    const uint8_t* a3 = g64 || g32 ? p + n - 16 : D;
+    Blk b;
+    b.v0 = gld16(a0);
+    b.v1 = gld16(a1);
+    b.v2 = gld16(a2);
+    b.v3 = gld16(a3);
+    return b;
+}
+
+__device__ __forceinline__ uint32_t dw(const u64x2& v, int k) {
+    return (uint32_t)((k & 2 ? v.y : v.x) >> (32 * (k & 1)));
+}
+__device__ __forceinline__ uint32_t pick4(uint32_t q, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    return q == 0 ? a : q == 1 ? b : q == 2 ? c : d;
+}
+
+// Bytes [sh, sh+16) of the 32-byte concatenation c0 || c1 (sh in 0..15).
+__device__ __forceinline__ u64x2 window16(const u64x2& c0, const u64x2& c1, uint32_t sh) {
+    const uint32_t d0 = dw(c0, 0), d1 = dw(c0, 1), d2 = dw(c0, 2), d3 = dw(c0, 3);
+    const uint32_t d4 = dw(c1, 0), d5 = dw(c1, 1), d6 = dw(c1, 2), d7 = dw(c1, 3);
+    const uint32_t q = sh >> 2, r = sh & 3;
+    const uint32_t e0 = pick4(q, d0, d1, d2, d3), e1 = pick4(q, d1, d2, d3, d4);
+    const uint32_t e2 = pick4(q, d2, d3, d4, d5), e3 = pick4(q, d3, d4, d5, d6);
+    const uint32_t e4 = pick4(q, d4, d5, d6, d7);
+    const uint32_t o0 = __builtin_amdgcn_alignbyte(e1, e0, r), o1 = __builtin_amdgcn_alignbyte(e2, e1, r);
+    const uint32_t o2 = __builtin_amdgcn_alignbyte(e3, e2, r), o3 = __builtin_amdgcn_alignbyte(e4, e3, r);
+    u64x2 w;
+    w.x = ((uint64_t)o1 << 32) | o0;
+    w.y = ((uint64_t)o3 << 32) | o2;
+    return w;
+}
+
+// Bytes [sh, sh+8) of c0 || c1.
+__device__ __forceinline__ uint64_t window8(const u64x2& c0, const u64x2& c1, uint32_t sh) {
+    const uint32_t d0 = dw(c0, 0), d1 = dw(c0, 1), d2 = dw(c0, 2), d3 = dw(c0, 3);
+    const uint32_t d4 = dw(c1, 0), d5 = dw(c1, 1);
+    const uint32_t q = sh >> 2, r = sh & 3;
+    const uint32_t e0 = pick4(q, d0, d1, d2, d3), e1 = pick4(q, d1, d2, d3, d4);
+    const uint32_t e2 = pick4(q, d2, d3, d4, d5);
+    return ((uint64_t)__builtin_amdgcn_alignbyte(e2, e1, r) << 32) | __builtin_amdgcn_alignbyte(e1, e0, r);
+}
+
+// city.cc:278-301 with the (up to) 16 string bytes in registers.
+__device__ __forceinline__ uint64_t city_le16_reg(const u64x2& w, uint32_t n) {
+    const uint64_t mul = K2 + 2ull * n;
+    const uint32_t d0 = (uint32_t)w.x, d1 = (uint32_t)(w.x >> 32);
+    const uint32_t d2 = (uint32_t)w.y, d3 = (uint32_t)(w.y >> 32);
+    if (n >= 8) {
+        // b = bytes [n-8, n): shift by t = n-8 in 0..8
+        const uint32_t t = n - 8, q = t >> 2, r = t & 3;
+        const uint32_t e0 = q == 0 ? d0 : q == 1 ? d1 : d2;
+        const uint32_t e1 = q == 0 ? d1 : q == 1 ? d2 : d3;
+        const uint32_t e2 = q == 0 ? d2 : d3;
+        const uint64_t b = ((uint64_t)__builtin_amdgcn_alignbyte(e2, e1, r) << 32) |
+                           __builtin_amdgcn_alignbyte(e1, e0, r);
+        const uint64_t a = w.x + K2;
+        const uint64_t c = ror(b, 37) * mul + a;
+        const uint64_t d = (ror(a, 25) + b) * mul;
+        return mix16(c, d, mul);
+    }
+    if (n >= 4) {
+        const uint64_t a = d0;
+        const uint32_t b = __builtin_amdgcn_alignbyte(d1, d0, n - 4);
+        return mix16(n + (a << 3), b, mul);
+    }
+    if (n > 0) {
+        const uint32_t y = (d0 & 0xff) + (((d0 >> (8 * (n >> 1))) & 0xff) << 8);
+        const uint32_t z = n + (((d0 >> (8 * (n - 1))) & 0xff) << 2);
+        return shiftmix((uint64_t)y * K2 ^ (uint64_t)z * K0) * K2;
+    }
+    return K2;
+}
+
+// city.cc:361-397 for n > 64 with the tail block in registers; the first
+// 64-byte block is loaded up front (its first word is Fetch64(s) of :380).
+__device__ __forceinline__ uint64_t city_gt64_reg(const uint8_t* s, uint32_t n, const Blk& t) {
+    const u64x2 e0 = t.v0, e1 = t.v1, e2 = t.v2, e3 = t.v3;
+    uint64_t x = e1.y;
+    uint64_t y = e3.x + e0.y;
+    uint64_t z = mix16(e1.x + n, e2.y, KMUL);
+    uint64_t v0, v1, w0, w1;
+    weak32(e0.x, e0.y, e1.x, e1.y, n, z, v0, v1);
+    weak32(e2.x, e2.y, e3.x, e3.y, y + K1, x, w0, w1);
+    u64x2 b0 = gld16(s), b1 = gld16(s + 16), b2 = gld16(s + 32), b3 = gld16(s + 48);
+    x = x * K1 + b0.x;
+    const uint32_t blocks = (n - 1) >> 6;
+    for (uint32_t k = 0;;) {
+        x = ror(x + y + v0 + b0.y, 37) * K1;
+        y = ror(y + v1 + b3.x, 42) * K1;
+        x ^= w1;
+        y += v0 + b2.y;
+        z = ror(z + w0, 33) * K1;
+        uint64_t nv0, nv1, nw0, nw1;
+        weak32(b0.x, b0.y, b1.x, b1.y, v1 * K1, x + w0, nv0, nv1);
+        weak32(b2.x, b2.y, b3.x, b3.y, z + w1, y + b1.x, nw0, nw1);
+        v0 = nv0; v1 = nv1; w0 = nw0; w1 = nw1;
+        const uint64_t tt = z; z = x; x = tt;
+        if (++k == blocks) break;
+        s += 64;
+        b0 = gld16(s); b1 = gld16(s + 16); b2 = gld16(s + 32); b3 = gld16(s + 48);
+    }
+    return mix16(mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z, mix16(v1, w1, KMUL) + x, KMUL);
+}
+
+__device__ __forceinline__ uint64_t hash_blk(uint32_t code, const uint8_t* p, uint32_t n, const Blk& b,
+                                             bool& bad) {
+    const uint32_t sh = (uint32_t)(uintptr_t)p & 15;
+    if (code == CODE_STRING) {
+        if (n > 64) return city_gt64_reg(p, n, b);
+        if (n > 32) return city_33to64(b.v0, b.v1, b.v2, b.v3, n);
+        if (n > 16) return city_17to32(b.v0, b.v1, n);
+        return city_le16_reg(n == 16 ? b.v0 : window16(b.v0, b.v1, sh), n);
+    }
+    if (code == CODE_ZERO) return 0;
+    uint64_t bits = 0;
+    if (n == 8) {
+        bits = window8(b.v0, b.v1, sh);
+    } else if (n != 0) {
+        bad = true;
+        return 0;
+    }
+    return hash_numeric(code, bits);
+}
+
+// Inclusive wave64 prefix sum on DPP (row_shr within 16-lane rows, then the
+// row_bcast:15 / row_bcast:31 carries across rows).
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false); // row_bcast:15
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false); // row_bcast:31
+    return v;
+}
+
+template <bool NT_STORE, int MIN_WAVES>
+__global__ void __launch_bounds__(256, MIN_WAVES)
+hash_pipelined_kernel(const BatchArgs args) {
+    __shared__ uint8_t codes[HDX_MAX_ATTRS];
+    for (uint32_t j = threadIdx.x; j < args.A; j += blockDim.x) codes[j] = args.codes[j];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t o0 = wave * 64;
+    if (o0 >= args.n) return;
+    const uint32_t nobj = (uint32_t)min<uint64_t>(64, args.n - o0);
+    const uint32_t A = args.A;
+    const uint32_t qA = 64 / A, rA = 64 % A;
+    const uint32_t last = nobj * A - 1;  // last valid slot of this wave
+
+    const uint32_t* lens = args.attr_len + o0 * A;
+    uint64_t* out = args.coords + o0 * A;
+    const uint64_t my_base = args.obj_base[o0 + min<uint32_t>((uint32_t)lane, nobj - 1)];
+
+    uint32_t il = (uint32_t)lane / A, j = (uint32_t)lane % A;
+    uint32_t carry = 0;
+    bool bad = false;
+
+    auto advance = [&](uint32_t& il_, uint32_t& j_) {
+        j_ += rA;
+        il_ += qA;
+        if (j_ >= A) {
+            j_ -= A;
+            ++il_;
+        }
+    };
+    // unconditional, clamped length load for round r
+    auto load_len = [&](uint32_t r) -> uint32_t { return lens[min(r * 64 + (uint32_t)lane, last)]; };
+    auto locate = [&](uint32_t Lraw, uint32_t il_, uint32_t j_, uint32_t& L) -> const uint8_t* {
+        L = il_ < nobj ? Lraw : 0u;
+        const uint32_t Sx = wave_scan_dpp(L) - L;
+        const int head = lane - (int)j_;
+        const uint32_t head_sx = __shfl(Sx, head < 0 ? 0 : head, 64);
+        const uint32_t off = head >= 0 ? Sx - head_sx : carry + Sx;
+        carry = __builtin_amdgcn_readlane(off + L, 63);
+        const int src = il_ < nobj ? (int)il_ : 0;
+        const uint32_t blo = __shfl((uint32_t)my_base, src, 64);
+        const uint32_t bhi = __shfl((uint32_t)(my_base >> 32), src, 64);
+        return args.blob + (((uint64_t)bhi << 32) | blo) + off;
+    };
+
+    // Two round states used ping-pong (loop unrolled by two) so that data still
+    // in flight is never copied between registers.
+    struct Round {
+        const uint8_t* p;
+        uint32_t L, code, il, j, Lraw_next;
+        Blk blk;
+    };
+    // prologue: round 0 located; round 1 lengths and round 0 bytes in flight
+    Round S0, S1;
+    S0.il = il;
+    S0.j = j;
+    S0.p = locate(load_len(0), il, j, S0.L);
+    S0.code = codes[j];
+    S0.Lraw_next = load_len(1);
+    S0.blk = issue_block(S0.code, S0.p, S0.L);
+
+    // Hash round r held in `cur`; first locate round r+1 into `nxt` and put its
+    // bytes (and round r+2's lengths) in flight.  The prefetch is unconditional
+    // (past the last round every lane is invalid, so its loads hit the zero pad):
+    // no conditionally-assigned register survives into the next step.
+    auto step = [&](Round& cur, Round& nxt, uint32_t r) {
+        nxt.il = cur.il;
+        nxt.j = cur.j;
+        advance(nxt.il, nxt.j);
+        nxt.p = locate(cur.Lraw_next, nxt.il, nxt.j, nxt.L);
+        nxt.code = codes[nxt.j < A ? nxt.j : 0];
+        nxt.Lraw_next = load_len(r + 2);
+        nxt.blk = issue_block(nxt.code, nxt.p, nxt.L);
+        if (cur.il < nobj) {
+            const uint64_t h = hash_blk(cur.code, cur.p, cur.L, cur.blk, bad);
+            if (NT_STORE) __builtin_nontemporal_store(h, out + r * 64 + lane);
+            else out[r * 64 + lane] = h;
+        }
+    };
+    for (uint32_t r = 0;; r += 2) {
+        step(S0, S1, r);
+        if (r + 1 >= A) break;
+        step(S1, S0, r + 1);
+        if (r + 2 >= A) break;
+    }
+    if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
+}
+
+template <bool NT, int MIN_WAVES = 1>
+static hipError_t launch_pipe(const BatchArgs& args, hipStream_t stream) {
+    const uint64_t waves = (args.n + 63) / 64;
+    const uint64_t blocks = (waves + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((hash_pipelined_kernel<NT, MIN_WAVES>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    return hipGetLastError();
+}
+
 template <bool A_, bool B_, bool C_, bool D_ = false>
 static hipError_t launch_t(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n + 63) / 64;
@@ -256,11 +533,15 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 4: return launch_t<false, true, true>(args, stream);
         case 5: return launch_t<true, true, false, true>(args, stream);
         case 6: return launch_t<true, true, true, true>(args, stream);
+        case 7: return launch_pipe<false>(args, stream);
+        case 8: return launch_pipe<true>(args, stream);
+        case 9: return launch_pipe<true, 5>(args, stream);
+        case 10: return launch_pipe<true, 6>(args, stream);
         default: return hipErrorInvalidValue;
     }
 }
 
-static constexpr int kDefaultVariant = 3;
+static constexpr int kDefaultVariant = 8;
 
 int hash_variant() {
     static const int v = [] {
