@@ -50,6 +50,8 @@ SIGNATURES = [
     ("hdx_alloc_pinned", _i32, [_sz, _vp]),
     ("hdx_free_pinned", _i32, [_vp]),
     ("hdx_synth_lengths", _i32, [ctypes.POINTER(SynthRule), _u32, _u64, _u64, _u64, _vp, _vp]),
+    ("hdxdbg_set_kernel_variant", _i32, [_i32]),
+    ("hdxdbg_kernel_variant", _i32, []),
     ("hdx_synth_fill", _i32, [ctypes.POINTER(SynthRule), _u32, _u64, _u64, _u64, _vp, _vp, _vp,
                               _u64, _vp]),
 ]

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "hdx_internal.h"
+#include "../../include/hdxhash_debug.h"
 
 #define HDX_EXPORT extern "C" __attribute__((visibility("default")))
 
@@ -489,3 +490,8 @@ HDX_EXPORT hdx_status hdx_synth_fill(const hdx_synth_rule* rules, uint32_t attrs
     HIP_TRY(launch_synth_fill(a, obj_base_dev, attr_len_dev, blob_dev, bytes, s));
     return HDX_OK;
 }
+
+// ---- tuning hooks (include/hdxhash_debug.h) --------------------------------
+
+HDX_EXPORT int hdxdbg_set_kernel_variant(int variant) { return set_hash_variant(variant); }
+HDX_EXPORT int hdxdbg_kernel_variant(void) { return hash_variant(); }

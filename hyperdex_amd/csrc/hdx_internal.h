@@ -40,6 +40,7 @@ hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream);
 hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, int variant);
 // The variant launch_hash_batch uses: HDX_KERNEL_VARIANT (tuning knob) or the default.
 int hash_variant();
+int set_hash_variant(int v);  // -1 if unknown, else the previous variant
 
 struct SynthArgs {
     uint64_t seed;

@@ -541,14 +541,19 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
     }
 }
 
-static constexpr int kDefaultVariant = 8;
+static constexpr int kDefaultVariant = 7;
+static constexpr int kMaxVariant = 10;
 
-int hash_variant() {
-    static const int v = [] {
-        const char* e = getenv("HDX_KERNEL_VARIANT");
-        return e && *e ? atoi(e) : kDefaultVariant;
-    }();
-    return v;
+static int g_variant = [] {
+    const char* e = getenv("HDX_KERNEL_VARIANT");
+    return e && *e ? atoi(e) : kDefaultVariant;
+}();
+
+int hash_variant() { return __atomic_load_n(&g_variant, __ATOMIC_RELAXED); }
+
+int set_hash_variant(int v) {
+    if (v < 0 || v > kMaxVariant) return -1;
+    return __atomic_exchange_n(&g_variant, v, __ATOMIC_RELAXED);
 }
 
 hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream) {

@@ -1,0 +1,68 @@
+"""Interleaved in-process A/B of hash kernel variants (run on the GPU box).
+
+    python scripts/ab_variants.py --configs cfg3a,cfg3b --variants 0,7,8 --reps 7 --launches 5
+
+One batch per config is generated in HBM once; then for `reps` rounds every
+variant is timed back to back (HIP events around `launches` launches), so the
+variants see the same clocks and the same box.  Prints one JSON line per
+(config, variant) with the median and min kernel time and the roofline frac.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="cfg3a")
+    ap.add_argument("--variants", default="0,7")
+    ap.add_argument("--objects", type=int, default=10_000_000)
+    ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--launches", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import synth
+    lib = hdx.lib()
+    dev = torch.device("cuda", 0)
+    variants = [int(v) for v in args.variants.split(",")]
+    for cfg in args.configs.split(","):
+        types, blob, base, lens = synth.make_batch_device(cfg, args.objects, device=dev)
+        A = len(types)
+        coords = torch.empty((args.objects, A), dtype=torch.int64, device=dev)
+        ref = None
+        times = {v: [] for v in variants}
+        for rep in range(args.reps + 1):
+            for v in variants:
+                assert lib.hdxdbg_set_kernel_variant(v) >= 0
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(args.launches):
+                    hdx.hash_batch(types, blob, base, lens, coords=coords)
+                e.record()
+                torch.cuda.synchronize()
+                if rep == 0:  # warm-up round doubles as a cross-variant equality check
+                    if ref is None:
+                        ref = coords.clone()
+                    elif not torch.equal(ref, coords):
+                        raise SystemExit("variant %d differs from variant %d on %s" % (v, variants[0], cfg))
+                    continue
+                times[v].append(s.elapsed_time(e) / args.launches)
+        algo = blob.numel() + args.objects * A * 12
+        for v in variants:
+            t = np.array(times[v])
+            print(json.dumps({"config": cfg, "variant": v, "ms_median": round(float(np.median(t)), 4),
+                              "ms_min": round(float(t.min()), 4),
+                              "frac": round(algo / (np.median(t) / 1e3) / 8e12, 4)}), flush=True)
+        del blob, base, lens, coords, ref
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()

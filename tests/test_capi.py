@@ -14,9 +14,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_symbols():
-    text = open(os.path.join(ROOT, "include", "hdxhash.h")).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(hdx_[a-z0-9_]+)\s*\(", text)))
+    out = set()
+    for h in ("hdxhash.h", "hdxhash_debug.h"):
+        text = open(os.path.join(ROOT, "include", h)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        out |= set(re.findall(r"\b(hdx(?:dbg)?_[a-z0-9_]+)\s*\(", text))
+    return sorted(out)
 
 
 def test_header_matches_binding_table():
@@ -26,10 +29,10 @@ def test_header_matches_binding_table():
 def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH],
                          capture_output=True, text=True, check=True).stdout
-    exported = set(re.findall(r" T (hdx_\w+)", out))
+    exported = set(re.findall(r" T (hdx(?:dbg)?_\w+)", out))
     assert set(declared_symbols()) <= exported
     # nothing else leaks out of the C-ABI (hidden visibility for internals)
-    assert {s for s in exported if s.startswith("hdx_")} == set(declared_symbols())
+    assert exported == set(declared_symbols())
     lib = hdx.lib()
     for name in declared_symbols():
         assert getattr(lib, name) is not None
@@ -92,3 +95,11 @@ def test_product_does_not_reference_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".h", "Makefile")):
                 src = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in src.replace("no CPU", ""), f
+
+
+def test_variant_hook():
+    lib = hdx.lib()
+    cur = lib.hdxdbg_kernel_variant()
+    assert lib.hdxdbg_set_kernel_variant(999) == -1
+    assert lib.hdxdbg_set_kernel_variant(0) == cur
+    assert lib.hdxdbg_set_kernel_variant(cur) == 0

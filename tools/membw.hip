@@ -134,6 +134,42 @@ __global__ void __launch_bounds__(256) k_hashshape(const u32x4* p, const uint32_
     }
 }
 
+
+// one 4 KiB chunk per wave with the hash kernel's dependency chain: previous
+// chunk's lengths (carry) + this chunk's lengths -> dependent 64 B/lane loads
+// -> 8 B store.  Consecutive waves take consecutive chunks (linear front).
+template <bool NT>
+__global__ void __launch_bounds__(256) k_hashshape1(const u32x4* p, const uint32_t* lens, size_t chunks, uint64_t* out) {
+    const int lane = threadIdx.x & 63;
+    size_t w = blockIdx.x * 4ull + (threadIdx.x >> 6);
+    if (w >= chunks) return;
+    uint32_t Lp = w ? lens[(w - 1) * 64 + lane] : 0;
+    uint32_t L = lens[w * 64 + lane];
+    const u32x4* c = p + w * 256 + lane * 4 + ((L + Lp) >> 31);
+    u32x4 a = c[0] ^ c[1] ^ c[2] ^ c[3];
+    uint64_t h = ((uint64_t)(a.x ^ a.y) << 32) | (a.z ^ a.w) ^ L;
+    if (NT) __builtin_nontemporal_store(h, out + w * 64 + lane);
+    else out[w * 64 + lane] = h;
+}
+
+// 17 dependent rounds per wave but rounds strided by the whole grid
+// (round r of wave w = chunk r * W + w): same per-wave chain as hashshape17,
+// linear chip-wide front.
+template <int R>
+__global__ void __launch_bounds__(256) k_hashshape_strided(const u32x4* p, const uint32_t* lens, size_t chunks, uint64_t* out) {
+    const int lane = threadIdx.x & 63;
+    const size_t W = (size_t)gridDim.x * 4;
+    size_t w0 = blockIdx.x * 4ull + (threadIdx.x >> 6);
+    for (int r = 0; r < R; ++r) {
+        size_t w = w0 + r * W;
+        if (w >= chunks) return;
+        uint32_t L = lens[w * 64 + lane];
+        const u32x4* c = p + w * 256 + lane * 4 + (L >> 31);
+        u32x4 a = c[0] ^ c[1] ^ c[2] ^ c[3];
+        out[w * 64 + lane] = ((uint64_t)(a.x ^ a.y) << 32) | (a.z ^ a.w) ^ L;
+    }
+}
+
 // grid-stride streaming read, 2048 blocks, 4 x 16 B in flight per lane
 __global__ void __launch_bounds__(256) k_stream(const u32x4* p, size_t n16, uint32_t* out) {
     u32x4 a = {0, 0, 0, 0};
@@ -215,6 +251,12 @@ int main(int argc, char** argv) {
                [&] { k_hashshape<17, false><<<b17, 256>>>(p, lens, chunks, coords); });
         timeit("hashshape17_nt", bytes + chunks * 64 * 12.0, reps,
                [&] { k_hashshape<17, true><<<b17, 256>>>(p, lens, chunks, coords); });
+        timeit("hashshape1_plain", bytes + chunks * 64 * 12.0, reps,
+               [&] { k_hashshape1<false><<<blocks, 256>>>(p, lens, chunks, coords); });
+        timeit("hashshape1_nt", bytes + chunks * 64 * 12.0, reps,
+               [&] { k_hashshape1<true><<<blocks, 256>>>(p, lens, chunks, coords); });
+        timeit("hashshape17_strided", bytes + chunks * 64 * 12.0, reps,
+               [&] { k_hashshape_strided<17><<<b17, 256>>>(p, lens, chunks, coords); });
         CK(hipFree(lens));
     }
     for (unsigned g : {1024u, 2048u, 4096u, 8192u})
