@@ -244,6 +244,7 @@ static hdx_status hash_host(const uint8_t* codes, uint32_t A, const uint8_t* blo
     BatchArgs args{};
     args.A = A;
     std::memcpy(args.codes, codes, A);
+    finalize_args(args);
 
     struct Pending { uint64_t first = 0, cnt = 0; bool live = false; } pend[2];
     auto finish = [&](int k) -> hdx_status {
@@ -372,6 +373,7 @@ HDX_EXPORT hdx_status hdx_hash_batch_device(const uint32_t* types, uint32_t attr
     args.status = status_dev;
     args.n = n;
     args.A = attrs_sz;
+    finalize_args(args);
     HIP_TRY(launch_hash_batch(args, s));
     return HDX_OK;
 }

@@ -29,11 +29,13 @@ struct BatchArgs {
     uint32_t* status;
     uint64_t n;
     uint32_t A;
-    uint32_t pad_;
+    uint32_t uniform_code;  // the code every attribute shares, or 0xff if mixed
     uint8_t codes[HDX_MAX_ATTRS];
 };
 
 hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream);
+// Fills args.uniform_code from args.codes[0..A).
+void finalize_args(BatchArgs& args);
 // Kernel variants (hdx_kernels.hip): 0 plain, 1 +length prefetch, 2 +obj_base in
 // registers, 3 +string-block prefetch, 4 = 3 without length prefetch, 5/6 = 2/3 with
 // non-temporal coordinate stores.

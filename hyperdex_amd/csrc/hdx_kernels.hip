@@ -514,6 +514,97 @@ static hipError_t launch_pipe(const BatchArgs& args, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// ===========================================================================
+// Chunk kernel (variants 11/12): one wave = one chunk of 64 consecutive
+// (object, attribute) slots of the flattened n*A slot space — the layout's
+// natural unit: a coalesced 256 B length load, 64 attributes hashed, one
+// coalesced 512 B coordinate store.  A wave has a single dependent chain
+// (lengths -> prefix sum -> addresses -> bytes -> hash -> store) and exits, so
+// no store ever sits in front of a later load in the wave's vmcnt queue, and
+// the hardware keeps up to 8 waves per SIMD issuing fresh loads.  An object
+// that starts in an earlier chunk contributes a carry: the sum of its
+// attribute lengths that precede this chunk (read back from lengths the
+// neighbouring wave just pulled through L2).
+// ===========================================================================
+
+// Wave-uniform slot -> (object, attribute) split without a 64-bit integer
+// divide: q < 2^53, so the f64 quotient is off by at most one; fix it up.
+__device__ __forceinline__ void split_slot(uint64_t q, uint32_t A, uint64_t& i0, uint32_t& j0) {
+    uint64_t i = (uint64_t)((double)q * (1.0 / (double)A));
+    int64_t rem = (int64_t)(q - i * A);
+    if (rem < 0) { --i; rem += A; }
+    if (rem >= (int64_t)A) { ++i; rem -= A; }
+    i0 = i;
+    j0 = (uint32_t)rem;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
+    return __builtin_amdgcn_readlane(wave_scan_dpp(v), 63);
+}
+
+template <bool NT_STORE>
+__global__ void __launch_bounds__(256)
+hash_chunk_kernel(const BatchArgs args) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint32_t A = args.A;
+    const uint64_t nslots = args.n * A;
+    const uint64_t q0 = wave * 64;
+    if (q0 >= nslots) return;
+
+    // this lane's slot -> (object il, attribute j)
+    uint64_t i0;
+    uint32_t j0;
+    split_slot(q0, A, i0, j0);
+    const uint32_t t = j0 + (uint32_t)lane;
+    const uint32_t di = t / A;  // small: t < A + 64
+    const uint32_t j = t - di * A;
+    const uint64_t il = i0 + di;
+    const bool valid = q0 + lane < nslots;
+
+    // lengths of this chunk, the object bases, and the carry-in lengths
+    const uint32_t L = valid ? args.attr_len[q0 + lane] : 0u;
+    const uint64_t base = args.obj_base[valid ? il : i0];
+    uint32_t carry = 0;
+    for (uint32_t k = 0; k < j0; k += 64) {  // slots [q0 - j0, q0) belong to object i0
+        const uint32_t idx = k + (uint32_t)lane;
+        const uint32_t v = idx < j0 ? args.attr_len[q0 - j0 + idx] : 0u;
+        carry += wave_sum_dpp(v);
+    }
+    uint32_t code;
+    if (args.uniform_code != 0xffu) {
+        code = args.uniform_code;
+    } else {
+        const uint32_t packed = reinterpret_cast<const uint32_t*>(args.codes)[lane];
+        code = (__shfl(packed, (int)(j >> 2), 64) >> (8 * (j & 3))) & 0xffu;
+    }
+
+    const uint32_t Sx = wave_scan_dpp(L) - L;
+    const int head = lane - (int)j;  // lane holding this object's attribute 0, if in this chunk
+    const uint32_t head_sx = __shfl(Sx, head < 0 ? 0 : head, 64);
+    const uint32_t off = head >= 0 ? Sx - head_sx : carry + Sx;
+    const uint8_t* p = args.blob + base + off;
+
+    const Blk blk = issue_block(valid ? code : (uint32_t)CODE_ZERO, p, L);
+    if (valid) {
+        bool bad = false;
+        const uint64_t h = hash_blk(code, p, L, blk, bad);
+        if (NT_STORE) __builtin_nontemporal_store(h, args.coords + q0 + lane);
+        else args.coords[q0 + lane] = h;
+        if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
+    }
+}
+
+template <bool NT>
+static hipError_t launch_chunk(const BatchArgs& args, hipStream_t stream) {
+    const uint64_t waves = (args.n * args.A + 63) / 64;
+    const uint64_t blocks = (waves + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((hash_chunk_kernel<NT>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    return hipGetLastError();
+}
+
 template <bool A_, bool B_, bool C_, bool D_ = false>
 static hipError_t launch_t(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n + 63) / 64;
@@ -537,12 +628,14 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 8: return launch_pipe<true>(args, stream);
         case 9: return launch_pipe<true, 5>(args, stream);
         case 10: return launch_pipe<true, 6>(args, stream);
+        case 11: return launch_chunk<false>(args, stream);
+        case 12: return launch_chunk<true>(args, stream);
         default: return hipErrorInvalidValue;
     }
 }
 
 static constexpr int kDefaultVariant = 7;
-static constexpr int kMaxVariant = 10;
+static constexpr int kMaxVariant = 12;
 
 static int g_variant = [] {
     const char* e = getenv("HDX_KERNEL_VARIANT");
@@ -554,6 +647,12 @@ int hash_variant() { return __atomic_load_n(&g_variant, __ATOMIC_RELAXED); }
 int set_hash_variant(int v) {
     if (v < 0 || v > kMaxVariant) return -1;
     return __atomic_exchange_n(&g_variant, v, __ATOMIC_RELAXED);
+}
+
+void finalize_args(BatchArgs& args) {
+    args.uniform_code = args.codes[0];
+    for (uint32_t j = 1; j < args.A; ++j)
+        if (args.codes[j] != args.codes[0]) args.uniform_code = 0xffu;
 }
 
 hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream) {
