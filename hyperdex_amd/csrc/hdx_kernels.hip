@@ -262,12 +262,17 @@ __device__ __attribute__((aligned(64))) uint8_t g_zero_pad[64];
 // out-of-order completion would force full vmcnt/lgkmcnt drains).
 typedef u64x2 __attribute__((aligned(1))) u64x2_u;
 typedef const __attribute__((address_space(1))) u64x2_u* gvec_ptr;
-__device__ __forceinline__ u64x2 gld16(const uint8_t* p) { return *(gvec_ptr)p; }
+template <bool NT = false>
+__device__ __forceinline__ u64x2 gld16(const uint8_t* p) {
+    if (NT) return __builtin_nontemporal_load((gvec_ptr)p);
+    return *(gvec_ptr)p;
+}
 
 struct Blk {
     u64x2 v0, v1, v2, v3;
 };
 
+template <bool NTL = false>
 __device__ __forceinline__ Blk issue_block(uint32_t code, const uint8_t* p, uint32_t n) {
     const uint8_t* D = g_zero_pad;
     const bool str = code == CODE_STRING;
@@ -280,10 +285,10 @@ __device__ __forceinline__ Blk issue_block(uint32_t code, const uint8_t* p, uint
     const uint8_t* a2 = g64 || g32 ? p + n - 32 : D;
     const uint8_t* a3 = g64 || g32 ? p + n - 16 : D;
     Blk b;
-    b.v0 = gld16(a0);
-    b.v1 = gld16(a1);
-    b.v2 = gld16(a2);
-    b.v3 = gld16(a3);
+    b.v0 = gld16<NTL>(a0);
+    b.v1 = gld16<NTL>(a1);
+    b.v2 = gld16<NTL>(a2);
+    b.v3 = gld16<NTL>(a3);
     return b;
 }
 
@@ -353,6 +358,7 @@ __device__ __forceinline__ uint64_t city_le16_reg(const u64x2& w, uint32_t n) {
 
 // city.cc:361-397 for n > 64 with the tail block in registers; the first
 // 64-byte block is loaded up front (its first word is Fetch64(s) of :380).
+template <bool NTL = false>
 __device__ __forceinline__ uint64_t city_gt64_reg(const uint8_t* s, uint32_t n, const Blk& t) {
     const u64x2 e0 = t.v0, e1 = t.v1, e2 = t.v2, e3 = t.v3;
     uint64_t x = e1.y;
@@ -361,7 +367,7 @@ __device__ __forceinline__ uint64_t city_gt64_reg(const uint8_t* s, uint32_t n, 
     uint64_t v0, v1, w0, w1;
     weak32(e0.x, e0.y, e1.x, e1.y, n, z, v0, v1);
     weak32(e2.x, e2.y, e3.x, e3.y, y + K1, x, w0, w1);
-    u64x2 b0 = gld16(s), b1 = gld16(s + 16), b2 = gld16(s + 32), b3 = gld16(s + 48);
+    u64x2 b0 = gld16<NTL>(s), b1 = gld16<NTL>(s + 16), b2 = gld16<NTL>(s + 32), b3 = gld16<NTL>(s + 48);
     x = x * K1 + b0.x;
     const uint32_t blocks = (n - 1) >> 6;
     for (uint32_t k = 0;;) {
@@ -377,16 +383,17 @@ __device__ __forceinline__ uint64_t city_gt64_reg(const uint8_t* s, uint32_t n, 
         const uint64_t tt = z; z = x; x = tt;
         if (++k == blocks) break;
         s += 64;
-        b0 = gld16(s); b1 = gld16(s + 16); b2 = gld16(s + 32); b3 = gld16(s + 48);
+        b0 = gld16<NTL>(s); b1 = gld16<NTL>(s + 16); b2 = gld16<NTL>(s + 32); b3 = gld16<NTL>(s + 48);
     }
     return mix16(mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z, mix16(v1, w1, KMUL) + x, KMUL);
 }
 
+template <bool NTL = false>
 __device__ __forceinline__ uint64_t hash_blk(uint32_t code, const uint8_t* p, uint32_t n, const Blk& b,
                                              bool& bad) {
     const uint32_t sh = (uint32_t)(uintptr_t)p & 15;
     if (code == CODE_STRING) {
-        if (n > 64) return city_gt64_reg(p, n, b);
+        if (n > 64) return city_gt64_reg<NTL>(p, n, b);
         if (n > 32) return city_33to64(b.v0, b.v1, b.v2, b.v3, n);
         if (n > 16) return city_17to32(b.v0, b.v1, n);
         return city_le16_reg(n == 16 ? b.v0 : window16(b.v0, b.v1, sh), n);
@@ -414,7 +421,7 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
     return v;
 }
 
-template <bool NT_STORE, int MIN_WAVES>
+template <bool NT_STORE, int MIN_WAVES, bool NT_LOAD>
 __global__ void __launch_bounds__(256, MIN_WAVES)
 hash_pipelined_kernel(const BatchArgs args) {
     __shared__ uint8_t codes[HDX_MAX_ATTRS];
@@ -475,7 +482,7 @@ hash_pipelined_kernel(const BatchArgs args) {
     S0.p = locate(load_len(0), il, j, S0.L);
     S0.code = codes[j];
     S0.Lraw_next = load_len(1);
-    S0.blk = issue_block(S0.code, S0.p, S0.L);
+    S0.blk = issue_block<NT_LOAD>(S0.code, S0.p, S0.L);
 
     // Hash round r held in `cur`; first locate round r+1 into `nxt` and put its
     // bytes (and round r+2's lengths) in flight.  The prefetch is unconditional
@@ -488,9 +495,9 @@ hash_pipelined_kernel(const BatchArgs args) {
         nxt.p = locate(cur.Lraw_next, nxt.il, nxt.j, nxt.L);
         nxt.code = codes[nxt.j < A ? nxt.j : 0];
         nxt.Lraw_next = load_len(r + 2);
-        nxt.blk = issue_block(nxt.code, nxt.p, nxt.L);
+        nxt.blk = issue_block<NT_LOAD>(nxt.code, nxt.p, nxt.L);
         if (cur.il < nobj) {
-            const uint64_t h = hash_blk(cur.code, cur.p, cur.L, cur.blk, bad);
+            const uint64_t h = hash_blk<NT_LOAD>(cur.code, cur.p, cur.L, cur.blk, bad);
             if (NT_STORE) __builtin_nontemporal_store(h, out + r * 64 + lane);
             else out[r * 64 + lane] = h;
         }
@@ -504,13 +511,13 @@ hash_pipelined_kernel(const BatchArgs args) {
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <bool NT, int MIN_WAVES = 1>
+template <bool NT, int MIN_WAVES = 1, bool NTL = false>
 static hipError_t launch_pipe(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n + 63) / 64;
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_pipelined_kernel<NT, MIN_WAVES>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_pipelined_kernel<NT, MIN_WAVES, NTL>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
     return hipGetLastError();
 }
 
@@ -542,7 +549,7 @@ __device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
     return __builtin_amdgcn_readlane(wave_scan_dpp(v), 63);
 }
 
-template <bool NT_STORE>
+template <bool NT_STORE, bool NT_LOAD>
 __global__ void __launch_bounds__(256)
 hash_chunk_kernel(const BatchArgs args) {
     const int lane = threadIdx.x & 63;
@@ -585,23 +592,23 @@ hash_chunk_kernel(const BatchArgs args) {
     const uint32_t off = head >= 0 ? Sx - head_sx : carry + Sx;
     const uint8_t* p = args.blob + base + off;
 
-    const Blk blk = issue_block(valid ? code : (uint32_t)CODE_ZERO, p, L);
+    const Blk blk = issue_block<NT_LOAD>(valid ? code : (uint32_t)CODE_ZERO, p, L);
     if (valid) {
         bool bad = false;
-        const uint64_t h = hash_blk(code, p, L, blk, bad);
+        const uint64_t h = hash_blk<NT_LOAD>(code, p, L, blk, bad);
         if (NT_STORE) __builtin_nontemporal_store(h, args.coords + q0 + lane);
         else args.coords[q0 + lane] = h;
         if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
     }
 }
 
-template <bool NT>
+template <bool NT, bool NTL = false>
 static hipError_t launch_chunk(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + 63) / 64;
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_chunk_kernel<NT>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_chunk_kernel<NT, NTL>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
     return hipGetLastError();
 }
 
@@ -630,12 +637,14 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 10: return launch_pipe<true, 6>(args, stream);
         case 11: return launch_chunk<false>(args, stream);
         case 12: return launch_chunk<true>(args, stream);
+        case 13: return launch_chunk<true, true>(args, stream);
+        case 14: return launch_pipe<true, 1, true>(args, stream);
         default: return hipErrorInvalidValue;
     }
 }
 
 static constexpr int kDefaultVariant = 7;
-static constexpr int kMaxVariant = 12;
+static constexpr int kMaxVariant = 14;
 
 static int g_variant = [] {
     const char* e = getenv("HDX_KERNEL_VARIANT");
