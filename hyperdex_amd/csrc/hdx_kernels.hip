@@ -612,6 +612,154 @@ static hipError_t launch_chunk(const BatchArgs& args, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// ===========================================================================
+// Binned chunk kernel (variant 15/16): the chunk kernel at workgroup scope
+// (4 waves = 256 consecutive slots) with the slots regrouped by work class
+// before hashing, so that a wave's lanes run the same CityHash regime and the
+// same number of 64-byte loop blocks instead of the union of all of them.
+//   class 0: numeric, non-hashable, empty and <= 16-byte strings (cheap paths)
+//   class 1: 17..64-byte strings
+//   class 1+b: strings of b = ceil(len/64)-1 loop blocks (b = 1..5), 6+ -> 7
+// A counting sort in LDS (ballot + mbcnt ranks, per-wave class counts)
+// places a 16-byte descriptor {pointer, length, code, slot} per slot; every
+// wave hashes 64 consecutive sorted descriptors and writes its coordinates
+// back to LDS by slot, and the workgroup stores them in slot order (one
+// coalesced 512 B store per wave).  Workgroups whose 256 slots all fall into
+// one class skip the sort.
+// ===========================================================================
+constexpr int kClasses = 8;
+
+__device__ __forceinline__ uint32_t work_class(uint32_t code, uint32_t n, bool valid) {
+    if (!valid || code != CODE_STRING || n <= 16) return 0;
+    if (n <= 64) return 1;
+    const uint32_t b = (n - 1) >> 6;
+    return b >= 6 ? 7u : 1u + b;
+}
+
+struct alignas(16) SlotDesc {
+    const uint8_t* p;
+    uint32_t n;
+    uint32_t code_slot;  // code | slot << 8
+};
+
+template <bool NT_STORE>
+__global__ void __launch_bounds__(256)
+hash_binned_kernel(const BatchArgs args) {
+    __shared__ SlotDesc desc[256];
+    __shared__ uint64_t res[256];
+    __shared__ uint32_t counts[4][kClasses];
+    __shared__ uint32_t wave_cls[4];
+
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const uint64_t wave = (uint64_t)blockIdx.x * 4 + w;
+    const uint32_t A = args.A;
+    const uint64_t nslots = args.n * A;
+    const uint64_t q0 = wave * 64;
+    const bool live = q0 < nslots;  // wave-uniform: a dead wave still joins the barriers
+
+    uint32_t L = 0, code = CODE_ZERO;
+    const uint8_t* p = g_zero_pad;
+    bool valid = false;
+    if (live) {
+        uint64_t i0;
+        uint32_t j0;
+        split_slot(q0, A, i0, j0);
+        const uint32_t t = j0 + (uint32_t)lane;
+        const uint32_t di = t / A;
+        const uint32_t j = t - di * A;
+        const uint64_t il = i0 + di;
+        valid = q0 + lane < nslots;
+        L = valid ? args.attr_len[q0 + lane] : 0u;
+        const uint64_t base = args.obj_base[valid ? il : i0];
+        uint32_t carry = 0;
+        for (uint32_t k = 0; k < j0; k += 64) {
+            const uint32_t idx = k + (uint32_t)lane;
+            const uint32_t v = idx < j0 ? args.attr_len[q0 - j0 + idx] : 0u;
+            carry += wave_sum_dpp(v);
+        }
+        if (args.uniform_code != 0xffu) {
+            code = args.uniform_code;
+        } else {
+            const uint32_t packed = reinterpret_cast<const uint32_t*>(args.codes)[lane];
+            code = (__shfl(packed, (int)(j >> 2), 64) >> (8 * (j & 3))) & 0xffu;
+        }
+        const uint32_t Sx = wave_scan_dpp(L) - L;
+        const int head = lane - (int)j;
+        const uint32_t head_sx = __shfl(Sx, head < 0 ? 0 : head, 64);
+        const uint32_t off = head >= 0 ? Sx - head_sx : carry + Sx;
+        p = args.blob + base + off;
+        if (!valid) code = CODE_ZERO;
+    }
+
+    // ---- classify; skip the sort when the workgroup is one class ----------
+    const uint32_t cls = work_class(code, L, valid);
+    const uint32_t c0 = __builtin_amdgcn_readfirstlane(cls);
+    const bool wave_uniform = __all(cls == c0);
+    if (lane == 0) wave_cls[w] = live ? (wave_uniform ? c0 : 0xffu) : 0xfeu;
+    uint32_t my_count = 0;
+#pragma unroll
+    for (int c = 0; c < kClasses; ++c) {
+        const uint64_t m = __ballot(cls == (uint32_t)c);
+        if ((uint32_t)c == cls) my_count = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (lane == c) counts[w][c] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    uint32_t wc = 0xffu;
+    bool one_class = true;
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t x = wave_cls[k];
+        if (x == 0xfeu) continue;
+        if (x == 0xffu || (wc != 0xffu && x != wc)) one_class = false;
+        wc = x;
+    }
+
+    bool bad = false;
+    uint64_t h = 0;
+    if (one_class) {
+        const Blk blk = issue_block(code, p, L);
+        if (valid) h = hash_blk(code, p, L, blk, bad);
+    } else {
+        // sorted position = (slots of lower classes) + (this class in lower waves) + rank
+        uint32_t pos = my_count;
+        for (int c = 0; c < kClasses; ++c) {
+            const uint32_t tot = counts[0][c] + counts[1][c] + counts[2][c] + counts[3][c];
+            if ((uint32_t)c < cls) pos += tot;
+        }
+        for (int k = 0; k < 4; ++k)
+            if (k < w) pos += counts[k][cls];
+        SlotDesc d;
+        d.p = p;
+        d.n = L;
+        d.code_slot = code | ((uint32_t)threadIdx.x << 8);
+        desc[pos] = d;
+        __syncthreads();
+        const SlotDesc e = desc[threadIdx.x];
+        const uint32_t ecode = e.code_slot & 0xffu, eslot = e.code_slot >> 8;
+        const Blk blk = issue_block(ecode, e.p, e.n);
+        const uint64_t eh = hash_blk(ecode, e.p, e.n, blk, bad);
+        res[eslot] = eh;
+        __syncthreads();
+        h = res[threadIdx.x];
+    }
+    if (valid) {
+        if (NT_STORE) __builtin_nontemporal_store(h, args.coords + q0 + lane);
+        else args.coords[q0 + lane] = h;
+    }
+    if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
+}
+
+template <bool NT>
+static hipError_t launch_binned(const BatchArgs& args, hipStream_t stream) {
+    const uint64_t waves = (args.n * args.A + 63) / 64;
+    const uint64_t blocks = (waves + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((hash_binned_kernel<NT>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    return hipGetLastError();
+}
+
 template <bool A_, bool B_, bool C_, bool D_ = false>
 static hipError_t launch_t(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n + 63) / 64;
@@ -639,12 +787,14 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 12: return launch_chunk<true>(args, stream);
         case 13: return launch_chunk<true, true>(args, stream);
         case 14: return launch_pipe<true, 1, true>(args, stream);
+        case 15: return launch_binned<false>(args, stream);
+        case 16: return launch_binned<true>(args, stream);
         default: return hipErrorInvalidValue;
     }
 }
 
 static constexpr int kDefaultVariant = 7;
-static constexpr int kMaxVariant = 14;
+static constexpr int kMaxVariant = 16;
 
 static int g_variant = [] {
     const char* e = getenv("HDX_KERNEL_VARIANT");
