@@ -1,0 +1,34 @@
+"""Run the hash kernel a few times on one synthetic config (profiling target).
+
+    python scripts/run_kernel.py --config cfg3b --variant 12 --launches 3 [--objects N]
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="cfg3a")
+    ap.add_argument("--variant", type=int, default=-1)
+    ap.add_argument("--launches", type=int, default=3)
+    ap.add_argument("--objects", type=int, default=10_000_000)
+    a = ap.parse_args()
+    import torch
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import synth
+    if a.variant >= 0:
+        assert hdx.lib().hdxdbg_set_kernel_variant(a.variant) >= 0
+    dev = torch.device("cuda", 0)
+    types, blob, base, lens = synth.make_batch_device(a.config, a.objects, device=dev)
+    coords = torch.empty((a.objects, len(types)), dtype=torch.int64, device=dev)
+    for _ in range(a.launches):
+        hdx.hash_batch(types, blob, base, lens, coords=coords)
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()
