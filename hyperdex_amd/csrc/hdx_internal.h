@@ -42,7 +42,7 @@ void finalize_args(BatchArgs& args);
 hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, int variant);
 // The variant launch_hash_batch uses: HDX_KERNEL_VARIANT (tuning knob) or the default.
 int hash_variant();
-int set_hash_variant(int v);  // -1 if unknown, else the previous variant
+int set_hash_variant(int v);  // -2 if unknown, else the previous selection (-1 = auto)
 
 struct SynthArgs {
     uint64_t seed;

@@ -811,7 +811,10 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
     }
 }
 
-static constexpr int kDefaultVariant = 7;
+// -1 = automatic: the chunk kernel (12) unless most attributes are
+// fixed-size numerics, where the 64-objects-per-wave pipelined kernel (8)
+// amortises its per-wave setup better (scripts/ab_variants.py).
+static constexpr int kDefaultVariant = -1;
 static constexpr int kMaxVariant = 17;
 
 static int g_variant = [] {
@@ -819,10 +822,16 @@ static int g_variant = [] {
     return e && *e ? atoi(e) : kDefaultVariant;
 }();
 
+static int auto_variant(const BatchArgs& args) {
+    uint32_t numeric = 0;
+    for (uint32_t j = 0; j < args.A; ++j) numeric += args.codes[j] >= CODE_INT64;
+    return 2 * numeric > args.A ? 8 : 12;
+}
+
 int hash_variant() { return __atomic_load_n(&g_variant, __ATOMIC_RELAXED); }
 
 int set_hash_variant(int v) {
-    if (v < 0 || v > kMaxVariant) return -1;
+    if (v < -1 || v > kMaxVariant) return -2;
     return __atomic_exchange_n(&g_variant, v, __ATOMIC_RELAXED);
 }
 
@@ -833,7 +842,8 @@ void finalize_args(BatchArgs& args) {
 }
 
 hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream) {
-    return launch_hash_batch_variant(args, stream, hash_variant());
+    const int v = hash_variant();
+    return launch_hash_batch_variant(args, stream, v < 0 ? auto_variant(args) : v);
 }
 
 }  // namespace hdx

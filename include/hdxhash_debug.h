@@ -10,8 +10,9 @@ extern "C" {
 #endif
 
 /* Select the hash kernel variant for subsequent launches in this process
- * (see hyperdex_amd/csrc/hdx_kernels.hip); returns the previous one, or -1
- * for an unknown variant (nothing changed). */
+ * (see hyperdex_amd/csrc/hdx_kernels.hip; -1 = automatic per schema);
+ * returns the previous selection, or -2 for an unknown variant (nothing
+ * changed). */
 int hdxdbg_set_kernel_variant(int variant);
 int hdxdbg_kernel_variant(void);
 

@@ -21,7 +21,7 @@ def main():
     import hyperdex_amd as hdx
     from hyperdex_amd import synth
     if a.variant >= 0:
-        assert hdx.lib().hdxdbg_set_kernel_variant(a.variant) >= 0
+        assert hdx.lib().hdxdbg_set_kernel_variant(a.variant) >= -1
     dev = torch.device("cuda", 0)
     types, blob, base, lens = synth.make_batch_device(a.config, a.objects, device=dev)
     coords = torch.empty((a.objects, len(types)), dtype=torch.int64, device=dev)

@@ -100,6 +100,6 @@ def test_product_does_not_reference_oracle():
 def test_variant_hook():
     lib = hdx.lib()
     cur = lib.hdxdbg_kernel_variant()
-    assert lib.hdxdbg_set_kernel_variant(999) == -1
+    assert lib.hdxdbg_set_kernel_variant(999) == -2
     assert lib.hdxdbg_set_kernel_variant(0) == cur
     assert lib.hdxdbg_set_kernel_variant(cur) == 0
