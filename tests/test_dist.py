@@ -1,0 +1,71 @@
+"""Sharded batches on world_size 2 (gloo, CPU): shard_ranges + allgather_coords.
+
+The per-shard coordinates come from the oracle here (no GPU on this host);
+the GPU path runs the same functions over RCCL in bench.py --gpus N."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from hyperdex_amd import dist as hdist
+from hyperdex_amd import synth
+
+
+def test_shard_ranges_even():
+    for n in (0, 1, 7, 64, 1000):
+        for world in (1, 2, 3, 8):
+            r = hdist.shard_ranges(n, world)
+            assert [c for _, c in r] and sum(c for _, c in r) == n
+            assert r[0][0] == 0 and all(r[k][0] + r[k][1] == r[k + 1][0] for k in range(world - 1))
+            assert max(c for _, c in r) - min(c for _, c in r) <= 1
+
+
+def test_shard_ranges_byte_balanced():
+    rng = np.random.default_rng(2)
+    sizes = rng.integers(1, 2000, 5000)
+    for world in (2, 4, 8):
+        r = hdist.shard_ranges(len(sizes), world, sizes)
+        assert sum(c for _, c in r) == len(sizes)
+        per = [sizes[f:f + c].sum() for f, c in r]
+        assert max(per) - min(per) <= 2 * sizes.max()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, ret):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import oracle
+    n = 301
+    types, blob, base, lens = synth.make_batch_host("cfg3b", n, seed=42)
+    A = len(types)
+    sizes = lens.reshape(n, A).astype(np.int64).sum(axis=1)
+    ranges = hdist.shard_ranges(n, world, sizes)
+    first, cnt = ranges[rank]
+    local, err = oracle.hash_batch(types, blob, base[first:first + cnt],
+                                   lens[first * A:(first + cnt) * A])
+    assert err == 0
+    full = hdist.allgather_coords(torch.from_numpy(local.view(np.int64).copy()),
+                                  [c for _, c in ranges])
+    want, _ = oracle.hash_batch(types, blob, base, lens)
+    ret[rank] = bool(np.array_equal(full.numpy().view(np.uint64), want))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_allgather_matches_single_process(world):
+    ctx = mp.get_context("spawn")
+    ret = ctx.Manager().dict()
+    mp.start_processes(_worker, args=(world, _free_port(), ret), nprocs=world, start_method="spawn")
+    assert all(ret[r] for r in range(world))
