@@ -25,6 +25,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+ROOT = os.path.dirname(os.path.abspath(__file__))
 ALGO_EXTRA_PER_ATTR = 4 + 8  # u32 length read + u64 coordinate write
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
@@ -39,8 +40,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-allgather", action="store_true")
-    ap.add_argument("--host-path", action="store_true",
-                    help="also time the host-resident (PCIe-inclusive) path")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip timing the host-resident (PCIe-inclusive) path")
+    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+                    help="HBM bytes/launch measured by scripts/gpu_profile.sh (rocprofv3 PMC)")
     args = ap.parse_args()
 
     import torch
@@ -52,11 +55,26 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # HDX_BENCH_BACKEND=gloo rehearses the multi-rank flow with every rank on
+    # cuda:0 (one-GPU box); the real multi-GPU run is one rank per GPU on RCCL.
+    backend = os.environ.get("HDX_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = 0
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+
+    def max_over_ranks(*xs):
+        if world == 1:
+            return xs
+        t = torch.tensor(xs, dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return tuple(float(v) for v in t.tolist())
 
     cfg, n = args.config, args.objects
     types, blob, base, lens = synth.make_batch_device(cfg, n, first=rank * n, device=dev)
@@ -86,10 +104,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
-    if world > 1:
-        t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kernel_ms = float(t[0]), float(t[1])
+    elapsed, kernel_ms = max_over_ranks(elapsed, kernel_ms)
 
     ms_per_step = elapsed / args.steps * 1e3
     total_payload = payload * world
@@ -120,14 +135,16 @@ def main():
                    "parallelism": "shard%d" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": None, "kernel_ms": round(kernel_ms, 4),
-                     "algorithmic_bytes_per_launch": algo_bytes},
+                     "traffic": measured_traffic(args.traffic, cfg, n),
+                     "kernel_ms": round(kernel_ms, 4),
+                     "algorithmic_bytes_per_launch": algo_bytes,
+                     "kernel": "hdx::hash_chunk_kernel / hash_pipelined_kernel (auto per schema)"},
     }
 
     if world > 1 and not args.no_allgather:
-        result["allgather"] = time_allgather(coords, world, dev)
+        result["allgather"] = time_allgather(coords, world, dev, backend, max_over_ranks)
 
-    if args.host_path and rank == 0:
+    if not args.no_host_path and rank == 0 and world == 1:
         result["host_path"] = time_host_path(types, blob, base, lens, A)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -140,24 +157,37 @@ def main():
         dist.destroy_process_group()
 
 
-def time_allgather(coords, world, dev, reps=5):
+def time_allgather(coords, world, dev, backend, max_over_ranks, reps=3):
+    """RCCL all-gather of every rank's (n, A) u64 coordinates into (world*n, A)
+    (hyperdex_amd.dist.allgather_coords), timed apart from the hash phase."""
     import torch
     import torch.distributed as dist
-    out = torch.empty((world * coords.shape[0], coords.shape[1]), dtype=coords.dtype, device=dev)
-    dist.all_gather_into_tensor(out, coords)
+
+    from hyperdex_amd.dist import allgather_coords
+    src = coords if backend == "nccl" else coords[: min(coords.shape[0], 1_000_000)].cpu()
+    counts = [src.shape[0]] * world
+    out = allgather_coords(src, counts)
     torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
-        dist.all_gather_into_tensor(out, coords)
+        out = allgather_coords(src, counts)
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / reps
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t[0])
+    (dt,) = max_over_ranks((time.perf_counter() - t0) / reps)
     nbytes = out.numel() * 8
-    return {"ms": round(dt * 1e3, 3), "bytes": nbytes,
+    return {"ms": round(dt * 1e3, 3), "bytes": nbytes, "backend": backend,
             "busbw_GBps": round(nbytes * (world - 1) / world / dt / 1e9, 2)}
+
+
+def measured_traffic(path, cfg, n):
+    """HBM bytes per launch for this config from the committed PMC summary
+    (scripts/gpu_profile.sh -> scripts/traffic_from_pmc.py), scaled to n."""
+    try:
+        rec = json.load(open(path))[cfg]
+    except (OSError, KeyError, ValueError):
+        return None
+    per_obj = rec["traffic_bytes"] / rec.get("objects", 10_000_000)
+    return int(per_obj * n)
 
 
 def time_host_path(types, blob, base, lens, A, n_host=2_000_000):

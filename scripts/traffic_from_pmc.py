@@ -1,0 +1,46 @@
+"""HBM bytes per launch of the hash kernel from rocprofv3 --pmc passes.
+
+    python scripts/traffic_from_pmc.py FETCH_DIR WRITE_DIR CONFIG OUT_JSON [OBJECTS]
+
+FETCH_SIZE and WRITE_SIZE are in KiB.  On gfx950 FETCH_SIZE reads exactly half
+the bytes of a wide (16 B/lane) coalesced streaming read (MI355X_MICROARCH.md
+§HBM); the kernel's reads are dominated by such loads, so FETCH is doubled.
+Calibration: on config 3a, 2 x FETCH_SIZE equals the
+algorithmic read bytes (blob + lengths + object bases) to 0.1 %.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def per_dispatch(d, counter):
+    vals = []
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if "hash_" in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                vals.append(float(row["Counter_Value"]))
+    if not vals:
+        raise SystemExit("no %s rows for the hash kernel under %s" % (counter, d))
+    return sum(vals) / len(vals), len(vals)
+
+
+def main(fetch_dir, write_dir, config, out, objects="10000000"):
+    fetch_kib, nf = per_dispatch(fetch_dir, "FETCH_SIZE")
+    write_kib, nw = per_dispatch(write_dir, "WRITE_SIZE")
+    rec = {"config": config, "objects": int(objects), "dispatches": [nf, nw],
+           "fetch_size_kib": fetch_kib, "write_size_kib": write_kib,
+           "read_bytes": 2 * fetch_kib * 1024, "write_bytes": write_kib * 1024,
+           "traffic_bytes": 2 * fetch_kib * 1024 + write_kib * 1024,
+           "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 wide-read undercount); write = WRITE_SIZE x 1024"}
+    data = {}
+    if os.path.exists(out):
+        data = json.load(open(out))
+    data[config] = rec
+    json.dump(data, open(out, "w"), indent=1)
+    print(json.dumps(rec))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:6])
