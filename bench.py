@@ -204,7 +204,9 @@ def time_host_path(types, blob, base, lens, A, n_host=2_000_000):
         hdx._lib.check(lib.hdx_alloc_pinned(nbytes, ctypes.byref(p)))
         ptrs[name] = p.value
     for name, src in (("blob", blob[:nb]), ("base", base[:n]), ("lens", lens[:n * A])):
-        ctypes.memmove(ptrs[name], src.cpu().numpy().ctypes.data, src.numel() * src.element_size())
+        host = src.cpu().numpy()  # keep the temporary alive across the copy
+        ctypes.memmove(ptrs[name], host.ctypes.data, host.nbytes)
+        del host
     t = np.array(types, np.uint32)
     hdx._lib.check(lib.hdx_hash_batch_host(t.ctypes.data, A, ptrs["blob"], nb, ptrs["base"],
                                            ptrs["lens"], n, ptrs["out"]))
