@@ -42,7 +42,7 @@ def main():
     ap.add_argument("--no-allgather", action="store_true")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip timing the host-resident (PCIe-inclusive) path")
-    ap.add_argument("--traffic", default=os.path.join(ROOT, "profiles", "traffic.json"),
+    ap.add_argument("--traffic", default=latest_traffic_file(),
                     help="HBM bytes/launch measured by scripts/gpu_profile.sh (rocprofv3 PMC)")
     args = ap.parse_args()
 
@@ -177,6 +177,12 @@ def time_allgather(coords, world, dev, backend, max_over_ranks, reps=3):
     nbytes = out.numel() * 8
     return {"ms": round(dt * 1e3, 3), "bytes": nbytes, "backend": backend,
             "busbw_GBps": round(nbytes * (world - 1) / world / dt / 1e9, 2)}
+
+
+def latest_traffic_file():
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")))
+    return files[-1] if files else ""
 
 
 def measured_traffic(path, cfg, n):
