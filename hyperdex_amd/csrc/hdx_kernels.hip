@@ -777,6 +777,160 @@ static hipError_t launch_binned(const BatchArgs& args, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// ===========================================================================
+// Regroup kernel (variants 18/19): a wave owns C consecutive chunks (C*64
+// slots).  Phase 1 computes every slot's {pointer, length, code} as the chunk
+// kernel does (all C length loads issued at once; the carry chains from chunk
+// to chunk in registers) and writes a 16-byte descriptor per slot into the
+// wave's private LDS.  A counting sort by work class (ballot + popcount +
+// mbcnt, wave-local: no workgroup barrier) yields a permutation.  Phase 2
+// hashes C passes of 64 class-sorted slots — the next pass's descriptors and
+// bytes are in flight while the current pass is hashed — and writes each
+// coordinate over its (already consumed) descriptor.  Phase 3 stores the C
+// chunks in slot order, one coalesced 512 B store each.  A wave whose C*64
+// slots all share one class skips the permutation.
+// ===========================================================================
+template <int C>
+struct RegroupLds {
+    SlotDesc desc[4][C * 64];   // reused for the coordinates in phase 2
+    uint16_t perm[4][C * 64];
+};
+
+template <int C, bool NT_STORE>
+__global__ void __launch_bounds__(256)
+hash_regroup_kernel(const BatchArgs args) {
+    __shared__ RegroupLds<C> lds;
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    SlotDesc* desc = lds.desc[w];
+    uint16_t* perm = lds.perm[w];
+    uint64_t* res = reinterpret_cast<uint64_t*>(desc);  // res[2*s] = first 8 bytes of desc[s]
+
+    const uint64_t wave = (uint64_t)blockIdx.x * 4 + w;
+    const uint32_t A = args.A;
+    const uint64_t nslots = args.n * A;
+    const uint64_t qw = wave * (uint64_t)(C * 64);
+    if (qw >= nslots) return;  // no workgroup barrier anywhere: waves are independent
+
+    uint64_t i0;
+    uint32_t j0;
+    split_slot(qw, A, i0, j0);
+    uint32_t carry = 0;
+    for (uint32_t k = 0; k < j0; k += 64) {
+        const uint32_t idx = k + (uint32_t)lane;
+        const uint32_t v = idx < j0 ? args.attr_len[qw - j0 + idx] : 0u;
+        carry += wave_sum_dpp(v);
+    }
+    const uint64_t last_slot = nslots - 1;
+    uint32_t Lraw[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) Lraw[c] = args.attr_len[min(qw + c * 64 + lane, last_slot)];
+    uint32_t packed_codes = 0;
+    if (args.uniform_code == 0xffu) packed_codes = reinterpret_cast<const uint32_t*>(args.codes)[lane];
+
+    // ---- phase 1: descriptors + classes -------------------------------------
+    uint32_t cls[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const uint32_t t = j0 + (uint32_t)(c * 64 + lane);
+        const uint32_t di = t / A;
+        const uint32_t j = t - di * A;
+        const bool valid = qw + c * 64 + lane < nslots;
+        const uint64_t il = valid ? i0 + di : i0;
+        const uint64_t base = args.obj_base[il];
+        const uint32_t L = valid ? Lraw[c] : 0u;
+        const uint32_t Sx = wave_scan_dpp(L) - L;
+        const int head = lane - (int)j;
+        const uint32_t head_sx = __shfl(Sx, head < 0 ? 0 : head, 64);
+        const uint32_t off = head >= 0 ? Sx - head_sx : carry + Sx;
+        carry = __builtin_amdgcn_readlane(off + L, 63);
+        uint32_t code = args.uniform_code != 0xffu
+                            ? args.uniform_code
+                            : (__shfl(packed_codes, (int)(j >> 2), 64) >> (8 * (j & 3))) & 0xffu;
+        if (!valid) code = CODE_ZERO;
+        SlotDesc d;
+        d.p = args.blob + base + off;
+        d.n = L;
+        d.code_slot = code | ((uint32_t)(c * 64 + lane) << 8);
+        desc[c * 64 + lane] = d;
+        cls[c] = work_class(code, L, valid);
+    }
+
+    // ---- counting sort by class (wave-local) ---------------------------------
+    const uint32_t c00 = __builtin_amdgcn_readfirstlane(cls[0]);
+    bool uniform = true;
+#pragma unroll
+    for (int c = 0; c < C; ++c) uniform &= __all(cls[c] == c00);
+    if (!uniform) {
+        uint32_t before = 0;  // slots of lower classes, then of this class in lower chunks
+#pragma unroll
+        for (int k = 0; k < kClasses; ++k) {
+#pragma unroll
+            for (int c = 0; c < C; ++c) {
+                const uint64_t m = __ballot(cls[c] == (uint32_t)k);
+                if (cls[c] == (uint32_t)k) {
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                    perm[before + rank] = (uint16_t)(c * 64 + lane);
+                }
+                before += (uint32_t)__popcll(m);
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // ---- phase 2: C class-homogeneous passes, next pass in flight ------------
+    // A slot's coordinate overwrites the first 8 bytes of its own descriptor,
+    // which exactly one lane has already read (each slot is in one pass).
+    struct Pass {
+        SlotDesc d;
+        Blk blk;
+    };
+    auto load_pass = [&](int t, Pass& P) {
+        const uint32_t s = uniform ? (uint32_t)(t * 64 + lane) : perm[t * 64 + lane];
+        P.d = desc[s];
+        P.blk = issue_block(P.d.code_slot & 0xffu, P.d.p, P.d.n);
+    };
+    bool bad = false;
+    Pass P0, P1;
+    load_pass(0, P0);
+#pragma unroll
+    for (int t = 0; t < C; ++t) {
+        Pass& cur = (t & 1) ? P1 : P0;
+        Pass& nxt = (t & 1) ? P0 : P1;
+        if (t + 1 < C) load_pass(t + 1, nxt);
+        const uint64_t h = hash_blk(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n, cur.blk, bad);
+        res[2 * (cur.d.code_slot >> 8)] = h;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // ---- phase 3: coalesced stores in slot order -----------------------------
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const uint64_t q = qw + c * 64 + lane;
+        if (q < nslots) {
+            const uint64_t h = res[2 * (c * 64 + lane)];
+            if (NT_STORE) __builtin_nontemporal_store(h, args.coords + q);
+            else args.coords[q] = h;
+        }
+    }
+    if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
+}
+
+template <int C, bool NT>
+static hipError_t launch_regroup(const BatchArgs& args, hipStream_t stream) {
+    const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
+    const uint64_t blocks = (waves + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((hash_regroup_kernel<C, NT>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    return hipGetLastError();
+}
+
 template <bool A_, bool B_, bool C_, bool D_ = false>
 static hipError_t launch_t(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n + 63) / 64;
@@ -807,6 +961,8 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 15: return launch_binned<false>(args, stream);
         case 16: return launch_binned<true>(args, stream);
         case 17: return launch_chunk<true, false, true>(args, stream);
+        case 18: return launch_regroup<4, true>(args, stream);
+        case 19: return launch_regroup<8, true>(args, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -815,7 +971,7 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
 // fixed-size numerics, where the 64-objects-per-wave pipelined kernel (8)
 // amortises its per-wave setup better (scripts/ab_variants.py).
 static constexpr int kDefaultVariant = -1;
-static constexpr int kMaxVariant = 17;
+static constexpr int kMaxVariant = 19;
 
 static int g_variant = [] {
     const char* e = getenv("HDX_KERNEL_VARIANT");
