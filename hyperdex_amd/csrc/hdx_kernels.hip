@@ -796,7 +796,7 @@ struct RegroupLds {
     uint16_t perm[4][C * 64];
 };
 
-template <int C, bool NT_STORE>
+template <int C, bool NT_STORE, bool SORT = true>
 __global__ void __launch_bounds__(256)
 hash_regroup_kernel(const BatchArgs args) {
     __shared__ RegroupLds<C> lds;
@@ -861,6 +861,7 @@ hash_regroup_kernel(const BatchArgs args) {
     bool uniform = true;
 #pragma unroll
     for (int c = 0; c < C; ++c) uniform &= __all(cls[c] == c00);
+    if (!SORT) uniform = true;
     if (!uniform) {
         uint32_t before = 0;  // slots of lower classes, then of this class in lower chunks
 #pragma unroll
@@ -921,13 +922,13 @@ hash_regroup_kernel(const BatchArgs args) {
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <int C, bool NT>
+template <int C, bool NT, bool SORT = true>
 static hipError_t launch_regroup(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_regroup_kernel<C, NT>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
     return hipGetLastError();
 }
 
@@ -963,6 +964,9 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 17: return launch_chunk<true, false, true>(args, stream);
         case 18: return launch_regroup<4, true>(args, stream);
         case 19: return launch_regroup<8, true>(args, stream);
+        case 20: return launch_regroup<8, true, false>(args, stream);
+        case 21: return launch_regroup<4, true, false>(args, stream);
+        case 22: return launch_regroup<16, true, false>(args, stream);
         default: return hipErrorInvalidValue;
     }
 }
@@ -971,7 +975,7 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
 // fixed-size numerics, where the 64-objects-per-wave pipelined kernel (8)
 // amortises its per-wave setup better (scripts/ab_variants.py).
 static constexpr int kDefaultVariant = -1;
-static constexpr int kMaxVariant = 19;
+static constexpr int kMaxVariant = 22;
 
 static int g_variant = [] {
     const char* e = getenv("HDX_KERNEL_VARIANT");
