@@ -982,10 +982,30 @@ static int g_variant = [] {
     return e && *e ? atoi(e) : kDefaultVariant;
 }();
 
+// Automatic choice (interleaved A/B on one MI355X, profiles/r1/ab_variants_*.jsonl):
+//  * schemas with timestamps or non-hashable attributes: regroup kernel with the
+//    class sort (19) — their expensive/diverse paths dominate (mixed: -26 %);
+//  * mostly numerics: multi-chunk, 4 chunks per wave (21) (config 2);
+//  * one code everywhere (all strings): multi-chunk without sort, 16 or 8
+//    chunks per wave when the grid stays >= 64 K waves (22/20) (config 3a),
+//    else the one-chunk kernel (12) (config 1);
+//  * otherwise (strings + int64/float, config 3b): one-chunk kernel (12).
 static int auto_variant(const BatchArgs& args) {
     uint32_t numeric = 0;
-    for (uint32_t j = 0; j < args.A; ++j) numeric += args.codes[j] >= CODE_INT64;
-    return 2 * numeric > args.A ? 8 : 12;
+    bool complex_types = false;
+    for (uint32_t j = 0; j < args.A; ++j) {
+        const uint8_t c = args.codes[j];
+        numeric += c >= CODE_INT64;
+        complex_types |= c == CODE_ZERO || c >= CODE_TS_SECOND;
+    }
+    const uint64_t slots = args.n * args.A;
+    if (complex_types) return 19;
+    if (2 * numeric > args.A) return 21;
+    if (args.uniform_code != 0xffu) {
+        if (slots >= (64ull << 20)) return 22;
+        if (slots >= (32ull << 20)) return 20;
+    }
+    return 12;
 }
 
 int hash_variant() { return __atomic_load_n(&g_variant, __ATOMIC_RELAXED); }
