@@ -47,6 +47,9 @@ SIGNATURES = [
     ("hdx_hash_value", _i32, [_u32, _vp, _sz, _vp]),
     ("hdx_hash_key", _i32, [_vp, _u32, _vp, _sz, _vp]),
     ("hdx_hash_object", _i32, [_vp, _u32, _vp, _sz, _vp, _vp, _vp]),
+    ("hdx_region_table_create", _i32, [_u32, _u32, _vp, _vp, _vp, _vp, _vp]),
+    ("hdx_region_table_destroy", _i32, [_vp]),
+    ("hdx_lookup_region_device", _i32, [_vp, _vp, _u32, _u64, _vp, _vp]),
     ("hdx_alloc_pinned", _i32, [_sz, _vp]),
     ("hdx_free_pinned", _i32, [_vp]),
     ("hdx_synth_lengths", _i32, [ctypes.POINTER(SynthRule), _u32, _u64, _u64, _u64, _vp, _vp]),

@@ -493,6 +493,85 @@ HDX_EXPORT hdx_status hdx_synth_fill(const hdx_synth_rule* rules, uint32_t attrs
     return HDX_OK;
 }
 
+// ---- region tables (hdx_regions.hip) ----------------------------------------
+
+struct hdx_region_table_s {
+    int device;
+    uint32_t D, R;
+    uint16_t attrs[16];
+    uint64_t* d_lower;
+    uint64_t* d_upper;
+    uint64_t* d_ids;
+};
+
+HDX_EXPORT hdx_status hdx_region_table_create(uint32_t dims, uint32_t regions, const uint16_t* attrs,
+                                              const uint64_t* lower, const uint64_t* upper,
+                                              const uint64_t* ids, hdx_region_table* out) {
+    if (!out || !attrs || (regions && (!lower || !upper || !ids)))
+        return fail(HDX_E_INVALID, "NULL pointer");
+    if (dims == 0 || dims > 16) return fail(HDX_E_INVALID, "dims=%u outside [1, 16]", dims);
+    *out = nullptr;
+    hdx_status st = bind_device(-1);
+    if (st != HDX_OK) return st;
+    hdx_region_table t = new hdx_region_table_s();
+    t->device = t_state.device;
+    t->D = dims;
+    t->R = regions;
+    std::memcpy(t->attrs, attrs, dims * sizeof(uint16_t));
+    const size_t box = (size_t)regions * dims * 8;
+    if (hipMalloc((void**)&t->d_lower, box + 8) != hipSuccess ||
+        hipMalloc((void**)&t->d_upper, box + 8) != hipSuccess ||
+        hipMalloc((void**)&t->d_ids, (size_t)regions * 8 + 8) != hipSuccess) {
+        (void)hipGetLastError();
+        hdx_region_table_destroy(t);
+        return fail(HDX_E_NOMEM, "region table of %u regions", regions);
+    }
+    if (regions &&
+        (hipMemcpy(t->d_lower, lower, box, hipMemcpyHostToDevice) != hipSuccess ||
+         hipMemcpy(t->d_upper, upper, box, hipMemcpyHostToDevice) != hipSuccess ||
+         hipMemcpy(t->d_ids, ids, (size_t)regions * 8, hipMemcpyHostToDevice) != hipSuccess)) {
+        hdx_region_table_destroy(t);
+        return fail(HDX_E_DEVICE, "region table upload failed");
+    }
+    *out = t;
+    return HDX_OK;
+}
+
+HDX_EXPORT hdx_status hdx_region_table_destroy(hdx_region_table t) {
+    if (!t) return HDX_OK;
+    (void)hipFree(t->d_lower);
+    (void)hipFree(t->d_upper);
+    (void)hipFree(t->d_ids);
+    delete t;
+    return HDX_OK;
+}
+
+HDX_EXPORT hdx_status hdx_lookup_region_device(hdx_region_table t, const uint64_t* coords,
+                                               uint32_t attrs_sz, uint64_t n, uint64_t* region_ids,
+                                               hdx_stream stream) {
+    if (!t) return fail(HDX_E_INVALID, "NULL table");
+    if (n == 0) return HDX_OK;
+    if (!coords || !region_ids) return fail(HDX_E_INVALID, "NULL device pointer");
+    for (uint32_t d = 0; d < t->D; ++d)
+        if (t->attrs[d] >= attrs_sz)
+            return fail(HDX_E_INVALID, "subspace attribute %u >= attrs_sz %u", t->attrs[d], attrs_sz);
+    hdx_status st = bind_device(-1);
+    if (st != HDX_OK) return st;
+    RegionArgs a{};
+    a.lower = t->d_lower;
+    a.upper = t->d_upper;
+    a.ids = t->d_ids;
+    a.coords = coords;
+    a.out = region_ids;
+    a.n = n;
+    a.A = attrs_sz;
+    a.D = t->D;
+    a.R = t->R;
+    std::memcpy(a.attrs, t->attrs, sizeof a.attrs);
+    HIP_TRY(launch_lookup_region(a, (hipStream_t)stream));
+    return HDX_OK;
+}
+
 // ---- tuning hooks (include/hdxhash_debug.h) --------------------------------
 
 HDX_EXPORT int hdxdbg_set_kernel_variant(int variant) { return set_hash_variant(variant); }

@@ -44,6 +44,21 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
 int hash_variant();
 int set_hash_variant(int v);  // -2 if unknown, else the previous selection (-1 = auto)
 
+// Region lookup (hdx_regions.hip): table pointers are device memory owned by
+// an hdx_region_table handle; attrs[] holds the subspace's attribute indices.
+struct RegionArgs {
+    const uint64_t* lower;   // [R*D]
+    const uint64_t* upper;   // [R*D]
+    const uint64_t* ids;     // [R]
+    const uint64_t* coords;  // [n*A]
+    uint64_t* out;           // [n]
+    uint64_t n;
+    uint32_t A, D, R;
+    uint16_t attrs[16];
+};
+
+hipError_t launch_lookup_region(const RegionArgs& a, hipStream_t stream);
+
 struct SynthArgs {
     uint64_t seed;
     uint64_t first;

@@ -1,0 +1,74 @@
+// hdx_regions.hip — coordinates -> region ids on gfx950.
+//
+// configuration::lookup_region (common/configuration.cc:698-735): the first
+// region r of a subspace whose box holds the object's coordinates,
+//   lower[r][a] <= hs[attrs[a]] <= upper[r][a]   for every subspace dimension a,
+// else region_id() (0).  point_leader (:427-497) is the same lookup on subspace
+// 0 (attrs = {0}).  One lane per object; the region table is staged in LDS
+// once per workgroup and every lane walks it in the reference's order, so the
+// table reads are LDS broadcasts.  The region boxes come from
+// admin/partition.cc and are taken as input (coordinator-assigned ids,
+// coordinator/coordinator.cc:586-596), never recomputed here.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hdx_internal.h"
+
+namespace hdx {
+
+constexpr uint32_t kMaxLookupDims = 16;
+
+template <bool IN_LDS>
+__global__ void __launch_bounds__(256)
+lookup_region_kernel(const RegionArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    const uint64_t* lower = a.lower;
+    const uint64_t* upper = a.upper;
+    const uint64_t* ids = a.ids;
+    if (IN_LDS) {
+        const uint32_t box = a.R * a.D;
+        for (uint32_t k = threadIdx.x; k < box; k += blockDim.x) {
+            smem[k] = a.lower[k];
+            smem[box + k] = a.upper[k];
+        }
+        for (uint32_t k = threadIdx.x; k < a.R; k += blockDim.x) smem[2 * box + k] = a.ids[k];
+        __syncthreads();
+        lower = smem;
+        upper = smem + box;
+        ids = smem + 2 * box;
+    }
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    uint64_t h[kMaxLookupDims];
+    const uint64_t* row = a.coords + i * a.A;
+#pragma unroll
+    for (uint32_t d = 0; d < kMaxLookupDims; ++d)
+        if (d < a.D) h[d] = row[a.attrs[d]];
+    uint64_t rid = 0;  // region_id()
+    for (uint32_t r = 0; r < a.R; ++r) {
+        bool match = true;
+#pragma unroll
+        for (uint32_t d = 0; d < kMaxLookupDims; ++d)
+            if (d < a.D) match &= lower[r * a.D + d] <= h[d] && h[d] <= upper[r * a.D + d];
+        if (match) {
+            rid = ids[r];
+            break;
+        }
+    }
+    a.out[i] = rid;
+}
+
+hipError_t launch_lookup_region(const RegionArgs& a, hipStream_t stream) {
+    if (a.n == 0) return hipSuccess;
+    const uint64_t blocks = (a.n + 255) / 256;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    const size_t lds = (size_t)a.R * a.D * 16 + (size_t)a.R * 8;
+    if (lds <= 48 * 1024) {
+        hipLaunchKernelGGL(lookup_region_kernel<true>, dim3((uint32_t)blocks), dim3(256), lds, stream, a);
+    } else {
+        hipLaunchKernelGGL(lookup_region_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace hdx

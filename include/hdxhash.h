@@ -130,6 +130,27 @@ hdx_status hdx_hash_object(const uint32_t* types, uint32_t attrs_sz,
                            const uint8_t* const* values, const size_t* value_lens,
                            uint64_t* hs);
 
+/* ---- coordinates -> regions ------------------------------ */
+
+/* A subspace's region table on the device: `dims` = subspace.attrs.size()
+ * (<= 16), attrs[dims] the schema attribute indices of the subspace
+ * (common/hyperspace.h:99-113), lower/upper[regions*dims] the boxes and
+ * ids[regions] the region ids (region.id, common/hyperspace.h:122-137), all
+ * host arrays, copied at creation. */
+typedef struct hdx_region_table_s* hdx_region_table;
+hdx_status hdx_region_table_create(uint32_t dims, uint32_t regions, const uint16_t* attrs,
+                                   const uint64_t* lower, const uint64_t* upper,
+                                   const uint64_t* ids, hdx_region_table* out);
+hdx_status hdx_region_table_destroy(hdx_region_table table);
+/* configuration::lookup_region (common/configuration.cc:698-735) for n
+ * objects: region_ids[i] = id of the first region whose box holds
+ * coords[i*attrs_sz + attrs[a]] for every a (bounds inclusive), else 0
+ * (region_id()).  Device pointers; asynchronous on `stream`.  With a table
+ * of subspace 0 (attrs = {0}) this is point_leader's region (:427-497). */
+hdx_status hdx_lookup_region_device(hdx_region_table table, const uint64_t* coords,
+                                    uint32_t attrs_sz, uint64_t n, uint64_t* region_ids,
+                                    hdx_stream stream);
+
 /* ---- pinned host memory ------------------------------------------------- */
 
 hdx_status hdx_alloc_pinned(size_t bytes, void** out);

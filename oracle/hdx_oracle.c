@@ -314,3 +314,75 @@ int hdxo_hash_batch(const uint32_t* types, uint32_t A, const uint8_t* blob,
     free(th);
     return err;
 }
+
+/* ---- region grid (admin/partition.cc) --------------------------------- */
+
+/* partition.cc:36-55 */
+static void points(uint64_t intervals, uint64_t* lbs, uint64_t* ubs) {
+    uint64_t interval = (0x8000000000000000ULL / intervals) * 2;
+    for (uint64_t i = 0; i < intervals; ++i) lbs[i] = i * interval;
+    for (uint64_t i = 1; i < intervals; ++i) ubs[i - 1] = lbs[i] - 1;
+    ubs[intervals - 1] = UINT64_MAX;
+}
+
+/* partition.cc:102-135 (recursively_generate :57-100 as an odometer over the
+ * dimensions, first dimension outermost) */
+uint64_t hdxo_partition(uint32_t num_attrs, uint32_t num_servers, uint64_t* lower,
+                        uint64_t* upper, uint64_t max_regions) {
+    if (num_attrs == 0) return 0;
+    double per_dim = pow((double)num_servers, 1 / (double)num_attrs);
+    uint64_t* dims = (uint64_t*)calloc(num_attrs, sizeof(uint64_t));
+    for (uint32_t i = 0; i < num_attrs; ++i) dims[i] = (uint64_t)per_dim;
+    uint64_t partitions = num_attrs * dims[0]; /* sic: partition.cc:109 */
+    for (uint32_t i = 0; partitions < num_servers && i < num_attrs; ++i) {
+        partitions = partitions / dims[i];
+        ++dims[i];
+        partitions = partitions * dims[i];
+    }
+    uint64_t bigger = dims[0], smaller = dims[num_attrs - 1];
+    uint64_t *blb = (uint64_t*)calloc(bigger, 8), *bub = (uint64_t*)calloc(bigger, 8);
+    uint64_t *slb = (uint64_t*)calloc(smaller, 8), *sub = (uint64_t*)calloc(smaller, 8);
+    points(bigger, blb, bub);
+    points(smaller, slb, sub);
+    uint64_t total = 1;
+    for (uint32_t i = 0; i < num_attrs; ++i) total *= dims[i];
+    uint64_t* idx = (uint64_t*)calloc(num_attrs, 8);
+    for (uint64_t r = 0; r < total; ++r) {
+        if (r < max_regions) {
+            for (uint32_t a = 0; a < num_attrs; ++a) {
+                const int big = dims[a] == bigger;
+                lower[r * num_attrs + a] = big ? blb[idx[a]] : slb[idx[a]];
+                upper[r * num_attrs + a] = big ? bub[idx[a]] : sub[idx[a]];
+            }
+        }
+        for (int a = (int)num_attrs - 1; a >= 0; --a) { /* last dimension fastest */
+            if (++idx[a] < dims[a]) break;
+            idx[a] = 0;
+        }
+    }
+    free(dims); free(blb); free(bub); free(slb); free(sub); free(idx);
+    return total;
+}
+
+/* ---- region lookup (common/configuration.cc:698-735) ------------------- */
+
+void hdxo_lookup_region(uint32_t D, uint32_t R, const uint16_t* attrs, const uint64_t* lower,
+                        const uint64_t* upper, const uint64_t* ids, const uint64_t* coords,
+                        uint32_t A, uint64_t n, uint64_t* out) {
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t* hs = coords + i * A;
+        uint64_t rid = 0; /* region_id() */
+        for (uint32_t r = 0; r < R; ++r) {
+            int matches = 1;
+            for (uint32_t a = 0; matches && a < D; ++a) {
+                const uint64_t h = hs[attrs[a]];
+                matches &= lower[(uint64_t)r * D + a] <= h && h <= upper[(uint64_t)r * D + a];
+            }
+            if (matches) {
+                rid = ids[r];
+                break;
+            }
+        }
+        out[i] = rid;
+    }
+}

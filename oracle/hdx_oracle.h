@@ -46,6 +46,21 @@ int hdxo_hash_batch(const uint32_t* types, uint32_t A, const uint8_t* blob,
                     const uint64_t* obj_base, const uint32_t* attr_len,
                     uint64_t n, uint64_t* coords, int nthreads);
 
+/* admin/partition.cc:36-135: the rectilinear region grid HyperDex builds for a
+ * subspace of num_attrs dimensions and num_servers partitions.  Writes up to
+ * max_regions boxes (lower/upper row-major, num_attrs per region) and returns
+ * the number of regions the reference would create. */
+uint64_t hdxo_partition(uint32_t num_attrs, uint32_t num_servers, uint64_t* lower,
+                        uint64_t* upper, uint64_t max_regions);
+
+/* common/configuration.cc:698-735 (lookup_region) for a batch: region r of the
+ * table matches object i when lower[r*D+a] <= coords[i*A+attrs[a]] <=
+ * upper[r*D+a] for every a < D; the first match's id is written, 0
+ * (region_id()) when none matches. */
+void hdxo_lookup_region(uint32_t D, uint32_t R, const uint16_t* attrs, const uint64_t* lower,
+                        const uint64_t* upper, const uint64_t* ids, const uint64_t* coords,
+                        uint32_t A, uint64_t n, uint64_t* out);
+
 #ifdef __cplusplus
 }
 #endif

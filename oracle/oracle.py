@@ -39,6 +39,10 @@ def lib():
         L.hdxo_hash_value.restype = u64
         L.hdxo_hash_batch.argtypes = [vp, u32, vp, vp, vp, u64, vp, ctypes.c_int]
         L.hdxo_hash_batch.restype = ctypes.c_int
+        L.hdxo_partition.argtypes = [u32, u32, vp, vp, u64]
+        L.hdxo_partition.restype = u64
+        L.hdxo_lookup_region.argtypes = [u32, u32, vp, vp, vp, vp, vp, u32, u64, vp]
+        L.hdxo_lookup_region.restype = None
         _LIB = L
     return _LIB
 
@@ -88,3 +92,28 @@ def hash_batch(types, blob, obj_base, attr_len, nthreads=1):
                                 obj_base.ctypes.data, attr_len.ctypes.data, n,
                                 coords.ctypes.data, nthreads)
     return coords.reshape(n, A), err
+
+
+def partition(num_attrs, num_servers):
+    """admin/partition.cc: (lower, upper) as (R, num_attrs) uint64 arrays."""
+    L = lib()
+    R = L.hdxo_partition(num_attrs, num_servers, None, None, 0)
+    lower = np.zeros(R * num_attrs, np.uint64)
+    upper = np.zeros(R * num_attrs, np.uint64)
+    L.hdxo_partition(num_attrs, num_servers, lower.ctypes.data, upper.ctypes.data, R)
+    return lower.reshape(R, num_attrs), upper.reshape(R, num_attrs)
+
+
+def lookup_region(attrs, lower, upper, ids, coords):
+    """configuration::lookup_region over every row of coords (n, A)."""
+    attrs = np.ascontiguousarray(attrs, np.uint16)
+    lower = np.ascontiguousarray(lower, np.uint64)
+    upper = np.ascontiguousarray(upper, np.uint64)
+    ids = np.ascontiguousarray(ids, np.uint64)
+    coords = np.ascontiguousarray(coords, np.uint64)
+    n, A = coords.shape
+    out = np.zeros(n, np.uint64)
+    lib().hdxo_lookup_region(len(attrs), len(ids), attrs.ctypes.data, lower.ctypes.data,
+                             upper.ctypes.data, ids.ctypes.data, coords.ctypes.data, A, n,
+                             out.ctypes.data)
+    return out

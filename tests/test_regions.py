@@ -1,0 +1,107 @@
+"""Region lookup (configuration::lookup_region): oracle semantics
+on CPU, GPU kernel vs oracle on partition() grids and adversarial tables."""
+import numpy as np
+import pytest
+
+U64MAX = np.uint64(0xffffffffffffffff)
+
+
+def test_partition_matches_reference_counts(oracle):
+    """admin/partition.cc quirk (partitions = dims.size()*dims[0], :109)."""
+    counts = {(1, 64): 64, (16, 64): 4, (3, 8): 12, (3, 64): 64}
+    for (a, s), want in counts.items():
+        lo, up = oracle.partition(a, s)
+        assert len(lo) == want
+        # every cell tiles: per dimension the intervals start at 0 and end at 2^64-1
+        assert lo[:, 0].min() == 0 and up[:, 0].max() == U64MAX
+
+
+def test_lookup_semantics_first_match_inclusive(oracle):
+    attrs = [2]
+    lower = np.array([[10], [0], [5]], np.uint64)
+    upper = np.array([[20], [100], [15]], np.uint64)
+    ids = np.array([7, 8, 9], np.uint64)
+    coords = np.zeros((6, 3), np.uint64)
+    coords[:, 2] = [10, 20, 5, 21, 100, 101]
+    got = oracle.lookup_region(attrs, lower, upper, ids, coords)
+    assert list(got) == [7, 7, 8, 8, 8, 0]  # first match wins; inclusive; none -> 0
+
+
+def _grid_table(oracle, dims, servers, attrs, first_id=10):
+    lo, up = oracle.partition(dims, servers)
+    ids = np.arange(first_id, first_id + len(lo), dtype=np.uint64)
+    return attrs, lo, up, ids
+
+
+def _coords(rng, n, A, lo, up, attrs):
+    c = rng.integers(0, 2**64, size=(n, A), dtype=np.uint64)
+    # a quarter of the rows sit exactly on region boundaries
+    k = n // 4
+    for d, a in enumerate(attrs):
+        pick = rng.integers(0, len(lo), k)
+        c[:k // 2, a] = lo[pick[:k // 2], d]
+        c[k // 2:k, a] = up[pick[k // 2:], d]
+    c[0, :] = 0
+    c[1, :] = U64MAX
+    return c
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims,servers,A", [(1, 64, 17), (3, 64, 17), (2, 256, 5), (16, 64, 17),
+                                            (1, 1, 1), (4, 100, 9)])
+def test_gpu_lookup_matches_oracle_on_grids(oracle, dims, servers, A):
+    import torch
+
+    from hyperdex_amd import regions
+    rng = np.random.default_rng(dims * 1000 + servers)
+    attrs = list(rng.choice(A, size=dims, replace=False)) if dims <= A else None
+    attrs, lo, up, ids = _grid_table(oracle, dims, servers, attrs)
+    coords = _coords(rng, 20000, A, lo, up, attrs)
+    want = oracle.lookup_region(attrs, lo, up, ids, coords)
+    t = regions.RegionTable(attrs, lo, up, ids)
+    dev = torch.device("cuda", 0)
+    got = regions.lookup_region(t, torch.from_numpy(coords.view(np.int64)).to(dev))
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().view(np.uint64), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [1, 7, 300, 2500])
+def test_gpu_lookup_overlapping_boxes(oracle, R):
+    """Random overlapping boxes with gaps: first-match order and region_id() = 0
+    must follow the table order exactly (R=2500, D=3 exceeds the LDS path)."""
+    import torch
+
+    from hyperdex_amd import regions
+    rng = np.random.default_rng(R)
+    A, attrs = 6, [5, 0, 3]
+    a = rng.integers(0, 2**64, size=(R, 3), dtype=np.uint64)
+    b = rng.integers(0, 2**64, size=(R, 3), dtype=np.uint64)
+    lo, up = np.minimum(a, b), np.maximum(a, b)
+    ids = rng.integers(1, 2**63, R, dtype=np.uint64)
+    coords = _coords(rng, 30000, A, lo, up, attrs)
+    want = oracle.lookup_region(attrs, lo, up, ids, coords)
+    assert (want == 0).any() or R < 50
+    t = regions.RegionTable(attrs, lo, up, ids)
+    got = regions.lookup_region(t, torch.from_numpy(coords.view(np.int64)).to(torch.device("cuda", 0)))
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().view(np.uint64), want)
+
+
+@pytest.mark.gpu
+def test_gpu_hash_then_point_leader(oracle):
+    """hash -> lookup on subspace 0 (point_leader's region step) end to end."""
+    import torch
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import regions, synth
+    dev = torch.device("cuda", 0)
+    types, blob, base, lens = synth.make_batch_device("cfg3b", 50000, device=dev)
+    coords = hdx.hash_batch(types, blob, base, lens)
+    lo, up = oracle.partition(1, 64)
+    ids = np.arange(2, 66, dtype=np.uint64)
+    got = regions.lookup_region(regions.RegionTable([0], lo, up, ids), coords)
+    torch.cuda.synchronize()
+    want = oracle.lookup_region([0], lo, up, ids, coords.cpu().numpy().view(np.uint64))
+    assert np.array_equal(got.cpu().numpy().view(np.uint64), want)
+    assert (want != 0).all()  # the key grid covers the whole space
