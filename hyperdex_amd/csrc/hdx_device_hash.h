@@ -6,10 +6,10 @@
 //   ordered_encode_double      common/ordered_encoding.cc:114-161
 //   timestamp calendar hash    common/datatype_timestamp.cc:117-219
 //
-// Memory access: string bytes are read as 16-byte vectors (global_load_dwordx4
-// at any byte alignment; gfx950 runs in unaligned mode) — one 64-byte block
-// is four loads.  Scalar 64-bit multiplies lower to v_mad_u64_u32 +
-// v_mul_lo_u32 pairs; rotates to v_alignbit_b32; bswap to v_perm_b32.
+// Register-fed: the callers (hdx_kernels.hip) load the bytes; the 0..16-byte
+// and > 64-byte CityHash regimes, which need the loads interleaved with the
+// arithmetic, live there.  64-bit multiplies lower to v_mad_u64_u32 +
+// v_mul_lo_u32; rotates to v_alignbit_b32; bswap to v_perm_b32.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -30,22 +30,6 @@ __device__ __forceinline__ uint64_t ror(uint64_t v, int r) { return (v >> r) | (
 __device__ __forceinline__ uint64_t shiftmix(uint64_t v) { return v ^ (v >> 47); }
 __device__ __forceinline__ uint64_t bswap(uint64_t v) { return __builtin_bswap64(v); }
 
-__device__ __forceinline__ uint64_t ld8(const uint8_t* p) {
-    uint64_t v;
-    __builtin_memcpy(&v, p, 8);
-    return v;
-}
-__device__ __forceinline__ uint32_t ld4(const uint8_t* p) {
-    uint32_t v;
-    __builtin_memcpy(&v, p, 4);
-    return v;
-}
-__device__ __forceinline__ u64x2 ld16(const uint8_t* p) {
-    u64x2 v;
-    __builtin_memcpy(&v, p, 16);
-    return v;
-}
-
 // city.cc:268-276 (and Hash128to64 with mul = KMUL)
 __device__ __forceinline__ uint64_t mix16(uint64_t u, uint64_t v, uint64_t mul) {
     uint64_t a = (u ^ v) * mul;
@@ -53,28 +37,6 @@ __device__ __forceinline__ uint64_t mix16(uint64_t u, uint64_t v, uint64_t mul) 
     uint64_t b = (v ^ a) * mul;
     b ^= b >> 47;
     return b * mul;
-}
-
-// city.cc:278-301
-__device__ __forceinline__ uint64_t city_le16(const uint8_t* s, uint32_t n) {
-    const uint64_t mul = K2 + 2ull * n;
-    if (n >= 8) {
-        uint64_t a = ld8(s) + K2;
-        uint64_t b = ld8(s + n - 8);
-        uint64_t c = ror(b, 37) * mul + a;
-        uint64_t d = (ror(a, 25) + b) * mul;
-        return mix16(c, d, mul);
-    }
-    if (n >= 4) {
-        uint64_t a = ld4(s);
-        return mix16(n + (a << 3), ld4(s + n - 4), mul);
-    }
-    if (n > 0) {
-        uint32_t y = (uint32_t)s[0] + ((uint32_t)s[n >> 1] << 8);
-        uint32_t z = n + ((uint32_t)s[n - 1] << 2);
-        return shiftmix((uint64_t)y * K2 ^ (uint64_t)z * K0) * K2;
-    }
-    return K2;
 }
 
 // city.cc:305-313, operands as two 16-byte vectors: lo = s[0,16), hi = s[n-16,n)
@@ -120,45 +82,6 @@ __device__ __forceinline__ void weak32(uint64_t w, uint64_t x, uint64_t y, uint6
     b += ror(a, 44);
     o0 = a + z;
     o1 = b + c;
-}
-
-// city.cc:361-397, len > 64
-__device__ __forceinline__ uint64_t city_gt64(const uint8_t* s, uint32_t n) {
-    // Tail block s[n-64, n) as four 16-byte loads.
-    const u64x2 e0 = ld16(s + n - 64), e1 = ld16(s + n - 48);
-    const u64x2 e2 = ld16(s + n - 32), e3 = ld16(s + n - 16);
-    // e0 = {n-64, n-56}, e1 = {n-48, n-40}, e2 = {n-32, n-24}, e3 = {n-16, n-8}
-    uint64_t x = e1.y;
-    uint64_t y = e3.x + e0.y;
-    uint64_t z = mix16(e1.x + n, e2.y, KMUL);
-    uint64_t v0, v1, w0, w1;
-    weak32(e0.x, e0.y, e1.x, e1.y, n, z, v0, v1);
-    weak32(e2.x, e2.y, e3.x, e3.y, y + K1, x, w0, w1);
-    x = x * K1 + ld8(s);
-
-    uint32_t blocks = (n - 1) >> 6;  // (len-1) & ~63, in 64-byte blocks
-    for (uint32_t k = 0; k < blocks; ++k, s += 64) {
-        const u64x2 b0 = ld16(s), b1 = ld16(s + 16), b2 = ld16(s + 32), b3 = ld16(s + 48);
-        x = ror(x + y + v0 + b0.y, 37) * K1;
-        y = ror(y + v1 + b3.x, 42) * K1;
-        x ^= w1;
-        y += v0 + b2.y;
-        z = ror(z + w0, 33) * K1;
-        uint64_t nv0, nv1, nw0, nw1;
-        weak32(b0.x, b0.y, b1.x, b1.y, v1 * K1, x + w0, nv0, nv1);
-        weak32(b2.x, b2.y, b3.x, b3.y, z + w1, y + b1.x, nw0, nw1);
-        v0 = nv0; v1 = nv1; w0 = nw0; w1 = nw1;
-        uint64_t t = z; z = x; x = t;
-    }
-    return mix16(mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z, mix16(v1, w1, KMUL) + x, KMUL);
-}
-
-// CityHash64 (city.cc:361-397) over global memory at any alignment.
-__device__ __forceinline__ uint64_t cityhash64(const uint8_t* s, uint32_t n) {
-    if (n <= 16) return city_le16(s, n);
-    if (n <= 32) return city_17to32(ld16(s), ld16(s + n - 16), n);
-    if (n <= 64) return city_33to64(ld16(s), ld16(s + 16), ld16(s + n - 32), ld16(s + n - 16), n);
-    return city_gt64(s, n);
 }
 
 // ordered_encoding.cc:43-49: x + (x >= 0 ? 2^63 : INT64_MIN) == x ^ 2^63 (mod 2^64)

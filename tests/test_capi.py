@@ -101,5 +101,6 @@ def test_variant_hook():
     lib = hdx.lib()
     cur = lib.hdxdbg_kernel_variant()
     assert lib.hdxdbg_set_kernel_variant(999) == -2
-    assert lib.hdxdbg_set_kernel_variant(0) == cur
-    assert lib.hdxdbg_set_kernel_variant(cur) == 0
+    assert lib.hdxdbg_set_kernel_variant(0) == -2  # retired variant
+    assert lib.hdxdbg_set_kernel_variant(12) == cur
+    assert lib.hdxdbg_set_kernel_variant(cur) == 12
