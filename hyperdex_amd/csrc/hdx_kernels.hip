@@ -430,7 +430,19 @@ hash_regroup_kernel(const BatchArgs args) {
         Pass& nxt = (t & 1) ? P0 : P1;
         if (t + 1 < C) load_pass(t + 1, nxt);
         const uint64_t h = hash_blk(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n, cur.blk, bad);
-        res[2 * (cur.d.code_slot >> 8)] = h;
+        if (uniform) {  // pass t is chunk t in slot order: store straight to HBM
+            const uint64_t q = qw + t * 64 + lane;
+            if (q < nslots) {
+                if (NT_STORE) __builtin_nontemporal_store(h, args.coords + q);
+                else args.coords[q] = h;
+            }
+        } else {
+            res[2 * (cur.d.code_slot >> 8)] = h;
+        }
+    }
+    if (uniform) {
+        if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
+        return;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

@@ -69,3 +69,21 @@ def test_allgather_matches_single_process(world):
     ret = ctx.Manager().dict()
     mp.start_processes(_worker, args=(world, _free_port(), ret), nprocs=world, start_method="spawn")
     assert all(ret[r] for r in range(world))
+
+
+@pytest.mark.gpu
+def test_hash_sharded_rccl_world1():
+    """The RCCL branch of allgather_coords / hash_sharded in one process."""
+    from hyperdex_amd import hashing
+    dev = torch.device("cuda", 0)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        types, blob, base, lens = synth.make_batch_device("cfg3b", 5000, device=dev)
+        full = hdist.hash_sharded(types, blob, base, lens, [5000])
+        want = hashing.hash_batch(types, blob, base, lens)
+        torch.cuda.synchronize()
+        assert torch.equal(full, want)
+    finally:
+        dist.destroy_process_group()
