@@ -323,7 +323,7 @@ struct RegroupLds {
     uint16_t perm[4][C * 64];
 };
 
-template <int C, bool NT_STORE, bool SORT = true>
+template <int C, bool NT_STORE, bool SORT = true, bool DIRECT = true>
 __global__ void __launch_bounds__(256)
 hash_regroup_kernel(const BatchArgs args) {
     __shared__ RegroupLds<C> lds;
@@ -430,7 +430,7 @@ hash_regroup_kernel(const BatchArgs args) {
         Pass& nxt = (t & 1) ? P0 : P1;
         if (t + 1 < C) load_pass(t + 1, nxt);
         const uint64_t h = hash_blk(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n, cur.blk, bad);
-        if (uniform) {  // pass t is chunk t in slot order: store straight to HBM
+        if (DIRECT && uniform) {  // pass t is chunk t in slot order: store straight to HBM
             const uint64_t q = qw + t * 64 + lane;
             if (q < nslots) {
                 if (NT_STORE) __builtin_nontemporal_store(h, args.coords + q);
@@ -440,7 +440,7 @@ hash_regroup_kernel(const BatchArgs args) {
             res[2 * (cur.d.code_slot >> 8)] = h;
         }
     }
-    if (uniform) {
+    if (DIRECT && uniform) {
         if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
         return;
     }
@@ -461,13 +461,13 @@ hash_regroup_kernel(const BatchArgs args) {
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <int C, bool NT, bool SORT = true>
+template <int C, bool NT, bool SORT = true, bool DIRECT = true>
 static hipError_t launch_regroup(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT, DIRECT>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
     return hipGetLastError();
 }
 
@@ -489,12 +489,15 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 20: return launch_regroup<8, true, false>(args, stream);
         case 21: return launch_regroup<4, true, false>(args, stream);
         case 22: return launch_regroup<16, true, false>(args, stream);
+        case 23: return launch_regroup<8, true, false, false>(args, stream);
+        case 24: return launch_regroup<4, true, false, false>(args, stream);
+        case 25: return launch_regroup<16, true, false, false>(args, stream);
         default: return hipErrorInvalidValue;
     }
 }
 
 static constexpr int kDefaultVariant = -1;  // automatic
-static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 22); }
+static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 25); }
 
 static int g_variant = [] {
     const char* e = getenv("HDX_KERNEL_VARIANT");
