@@ -506,11 +506,13 @@ static int g_variant = [] {
 
 // Automatic choice (interleaved A/B on one MI355X, profiles/r1/ab_variants_*.jsonl):
 //  * schemas with timestamps or non-hashable attributes: regroup kernel with the
-//    class sort (19) — their expensive/diverse paths dominate (mixed: -26 %);
-//  * mostly numerics: multi-chunk, 4 chunks per wave (21) (config 2);
-//  * one code everywhere (all strings): multi-chunk without sort, 16 or 8
-//    chunks per wave when the grid stays >= 64 K waves (22/20) (config 3a),
-//    else the one-chunk kernel (12) (config 1);
+//    class sort, 8 chunks per wave (19) — their diverse paths dominate (mixed: -26 %);
+//  * mostly numerics: regroup unsorted, 4 chunks per wave, direct stores (21)
+//    (config 2: 0.31 vs 0.42 ms);
+//  * one code everywhere (all strings): regroup unsorted with 16 chunks per wave
+//    and burst stores (25) when the grid keeps >= 64 K waves, 8 chunks (20) from
+//    32 M slots (config 3a: 2.24 vs 2.38 ms), else the one-chunk kernel (12)
+//    (config 1);
 //  * otherwise (strings + int64/float, config 3b): one-chunk kernel (12).
 static int auto_variant(const BatchArgs& args) {
     uint32_t numeric = 0;
@@ -524,7 +526,7 @@ static int auto_variant(const BatchArgs& args) {
     if (complex_types) return 19;
     if (2 * numeric > args.A) return 21;
     if (args.uniform_code != 0xffu) {
-        if (slots >= (64ull << 20)) return 22;
+        if (slots >= (64ull << 20)) return 25;
         if (slots >= (32ull << 20)) return 20;
     }
     return 12;
