@@ -17,11 +17,13 @@ HDX_E_BADSIZE = 2
 HDX_E_DEVICE = 3
 HDX_E_INVALID = 4
 HDX_E_NOMEM = 5
+HDX_E_BADENC = 6
 HDX_MAX_ATTRS = 256
 
 STATUS_NAMES = {
     HDX_OK: "HDX_OK", HDX_E_BADTYPE: "HDX_E_BADTYPE", HDX_E_BADSIZE: "HDX_E_BADSIZE",
     HDX_E_DEVICE: "HDX_E_DEVICE", HDX_E_INVALID: "HDX_E_INVALID", HDX_E_NOMEM: "HDX_E_NOMEM",
+    HDX_E_BADENC: "HDX_E_BADENC",
 }
 
 # Every symbol include/hdxhash.h declares: (name, restype, argtypes)
@@ -43,6 +45,9 @@ SIGNATURES = [
     ("hdx_schema_check", _i32, [_vp, _u32]),
     ("hdx_type_hashable", _i32, [_u32]),
     ("hdx_hash_batch_device", _i32, [_vp, _u32, _vp, _vp, _vp, _u64, _vp, _vp, _vp]),
+    ("hdx_hash_encoded_device", _i32, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp,
+                                       _vp, _vp]),
+    ("hdx_synth_encode_values", _i32, [_vp, _vp, _vp, _u32, _u64, _u64, _vp, _vp, _vp]),
     ("hdx_hash_batch_host", _i32, [_vp, _u32, _vp, _u64, _vp, _vp, _u64, _vp]),
     ("hdx_hash_value", _i32, [_u32, _vp, _sz, _vp]),
     ("hdx_hash_key", _i32, [_vp, _u32, _vp, _sz, _vp]),

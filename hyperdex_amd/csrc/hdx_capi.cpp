@@ -378,6 +378,35 @@ HDX_EXPORT hdx_status hdx_hash_batch_device(const uint32_t* types, uint32_t attr
     return HDX_OK;
 }
 
+HDX_EXPORT hdx_status hdx_hash_encoded_device(const uint32_t* types, uint32_t attrs_sz,
+                                              const uint8_t* keys, const uint64_t* key_off,
+                                              const uint32_t* key_len, const uint8_t* vals,
+                                              const uint64_t* val_off, const uint32_t* val_len,
+                                              uint64_t n, uint64_t* coords, uint64_t* versions,
+                                              uint32_t* status_dev, hdx_stream stream) {
+    EncodedArgs a{};
+    hdx_status st = check_schema(types, attrs_sz, a.codes);
+    if (st != HDX_OK) return st;
+    if (attrs_sz > 128) return fail(HDX_E_INVALID, "attrs_sz=%u > 128 for stored objects", attrs_sz);
+    if (n == 0) return HDX_OK;
+    if (!keys || !key_off || !key_len || !vals || !val_off || !val_len || !coords)
+        return fail(HDX_E_INVALID, "NULL device pointer");
+    if ((st = bind_device(-1)) != HDX_OK) return st;
+    a.keys = keys;
+    a.key_off = key_off;
+    a.key_len = key_len;
+    a.vals = vals;
+    a.val_off = val_off;
+    a.val_len = val_len;
+    a.coords = coords;
+    a.versions = versions;
+    a.status = status_dev;
+    a.n = n;
+    a.A = attrs_sz;
+    HIP_TRY(launch_hash_encoded(a, (hipStream_t)stream));
+    return HDX_OK;
+}
+
 HDX_EXPORT hdx_status hdx_hash_batch_host(const uint32_t* types, uint32_t attrs_sz,
                                           const uint8_t* blob, uint64_t blob_bytes,
                                           const uint64_t* obj_base, const uint32_t* attr_len,
@@ -465,6 +494,18 @@ static hdx_status synth_args(const hdx_synth_rule* rules, uint32_t A, uint64_t s
             return fail(HDX_E_INVALID, "synth: bad rule at %u", j);
         a->rules[j] = rules[j];
     }
+    return HDX_OK;
+}
+
+HDX_EXPORT hdx_status hdx_synth_encode_values(const uint8_t* blob_dev, const uint64_t* obj_base_dev,
+                                              const uint32_t* attr_len_dev, uint32_t attrs_sz, uint64_t n,
+                                              uint64_t first_version, const uint64_t* val_off_dev,
+                                              uint8_t* vals_dev, hdx_stream stream) {
+    if (attrs_sz == 0 || attrs_sz > 65535) return fail(HDX_E_INVALID, "attrs_sz=%u", attrs_sz);
+    hdx_status st = bind_device(-1);
+    if (st != HDX_OK) return st;
+    HIP_TRY(launch_synth_encode(blob_dev, obj_base_dev, attr_len_dev, attrs_sz, n, first_version,
+                                val_off_dev, vals_dev, (hipStream_t)stream));
     return HDX_OK;
 }
 

@@ -59,6 +59,25 @@ struct RegionArgs {
 
 hipError_t launch_lookup_region(const RegionArgs& a, hipStream_t stream);
 
+// Stored-object sweep (hdx_encoded.hip): device arrays.
+struct EncodedArgs {
+    const uint8_t* keys;
+    const uint64_t* key_off;
+    const uint32_t* key_len;
+    const uint8_t* vals;
+    const uint64_t* val_off;
+    const uint32_t* val_len;
+    uint64_t* coords;
+    uint64_t* versions;  // may be NULL
+    uint32_t* status;    // may be NULL
+    uint64_t n;
+    uint32_t A;
+    uint32_t pad_;
+    uint8_t codes[HDX_MAX_ATTRS];
+};
+
+hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream);
+
 struct SynthArgs {
     uint64_t seed;
     uint64_t first;
@@ -71,6 +90,10 @@ struct SynthArgs {
 hipError_t launch_synth_lengths(const SynthArgs& a, uint32_t* attr_len, hipStream_t s);
 hipError_t launch_synth_fill(const SynthArgs& a, const uint64_t* obj_base, const uint32_t* attr_len,
                              uint8_t* blob, uint64_t bytes, hipStream_t s);
+
+hipError_t launch_synth_encode(const uint8_t* blob, const uint64_t* obj_base, const uint32_t* attr_len,
+                               uint32_t A, uint64_t n, uint64_t first_version, const uint64_t* val_off,
+                               uint8_t* vals, hipStream_t s);
 
 // hyperdatatype -> dispatch code; -1 for an id datatype_info::lookup rejects.
 int type_code(uint32_t type);

@@ -95,6 +95,48 @@ __global__ void synth_numeric_kernel(const SynthArgs a, const uint64_t* obj_base
     }
 }
 
+// daemon/datalayer_encodings.cc:139-166 (encode_value) for object i of a
+// packed batch: attributes 1..A-1 become the value (attribute 0 is the key).
+__global__ void synth_encode_kernel(const uint8_t* blob, const uint64_t* obj_base, const uint32_t* attr_len,
+                                    uint32_t A, uint64_t n, uint64_t first_version, const uint64_t* val_off,
+                                    uint8_t* vals) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint8_t* o = vals + val_off[i];
+    const uint64_t ver = first_version + i;
+    for (int b = 0; b < 8; ++b) o[b] = (uint8_t)(ver >> (56 - 8 * b));
+    o[8] = (uint8_t)((A - 1) >> 8);
+    o[9] = (uint8_t)(A - 1);
+    o += 10;
+    const uint8_t* src = blob + obj_base[i] + attr_len[i * A];
+    for (uint32_t j = 1; j < A; ++j) {
+        const uint32_t L = attr_len[i * A + j];
+        o[0] = (uint8_t)(L >> 24);
+        o[1] = (uint8_t)(L >> 16);
+        o[2] = (uint8_t)(L >> 8);
+        o[3] = (uint8_t)L;
+        o += 4;
+        uint32_t k = 0;
+        for (; k + 8 <= L; k += 8) {
+            uint64_t w;
+            __builtin_memcpy(&w, src + k, 8);
+            __builtin_memcpy(o + k, &w, 8);
+        }
+        for (; k < L; ++k) o[k] = src[k];
+        o += L;
+        src += L;
+    }
+}
+
+hipError_t launch_synth_encode(const uint8_t* blob, const uint64_t* obj_base, const uint32_t* attr_len,
+                               uint32_t A, uint64_t n, uint64_t first_version, const uint64_t* val_off,
+                               uint8_t* vals, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(synth_encode_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, blob, obj_base,
+                       attr_len, A, n, first_version, val_off, vals);
+    return hipGetLastError();
+}
+
 static uint32_t grid_for(uint64_t work, uint32_t block) {
     uint64_t g = (work + block - 1) / block;
     if (g > 65536) g = 65536;

@@ -110,3 +110,29 @@ def hash_batch_host(types, blob, obj_base, attr_len, out: Optional[np.ndarray] =
                                     blob.size, obj_base.ctypes.data, attr_len.ctypes.data, n,
                                     out.ctypes.data))
     return out
+
+
+def hash_encoded(types, keys, key_off, key_len, vals, val_off, val_len, coords=None,
+                 versions=None, status=None, stream=None):
+    """Reindex sweep over stored objects (hdx_hash_encoded_device): values in the
+    daemon's on-disk encoding (daemon/datalayer_encodings.cc:139-217) and keys,
+    as torch HIP tensors; returns coords (n, A) int64 (uint64 bit patterns)."""
+    import torch
+
+    t = _u32_array(types)
+    A = len(t)
+    n = val_off.numel()
+    assert key_off.numel() == n and key_len.numel() == n and val_len.numel() == n
+    for x in (keys, key_off, key_len, vals, val_off, val_len):
+        assert x.is_cuda and x.is_contiguous()
+    if coords is None:
+        coords = torch.empty((n, A), dtype=torch.int64, device=val_off.device)
+    if stream is None:
+        stream = torch.cuda.current_stream(val_off.device)
+    handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+    check(lib().hdx_hash_encoded_device(
+        t.ctypes.data, A, keys.data_ptr(), key_off.data_ptr(), key_len.data_ptr(), vals.data_ptr(),
+        val_off.data_ptr(), val_len.data_ptr(), n, coords.data_ptr(),
+        versions.data_ptr() if versions is not None else None,
+        status.data_ptr() if status is not None else None, handle))
+    return coords

@@ -191,3 +191,56 @@ def make_batch_device(name_or_rules, n: int, seed: int = SEED, first: int = 0, d
                                blob.data_ptr(), total, stream))
     types = np.array([r.type for r in rules], dtype=np.uint32)
     return types, blob, obj_base, attr_len
+
+
+def encode_values_host(types, blob, obj_base, attr_len, first_version=0):
+    """daemon/datalayer_encodings.cc:139-166 (encode_value) on the host: the
+    packed batch's attribute 0 becomes the key, attributes 1..A-1 the value.
+    Returns (keys, key_off, key_len, vals, val_off, val_len) numpy arrays."""
+    A = len(types)
+    n = len(obj_base)
+    Lm = attr_len.reshape(n, A).astype(np.uint64)
+    key_off = obj_base.astype(np.uint64)
+    key_len = Lm[:, 0].astype(np.uint32)
+    val_len = (10 + (4 + Lm[:, 1:]).sum(axis=1)).astype(np.uint32)
+    val_off = np.zeros(n, np.uint64)
+    if n > 1:
+        val_off[1:] = np.cumsum(val_len[:-1].astype(np.uint64))
+    vals = np.zeros(int(val_len.astype(np.uint64).sum()) if n else 0, np.uint8)
+    for i in range(n):
+        o = int(val_off[i])
+        vals[o:o + 8] = np.frombuffer(int(first_version + i).to_bytes(8, "big"), np.uint8)
+        vals[o + 8:o + 10] = np.frombuffer((A - 1).to_bytes(2, "big"), np.uint8)
+        o += 10
+        src = int(obj_base[i]) + int(Lm[i, 0])
+        for j in range(1, A):
+            L = int(Lm[i, j])
+            vals[o:o + 4] = np.frombuffer(L.to_bytes(4, "big"), np.uint8)
+            vals[o + 4:o + 4 + L] = blob[src:src + L]
+            o += 4 + L
+            src += L
+    return blob, key_off, key_len, vals, val_off, val_len
+
+
+def make_encoded_device(name_or_rules, n: int, seed: int = SEED, first: int = 0, device=None):
+    """A packed synthetic batch re-encoded as stored objects in HBM (config 5):
+    returns (types, keys, key_off, key_len, vals, val_off, val_len) with
+    keys = the batch blob (key_off = obj_base), values in a new buffer."""
+    import torch
+
+    from ._lib import check, lib
+
+    types, blob, obj_base, attr_len = make_batch_device(name_or_rules, n, seed, first, device)
+    A = len(types)
+    L = attr_len.view(n, A).to(torch.int64)
+    key_len = attr_len.view(n, A)[:, 0].contiguous()
+    val_len64 = 10 + (4 + L[:, 1:]).sum(dim=1)
+    val_off = torch.zeros(n, dtype=torch.int64, device=blob.device)
+    if n > 1:
+        val_off[1:] = torch.cumsum(val_len64[:-1], dim=0)
+    total = int(val_len64.sum().item()) if n else 0
+    vals = torch.empty(max(total, 1), dtype=torch.uint8, device=blob.device)
+    stream = torch.cuda.current_stream(blob.device).cuda_stream
+    check(lib().hdx_synth_encode_values(blob.data_ptr(), obj_base.data_ptr(), attr_len.data_ptr(), A, n,
+                                        first, val_off.data_ptr(), vals.data_ptr(), stream))
+    return (types, blob, obj_base, key_len, vals, val_off, val_len64.to(torch.int32))

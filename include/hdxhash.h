@@ -60,7 +60,8 @@ typedef enum hdx_status {
     HDX_E_BADSIZE = 2,     /* int64/float/timestamp value of size not in {0, 8} */
     HDX_E_DEVICE = 3,      /* no usable device, or a HIP runtime error */
     HDX_E_INVALID = 4,     /* bad argument: NULL pointer, A == 0, A > HDX_MAX_ATTRS */
-    HDX_E_NOMEM = 5        /* device or pinned allocation failed */
+    HDX_E_NOMEM = 5,       /* device or pinned allocation failed */
+    HDX_E_BADENC = 6       /* a stored value does not decode (hdx_hash_encoded_device) */
 } hdx_status;
 
 /* An opaque hipStream_t.  NULL is the HIP null (default) stream. */
@@ -115,6 +116,26 @@ hdx_status hdx_hash_batch_host(const uint32_t* types, uint32_t attrs_sz,
                                const uint8_t* blob, uint64_t blob_bytes,
                                const uint64_t* obj_base, const uint32_t* attr_len,
                                uint64_t n, uint64_t* coords);
+
+/* Reindex sweep over stored objects: value i is
+ * vals[val_off[i], +val_len[i]) in the daemon's on-disk encoding
+ * [u64 BE version][u16 BE count]{[u32 BE len][bytes]}*count
+ * (daemon/datalayer_encodings.cc:139-217), key i is keys[key_off[i],
+ * +key_len[i]).  Decodes and hashes every object in one launch:
+ * coords[i*A + 0] = hash(types[0], key), coords[i*A + 1 + k] =
+ * hash(types[1+k], attribute k); versions[i] (may be NULL) = the value's
+ * version.  An object whose value does not decode into exactly A-1
+ * attributes lying inside its bytes gets zero coordinates (and version 0)
+ * and (1u << HDX_E_BADENC) is ORed into status_dev (may be NULL).  The
+ * reference's decode_value does not check that the last attribute ends
+ * inside the value (:201-213); this does.  Device pointers, asynchronous;
+ * attrs_sz <= 128. */
+hdx_status hdx_hash_encoded_device(const uint32_t* types, uint32_t attrs_sz,
+                                   const uint8_t* keys, const uint64_t* key_off,
+                                   const uint32_t* key_len, const uint8_t* vals,
+                                   const uint64_t* val_off, const uint32_t* val_len,
+                                   uint64_t n, uint64_t* coords, uint64_t* versions,
+                                   uint32_t* status_dev, hdx_stream stream);
 
 /* ---- per-value / per-object (the reference signatures, C form) ---------- */
 
@@ -177,6 +198,14 @@ hdx_status hdx_synth_fill(const hdx_synth_rule* rules, uint32_t attrs_sz, uint64
                           uint64_t first, uint64_t n, const uint64_t* obj_base_dev,
                           const uint32_t* attr_len_dev, uint8_t* blob_dev, uint64_t bytes,
                           hdx_stream stream);
+
+/* Encode objects of a packed batch into stored values (the encode_value
+ * format above), version first_version + i, at vals_dev + val_off_dev[i];
+ * val_off must hold room for 10 + sum_{j>=1}(4 + attr_len[i*A+j]) bytes each. */
+hdx_status hdx_synth_encode_values(const uint8_t* blob_dev, const uint64_t* obj_base_dev,
+                                   const uint32_t* attr_len_dev, uint32_t attrs_sz, uint64_t n,
+                                   uint64_t first_version, const uint64_t* val_off_dev,
+                                   uint8_t* vals_dev, hdx_stream stream);
 
 #ifdef __cplusplus
 }

@@ -10,6 +10,8 @@
 #define _GNU_SOURCE
 #include "hdx_oracle.h"
 
+#define HDXO_MAX_ATTRS 256
+
 #include <math.h>
 #include <pthread.h>
 #include <stdlib.h>
@@ -385,4 +387,61 @@ void hdxo_lookup_region(uint32_t D, uint32_t R, const uint16_t* attrs, const uin
         }
         out[i] = rid;
     }
+}
+
+/* ---- stored objects (daemon/datalayer_encodings.cc:139-217) ------------ */
+
+static uint64_t be64(const uint8_t* p) {
+    uint64_t v = 0;
+    for (int i = 0; i < 8; ++i) v = (v << 8) | p[i];
+    return v;
+}
+static uint32_t be32(const uint8_t* p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+int64_t hdxo_hash_encoded(const uint32_t* types, uint32_t A, const uint8_t* keys,
+                          const uint64_t* key_off, const uint32_t* key_len, const uint8_t* vals,
+                          const uint64_t* val_off, const uint32_t* val_len, uint64_t n,
+                          uint64_t* coords, uint64_t* versions, uint8_t* bad) {
+    int64_t nbad = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        uint64_t* hs = coords + i * A;
+        const uint8_t* v = vals + val_off[i];
+        const uint8_t* end = v + val_len[i];
+        const uint8_t* ptr = v;
+        int ok = 1;
+        uint64_t version = 0;
+        /* :174-181 version, :185-192 count */
+        if (ptr + 8 <= end) { version = be64(ptr); ptr += 8; } else ok = 0;
+        uint32_t count = 0;
+        if (ok && ptr + 2 <= end) { count = ((uint32_t)ptr[0] << 8) | ptr[1]; ptr += 2; } else ok = 0;
+        if (ok && count != A - 1) ok = 0; /* the schema's value attributes */
+        const uint8_t* attr_p[HDXO_MAX_ATTRS];
+        uint32_t attr_n[HDXO_MAX_ATTRS];
+        for (uint32_t k = 0; ok && k < count; ++k) {
+            /* :198-213; unlike the reference, the attribute must end inside the value */
+            if (ptr + 4 > end) { ok = 0; break; }
+            attr_n[k] = be32(ptr);
+            ptr += 4;
+            if ((uint64_t)(end - ptr) < attr_n[k]) { ok = 0; break; }
+            attr_p[k] = ptr;
+            ptr += attr_n[k];
+        }
+        if (versions) versions[i] = ok ? version : 0;
+        bad[i] = !ok;
+        if (!ok) {
+            for (uint32_t j = 0; j < A; ++j) hs[j] = 0;
+            ++nbad;
+            continue;
+        }
+        int e;
+        hs[0] = hdxo_hash_value(types[0], keys + key_off[i], key_len[i], &e);
+        if (e) return -1;
+        for (uint32_t k = 0; k + 1 < A; ++k) {
+            hs[k + 1] = hdxo_hash_value(types[k + 1], attr_p[k], attr_n[k], &e);
+            if (e) return -1;
+        }
+    }
+    return nbad;
 }

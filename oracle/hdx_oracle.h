@@ -61,6 +61,19 @@ void hdxo_lookup_region(uint32_t D, uint32_t R, const uint16_t* attrs, const uin
                         const uint64_t* upper, const uint64_t* ids, const uint64_t* coords,
                         uint32_t A, uint64_t n, uint64_t* out);
 
+/* daemon/datalayer_encodings.cc:168-217 (decode_value) + common/hash.cc:56-68
+ * over stored objects: value i = vals[val_off[i], +val_len[i]) encoded as
+ * [u64 BE version][u16 BE count]{[u32 BE len][bytes]}*count, key i =
+ * keys[key_off[i], +key_len[i]).  coords[i*A+0] = hash(types[0], key),
+ * coords[i*A+1+k] = hash(types[1+k], attribute k).  versions may be NULL.
+ * bad[i] = 1 (and coords 0) when the value does not decode into A-1
+ * attributes inside its bytes; returns the number of such objects, or -1 on
+ * an unknown type / mis-sized numeric. */
+int64_t hdxo_hash_encoded(const uint32_t* types, uint32_t A, const uint8_t* keys,
+                          const uint64_t* key_off, const uint32_t* key_len, const uint8_t* vals,
+                          const uint64_t* val_off, const uint32_t* val_len, uint64_t n,
+                          uint64_t* coords, uint64_t* versions, uint8_t* bad);
+
 #ifdef __cplusplus
 }
 #endif

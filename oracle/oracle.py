@@ -43,6 +43,8 @@ def lib():
         L.hdxo_partition.restype = u64
         L.hdxo_lookup_region.argtypes = [u32, u32, vp, vp, vp, vp, vp, u32, u64, vp]
         L.hdxo_lookup_region.restype = None
+        L.hdxo_hash_encoded.argtypes = [vp, u32, vp, vp, vp, vp, vp, vp, u64, vp, vp, vp]
+        L.hdxo_hash_encoded.restype = ctypes.c_int64
         _LIB = L
     return _LIB
 
@@ -117,3 +119,23 @@ def lookup_region(attrs, lower, upper, ids, coords):
                              upper.ctypes.data, ids.ctypes.data, coords.ctypes.data, A, n,
                              out.ctypes.data)
     return out
+
+
+def hash_encoded(types, keys, key_off, key_len, vals, val_off, val_len):
+    """decode_value + hash over stored objects -> (coords (n, A), versions, bad)."""
+    types = np.ascontiguousarray(types, np.uint32)
+    A = len(types)
+    arrs = [np.ascontiguousarray(x, dt) for x, dt in
+            ((keys, np.uint8), (key_off, np.uint64), (key_len, np.uint32), (vals, np.uint8),
+             (val_off, np.uint64), (val_len, np.uint32))]
+    keys, key_off, key_len, vals, val_off, val_len = [a if a.size else np.zeros(1, a.dtype) for a in arrs]
+    n = len(arrs[1])
+    coords = np.zeros(n * A, np.uint64)
+    versions = np.zeros(max(n, 1), np.uint64)
+    bad = np.zeros(max(n, 1), np.uint8)
+    r = lib().hdxo_hash_encoded(types.ctypes.data, A, keys.ctypes.data, key_off.ctypes.data,
+                                key_len.ctypes.data, vals.ctypes.data, val_off.ctypes.data,
+                                val_len.ctypes.data, n, coords.ctypes.data, versions.ctypes.data,
+                                bad.ctypes.data)
+    assert r >= 0
+    return coords.reshape(n, A), versions[:n], bad[:n].astype(bool)

@@ -1,0 +1,117 @@
+"""Reindex sweep over stored objects (config 5): decode_value
+(daemon/datalayer_encodings.cc:168-217) + hash, GPU vs oracle."""
+import numpy as np
+import pytest
+
+from hyperdex_amd import synth
+
+
+def test_oracle_decodes_what_encode_wrote(oracle):
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 300, seed=5)
+    enc = synth.encode_values_host(types, blob, base, lens, first_version=1000)
+    coords, versions, bad = oracle.hash_encoded(types, *enc)
+    want, _ = oracle.hash_batch(types, blob, base, lens)
+    assert not bad.any()
+    assert np.array_equal(coords, want)
+    assert np.array_equal(versions, 1000 + np.arange(300, dtype=np.uint64))
+
+
+def _corrupt(enc, rng):
+    """Truncations, bad counts, overrunning lengths, tiny and empty values."""
+    keys, key_off, key_len, vals, val_off, val_len = [np.array(x) for x in enc]
+    n = len(val_off)
+    cases = {}
+    for i in rng.choice(n, 40, replace=False):
+        kind = len(cases) % 5
+        o, L = int(val_off[i]), int(val_len[i])
+        if kind == 0:
+            val_len[i] = rng.integers(0, 10)          # shorter than the header
+        elif kind == 1:
+            vals[o + 9] ^= 1                           # count != A-1
+        elif kind == 2:
+            val_len[i] = L - rng.integers(1, 5)        # last attribute runs past the end
+        elif kind == 3:
+            vals[o + 10:o + 14] = [0xff, 0xff, 0xff, 0xf0]  # first length overruns
+        else:
+            val_len[i] = 10 + 2                        # truncated length prefix
+        cases[int(i)] = kind
+    return (keys, key_off, key_len, vals, val_off, val_len), cases
+
+
+def test_oracle_rejects_corrupt_values(oracle):
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 200, seed=6)
+    enc, cases = _corrupt(synth.encode_values_host(types, blob, base, lens), np.random.default_rng(1))
+    coords, versions, bad = oracle.hash_encoded(types, *enc)
+    assert set(np.nonzero(bad)[0]) == set(cases)
+    assert (coords[bad] == 0).all() and (versions[bad] == 0).all()
+
+
+def _to_dev(torch, dev, arrs):
+    out = []
+    for a in arrs:
+        a = np.ascontiguousarray(a)
+        if a.dtype == np.uint64:
+            a = a.view(np.int64)
+        elif a.dtype == np.uint32:
+            a = a.view(np.int32)
+        if a.size == 0:
+            a = np.zeros(1, a.dtype)
+        out.append(torch.from_numpy(a.copy()).to(dev))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,n", [("cfg3b", 3000), ("cfg2", 5000), ("mixed", 3000), ("cfg1", 2000),
+                                   ("wide", 300)])
+def test_gpu_encoded_matches_oracle(oracle, cfg, n):
+    import torch
+
+    import hyperdex_amd as hdx
+    dev = torch.device("cuda", 0)
+    types, blob, base, lens = synth.make_batch_host(cfg, n, seed=n + 3)
+    enc = synth.encode_values_host(types, blob, base, lens, first_version=77)
+    want, wver, _ = oracle.hash_encoded(types, *enc)
+    d = _to_dev(torch, dev, enc)
+    versions = torch.zeros(n, dtype=torch.int64, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    got = hdx.hash_encoded(types, *d, versions=versions, status=status)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().view(np.uint64), want)
+    assert np.array_equal(versions.cpu().numpy().view(np.uint64), wver)
+    assert int(status.item()) == 0
+
+
+@pytest.mark.gpu
+def test_gpu_encoded_corrupt_values(oracle):
+    import torch
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import _lib
+    dev = torch.device("cuda", 0)
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 1000, seed=9)
+    enc, cases = _corrupt(synth.encode_values_host(types, blob, base, lens), np.random.default_rng(2))
+    want, wver, bad = oracle.hash_encoded(types, *enc)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    versions = torch.zeros(1000, dtype=torch.int64, device=dev)
+    got = hdx.hash_encoded(types, *_to_dev(torch, dev, enc), versions=versions, status=status)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().view(np.uint64), want)
+    assert np.array_equal(versions.cpu().numpy().view(np.uint64), wver)
+    assert int(status.item()) == 1 << _lib.HDX_E_BADENC
+
+
+@pytest.mark.gpu
+def test_gpu_encoded_device_generator(oracle):
+    """make_encoded_device (HBM encoder) == host encoder, and the sweep is exact."""
+    import torch
+
+    import hyperdex_amd as hdx
+    dev = torch.device("cuda", 0)
+    types, keys, key_off, key_len, vals, val_off, val_len = synth.make_encoded_device("cfg3b", 4000, device=dev)
+    h = synth.encode_values_host(*synth.make_batch_host("cfg3b", 4000))
+    assert np.array_equal(vals.cpu().numpy()[:len(h[3])], h[3])
+    assert np.array_equal(val_off.cpu().numpy().view(np.uint64), h[4])
+    got = hdx.hash_encoded(types, keys, key_off, key_len, vals, val_off, val_len)
+    torch.cuda.synchronize()
+    want, _, _ = oracle.hash_encoded(types, *h)
+    assert np.array_equal(got.cpu().numpy().view(np.uint64), want)
