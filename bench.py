@@ -77,16 +77,34 @@ def main():
         return tuple(float(v) for v in t.tolist())
 
     cfg, n = args.config, args.objects
-    types, blob, base, lens = synth.make_batch_device(cfg, n, first=rank * n, device=dev)
-    A = len(types)
-    payload = int(blob.numel())
+    stream = torch.cuda.current_stream(dev)
+    if cfg == "cfg5":
+        # config 5: reindex sweep over stored objects (values in the daemon's
+        # on-disk encoding, keys apart) of the config-3b shape
+        types, keys, key_off, key_len, vals, val_off, val_len = synth.make_encoded_device(
+            "cfg3b", n, first=rank * n, device=dev)
+        A = len(types)
+        key_bytes = int(key_len.to(torch.int64).sum().item())
+        payload = key_bytes + int(val_len.to(torch.int64).sum().item())
+        extra_per_obj = 24  # key_off + val_off (u64) + key_len + val_len (u32)
+
+        def launch():
+            hdx.hash_encoded(types, keys, key_off, key_len, vals, val_off, val_len, coords=coords,
+                             stream=stream)
+    else:
+        types, blob, base, lens = synth.make_batch_device(cfg, n, first=rank * n, device=dev)
+        A = len(types)
+        payload = int(blob.numel())
+        extra_per_obj = 8 * 0  # object bases are not counted
+
+        def launch():
+            hdx.hash_batch(types, blob, base, lens, coords=coords, stream=stream)
     coords = torch.empty((n, A), dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
     log("rank %d: %s n=%d A=%d payload %.2f GB" % (rank, cfg, n, A, payload / 1e9))
 
-    stream = torch.cuda.current_stream(dev)
     for _ in range(args.warmup):
-        hdx.hash_batch(types, blob, base, lens, coords=coords, stream=stream)
+        launch()
     torch.cuda.synchronize()
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -97,7 +115,7 @@ def main():
     t0 = time.perf_counter()
     for s, e in ev:
         s.record(stream)
-        hdx.hash_batch(types, blob, base, lens, coords=coords, stream=stream)
+        launch()
         e.record(stream)
     torch.cuda.synchronize()
     if world > 1:
@@ -111,7 +129,10 @@ def main():
     total_objs = n * world
     gib_s = total_payload / (ms_per_step / 1e3) / 2**30
     mobj_s = total_objs / (ms_per_step / 1e3) / 1e6
-    algo_bytes = payload + n * A * ALGO_EXTRA_PER_ATTR  # per launch, this rank
+    if cfg == "cfg5":  # value + key bytes, per-object offsets/lengths, coordinates
+        algo_bytes = payload + n * extra_per_obj + n * A * 8
+    else:  # payload + 4 B length + 8 B coordinate per attribute
+        algo_bytes = payload + n * A * ALGO_EXTRA_PER_ATTR
     achieved = algo_bytes / (kernel_ms / 1e3) / 1e9
 
     result = {
@@ -129,7 +150,8 @@ def main():
         "dtype": "u8",
         "data": "synthetic (splitmix64 seed 0x4859504552444558, generated in HBM)",
         "config": {"workload": {"cfg3a": "config 3a", "cfg3b": "config 3b", "cfg2": "config 2",
-                                "cfg1": "config 1"}.get(cfg, cfg) +
+                                "cfg1": "config 1", "cfg5": "config 5 (reindex sweep, stored 3b objects)"
+                                }.get(cfg, cfg) +
                    ": %dM objects/GPU, key + %d attrs" % (n // 1_000_000, A - 1),
                    "objects_per_gpu": n, "attrs": A, "payload_bytes_per_gpu": payload,
                    "parallelism": "shard%d" % world},
@@ -141,15 +163,21 @@ def main():
                      "kernel": "hdx::hash_chunk_kernel / hash_pipelined_kernel (auto per schema)"},
     }
 
+    if cfg == "cfg5":
+        result["roofline"]["kernel"] = "hdx::hash_encoded_kernel (decode_value + hash)"
     if world > 1 and not args.no_allgather:
         result["allgather"] = time_allgather(coords, world, dev, backend, max_over_ranks)
 
-    if not args.no_host_path and rank == 0 and world == 1:
+    if not args.no_host_path and rank == 0 and world == 1 and cfg != "cfg5":
         result["host_path"] = time_host_path(types, blob, base, lens, A)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(types, blob, base, lens, A, args.cpu_seconds,
-                                              coords)
+        if cfg == "cfg5":
+            result["cpu_baseline"] = cpu_baseline_encoded(
+                types, (keys, key_off, key_len, vals, val_off, val_len), A, args.cpu_seconds, coords)
+        else:
+            result["cpu_baseline"] = cpu_baseline(types, blob, base, lens, A, args.cpu_seconds,
+                                                  coords)
 
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -269,6 +297,36 @@ def cpu_baseline(types, blob, base, lens, A, seconds, coords):
             "sample": "%d objects (%.0f MB) of the same batch, %d passes, oracle/hdx_oracle.c -O2 "
                       "pthreads; verified equal to the GPU coords" % (ns, nb / 1e6, reps),
             "cpu_model": model}
+
+
+def cpu_baseline_encoded(types, enc, A, seconds, coords):
+    """Config 5 CPU baseline: the oracle's decode_value + hash (single thread;
+    the oracle has no threaded form of the sweep) on a 20 k-object sample."""
+    from oracle import oracle
+    keys, key_off, key_len, vals, val_off, val_len = enc
+    ns = min(20_000, val_off.numel())
+    ko = key_off[:ns].cpu().numpy().view(np.uint64)
+    kl = key_len[:ns].cpu().numpy().view(np.uint32)
+    vo = val_off[:ns].cpu().numpy().view(np.uint64)
+    vl = val_len[:ns].cpu().numpy().view(np.uint32)
+    kend = int((ko.astype(np.uint64) + kl).max())
+    vend = int((vo.astype(np.uint64) + vl).max())
+    hk, hv = keys[:kend].cpu().numpy(), vals[:vend].cpu().numpy()
+    want, _, bad = oracle.hash_encoded(types, hk, ko, kl, hv, vo, vl)
+    if bad.any() or not np.array_equal(coords[:ns].cpu().numpy().view(np.uint64), want):
+        raise SystemExit("cpu_baseline: GPU coordinates differ from the oracle")
+    nbytes = int(kl.sum()) + int(vl.sum())
+    reps, t0 = 0, time.perf_counter()
+    while True:
+        oracle.hash_encoded(types, hk, ko, kl, hv, vo, vl)
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            break
+    return {"value": round(reps * nbytes / dt / 2**30, 3), "unit": "GiB/s", "cores": 1,
+            "kind": "port", "mobjects_per_s": round(reps * ns / dt / 1e6, 3),
+            "sample": "%d stored objects (%.0f MB), %d passes, oracle hdxo_hash_encoded -O2, 1 thread; "
+                      "verified equal to the GPU coords" % (ns, nbytes / 1e6, reps)}
 
 
 if __name__ == "__main__":
