@@ -148,8 +148,82 @@ hash_encoded_kernel(const EncodedArgs a) {
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
+// Lane-per-object variant: lane l owns object o0+l and walks its value once,
+// hashing attribute t while the length prefix of attribute t+2 is in flight
+// (the prefix of t+1 arrived during t-1).  Attribute positions share one
+// type, so every pass is type-uniform; no LDS.  Coordinates are stored as they
+// are produced; an object found undecodable later is zeroed afterwards.
+template <bool TOUCH>
+__global__ void __launch_bounds__(256)
+hash_encoded_lane_kernel(const EncodedArgs a) {
+    const uint32_t A = a.A;
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const uint64_t voff = a.val_off[i], koff = a.key_off[i];
+    const uint32_t vlen = a.val_len[i], klen = a.key_len[i];
+    const uint8_t* v = a.vals + voff;
+    uint32_t sink = 0;
+    if (TOUCH) {
+        const uint32_t touch = vlen >= 4 ? min(vlen - 3, 4096u) : 0u;
+        for (uint32_t off = 0; off < touch; off += 128)
+            sink ^= *(const __attribute__((address_space(1))) u32_u*)(v + off);
+    }
+    bool ok = vlen >= 10;
+    const uint64_t version = ok ? load_be64(v) : 0;
+    ok = ok && load_be16(v + 8) == A - 1;
+    uint64_t* out = a.coords + i * A;
+    bool bad = false;
+
+    // attribute t = 0 is the key; the value's attributes follow their prefixes
+    const uint8_t* p = a.keys + koff;
+    uint32_t L = klen, pos = 10;
+    uint32_t next_len = 0;  // prefix of attribute t+1, loaded one step ahead
+    auto read_prefix = [&](uint32_t at) -> uint32_t {
+        return (ok && vlen >= 4 && at <= vlen - 4) ? load_be32(v + at) : 0u;
+    };
+    if (A > 1) next_len = read_prefix(pos);
+    for (uint32_t t = 0; t < A; ++t) {
+        const uint32_t code = a.codes[t];
+        const Blk blk = issue_block(ok ? code : (uint32_t)CODE_ZERO, ok ? p : g_zero_pad, ok ? L : 0u);
+        // locate attribute t+1 and put the prefix of t+2 in flight
+        const uint8_t* pn = g_zero_pad;
+        uint32_t Ln = 0;
+        if (t + 1 < A) {
+            if (ok && vlen >= 4 && pos <= vlen - 4 && next_len <= vlen - pos - 4) {
+                pn = v + pos + 4;
+                Ln = next_len;
+                pos += 4 + next_len;
+                next_len = t + 2 < A ? read_prefix(pos) : 0u;
+            } else {
+                ok = false;
+            }
+        }
+        const uint64_t h = hash_blk(ok ? code : (uint32_t)CODE_ZERO, p, ok ? L : 0u, blk, bad);
+        __builtin_nontemporal_store(h, out + t);
+        p = pn;
+        L = Ln;
+    }
+    if (!ok) {
+        for (uint32_t t = 0; t < A; ++t) out[t] = 0;
+        if (a.status) atomicOr(a.status, 1u << 6 /* HDX_E_BADENC */);
+    }
+    if (a.versions) a.versions[i] = ok ? version : 0;
+    if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
+    if (TOUCH) asm volatile("; touch sink %0" ::"v"(sink));
+}
+
 hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
+    const int v = hash_variant();
+    if (v == 31 || v == 32 || v == -1) {
+        const uint64_t blocks = (a.n + 255) / 256;
+        if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+        if (v == 32)
+            hipLaunchKernelGGL(hash_encoded_lane_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+        else
+            hipLaunchKernelGGL(hash_encoded_lane_kernel<true>, dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+        return hipGetLastError();
+    }
     const uint32_t waves_per_block = a.A <= 32 ? 2 : 1;
     const uint64_t waves = (a.n + 63) / 64;
     const uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;

@@ -33,7 +33,19 @@ def main():
     dev = torch.device("cuda", 0)
     variants = [int(v) for v in args.variants.split(",")]
     for cfg in args.configs.split(","):
-        types, blob, base, lens = synth.make_batch_device(cfg, args.objects, device=dev)
+        if cfg == "cfg5":  # stored-object sweep (variants 30-32)
+            types, *enc = synth.make_encoded_device("cfg3b", args.objects, device=dev)
+            blob = enc[0][:int(enc[2].to(torch.int64).sum().item())]  # key bytes ...
+            extra = int(enc[5].to(torch.int64).sum().item())            # ... + value bytes
+
+            def run(coords):
+                hdx.hash_encoded(types, *enc, coords=coords)
+        else:
+            types, blob, base, lens = synth.make_batch_device(cfg, args.objects, device=dev)
+            extra = 0
+
+            def run(coords):
+                hdx.hash_batch(types, blob, base, lens, coords=coords)
         A = len(types)
         coords = torch.empty((args.objects, A), dtype=torch.int64, device=dev)
         ref = None
@@ -44,7 +56,7 @@ def main():
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
                 for _ in range(args.launches):
-                    hdx.hash_batch(types, blob, base, lens, coords=coords)
+                    run(coords)
                 e.record()
                 torch.cuda.synchronize()
                 if rep == 0:  # warm-up round doubles as a cross-variant equality check
@@ -54,13 +66,13 @@ def main():
                         raise SystemExit("variant %d differs from variant %d on %s" % (v, variants[0], cfg))
                     continue
                 times[v].append(s.elapsed_time(e) / args.launches)
-        algo = blob.numel() + args.objects * A * 12
+        algo = blob.numel() + extra + args.objects * A * 12
         for v in variants:
             t = np.array(times[v])
             print(json.dumps({"config": cfg, "variant": v, "ms_median": round(float(np.median(t)), 4),
                               "ms_min": round(float(t.min()), 4),
                               "frac": round(algo / (np.median(t) / 1e3) / 8e12, 4)}), flush=True)
-        del blob, base, lens, coords, ref
+        del blob, coords, ref
         torch.cuda.empty_cache()
 
 
