@@ -50,6 +50,10 @@ struct alignas(8) EncDesc {
 };
 constexpr uint32_t kZeroSlot = 0xffffffffu;
 
+__host__ __device__ constexpr size_t encoded_lds_per_wave(uint32_t A) {
+    return 64 * 16 + 256 + (size_t)64 * A * sizeof(EncDesc);
+}
+
 template <bool TOUCH>
 __global__ void __launch_bounds__(256)
 hash_encoded_kernel(const EncodedArgs a) {
@@ -57,7 +61,11 @@ hash_encoded_kernel(const EncodedArgs a) {
     const uint32_t A = a.A;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    EncDesc* desc = reinterpret_cast<EncDesc*>(smem_raw) + (size_t)w * 64 * A;
+    // wave-private LDS: 64 object bases {value, key}, the code table, descriptors
+    uint8_t* wsmem = smem_raw + (size_t)w * encoded_lds_per_wave(A);
+    uint64_t* bases = reinterpret_cast<uint64_t*>(wsmem);           // [64][2]
+    uint8_t* codes = wsmem + 64 * 16;                                // [256]
+    EncDesc* desc = reinterpret_cast<EncDesc*>(wsmem + 64 * 16 + 256);
     const uint64_t o0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + w) * 64;
     if (o0 >= a.n) return;  // no workgroup barrier: waves are independent
     const uint32_t nobj = (uint32_t)min<uint64_t>(64, a.n - o0);
@@ -67,6 +75,9 @@ hash_encoded_kernel(const EncodedArgs a) {
     const uint64_t voff = a.val_off[i], koff = a.key_off[i];
     const uint32_t vlen = valid ? a.val_len[i] : 0u, klen = valid ? a.key_len[i] : 0u;
     const uint8_t* v = a.vals + voff;
+    bases[2 * lane] = voff;
+    bases[2 * lane + 1] = koff;
+    for (uint32_t j = lane; j < A; j += 64) codes[j] = a.codes[j];
 
     // phase 0: pull the value's lines toward L2 (independent loads, consumed late)
     uint32_t sink = 0;
@@ -105,11 +116,12 @@ hash_encoded_kernel(const EncodedArgs a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    // phase 2: A passes of 64 slots, slot s = object * A + attribute; the
-    // object's key/value bases come from its owner lane by ds_bpermute
+    // phase 2: A passes of 64 slots, slot s = object * A + attribute.  The
+    // object's bases and the attribute's code are read from LDS, not from other
+    // lanes: in a partial pass the lanes past the batch end are inactive, and a
+    // ds_bpermute from an inactive lane returns 0.
     const uint32_t nslots = nobj * A;
     uint64_t* out = a.coords + o0 * A;
-    const uint32_t packed_codes = reinterpret_cast<const uint32_t*>(a.codes)[lane];
     struct Pass {
         const uint8_t* p;
         uint32_t n, code;
@@ -119,11 +131,9 @@ hash_encoded_kernel(const EncodedArgs a) {
         const uint32_t s = min(t * 64 + (uint32_t)lane, nslots - 1);
         const uint32_t obj = s / A, j = s - obj * A;
         const EncDesc d = desc[s];
-        const uint32_t vlo = __shfl((uint32_t)voff, (int)obj, 64), vhi = __shfl((uint32_t)(voff >> 32), (int)obj, 64);
-        const uint32_t klo = __shfl((uint32_t)koff, (int)obj, 64), khi = __shfl((uint32_t)(koff >> 32), (int)obj, 64);
-        const uint64_t base = j == 0 ? (((uint64_t)khi << 32) | klo) : (((uint64_t)vhi << 32) | vlo);
+        const uint64_t base = bases[2 * obj + (j == 0)];
         const bool zero = d.off == kZeroSlot || t * 64 + (uint32_t)lane >= nslots;
-        P.code = zero ? (uint32_t)CODE_ZERO : (__shfl(packed_codes, (int)(j >> 2), 64) >> (8 * (j & 3))) & 0xffu;
+        P.code = zero ? (uint32_t)CODE_ZERO : (uint32_t)codes[j];
         P.n = zero ? 0u : d.len;
         P.p = zero ? g_zero_pad : (j == 0 ? a.keys : a.vals) + base + d.off;
         P.blk = issue_block(P.code, P.p, P.n);
@@ -153,12 +163,12 @@ hash_encoded_kernel(const EncodedArgs a) {
 
 hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
-    // 4 waves per workgroup while the descriptors fit (A <= 64: 32 KiB), else 1
-    const uint32_t waves_per_block = a.A <= 64 ? 4 : 1;
+    // 4 waves per workgroup while they fit in 64 KiB of LDS (A <= 28), else 1
+    const uint32_t waves_per_block = 4 * encoded_lds_per_wave(a.A) <= 65536 ? 4 : 1;
     const uint64_t waves = (a.n + 63) / 64;
     const uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    const size_t lds = (size_t)waves_per_block * 64 * a.A * sizeof(EncDesc);
+    const size_t lds = (size_t)waves_per_block * encoded_lds_per_wave(a.A);
     if (hash_variant() == 33)
         hipLaunchKernelGGL((hash_encoded_kernel<false>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
                            lds, stream, a);

@@ -115,3 +115,21 @@ def test_gpu_encoded_device_generator(oracle):
     torch.cuda.synchronize()
     want, _, _ = oracle.hash_encoded(types, *h)
     assert np.array_equal(got.cpu().numpy().view(np.uint64), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("A,n", [(33, 66), (5, 104), (2, 100), (17, 70), (65, 130), (70, 130), (128, 65)])
+def test_gpu_encoded_partial_last_pass(oracle, A, n):
+    """Last wave with few objects: its final pass has most lanes past the batch
+    end while the active lanes need other objects' bases and other positions'
+    codes (regression: cross-lane reads from inactive lanes return 0)."""
+    import torch
+
+    import hyperdex_amd as hdx
+    rules = [synth.Rule(9217, synth.UNIFORM, 0, 130)] * (A - 2) + [synth._n(9218), synth._n(9219)]
+    types, blob, base, lens = synth.make_batch_host(rules[:A], n, seed=A * 1000 + n)
+    enc = synth.encode_values_host(types, blob, base, lens)
+    want, _, _ = oracle.hash_encoded(types, *enc)
+    got = hdx.hash_encoded(types, *_to_dev(torch, torch.device("cuda", 0), enc))
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().view(np.uint64), want)
