@@ -311,7 +311,7 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
 }
 
 static constexpr int kDefaultVariant = -1;  // automatic
-// 33 selects the stored-object sweep without its phase-0 line touch (hdx_encoded.hip).
+// 33 selects the stored-object sweep with its phase-0 line touch (hdx_encoded.hip).
 static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 25) || v == 33; }
 
 static int g_variant = [] {
