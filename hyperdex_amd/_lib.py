@@ -55,6 +55,9 @@ SIGNATURES = [
     ("hdx_region_table_create", _i32, [_u32, _u32, _vp, _vp, _vp, _vp, _vp]),
     ("hdx_region_table_destroy", _i32, [_vp]),
     ("hdx_lookup_region_device", _i32, [_vp, _vp, _u32, _u64, _vp, _vp]),
+    ("hdx_index_key_size", ctypes.c_size_t, [_u32]),
+    ("hdx_index_encode_device", _i32, [_u32, _vp, _vp, _vp, _u64, _vp, _vp, _vp]),
+    ("hdx_search_regions", _i32, [_vp, _vp, _u32, _vp, _vp]),
     ("hdx_alloc_pinned", _i32, [_sz, _vp]),
     ("hdx_free_pinned", _i32, [_vp]),
     ("hdx_synth_lengths", _i32, [ctypes.POINTER(SynthRule), _u32, _u64, _u64, _u64, _vp, _vp]),

@@ -15,10 +15,9 @@
 #include <string>
 #include <vector>
 
-#include "hdx_internal.h"
+#include "hdx_host.h"
 #include "../../include/hdxhash_debug.h"
 
-#define HDX_EXPORT extern "C" __attribute__((visibility("default")))
 
 namespace hdx {
 
@@ -26,8 +25,7 @@ namespace hdx {
 
 static thread_local std::string t_err;
 
-static hdx_status fail(hdx_status s, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
-static hdx_status fail(hdx_status s, const char* fmt, ...) {
+hdx_status fail(hdx_status s, const char* fmt, ...) {
     char buf[512];
     va_list ap;
     va_start(ap, fmt);
@@ -37,15 +35,10 @@ static hdx_status fail(hdx_status s, const char* fmt, ...) {
     return s;
 }
 
-static hdx_status hip_fail(hipError_t e, const char* what) {
+hdx_status hip_fail(hipError_t e, const char* what) {
     return fail(HDX_E_DEVICE, "%s: %s", what, hipGetErrorString(e));
 }
 
-#define HIP_TRY(expr)                                  \
-    do {                                               \
-        hipError_t e_ = (expr);                        \
-        if (e_ != hipSuccess) return hip_fail(e_, #expr); \
-    } while (0)
 
 // ---- types (include/hyperdex.h:53-102; datatype_info.cc:72-141) ----------
 
@@ -70,7 +63,7 @@ int type_code(uint32_t t) {
     }
 }
 
-static hdx_status check_schema(const uint32_t* types, uint32_t A, uint8_t* codes_out) {
+hdx_status check_schema(const uint32_t* types, uint32_t A, uint8_t* codes_out) {
     if (!types) return fail(HDX_E_INVALID, "types is NULL");
     if (A == 0 || A > HDX_MAX_ATTRS)
         return fail(HDX_E_INVALID, "attrs_sz=%u outside [1, %d]", A, HDX_MAX_ATTRS);
@@ -135,7 +128,7 @@ struct ThreadState {
 };
 static thread_local ThreadState t_state;
 
-static hdx_status bind_device(int want /* -1: current */) {
+hdx_status bind_device(int want /* -1: current */) {
     std::call_once(g_probe_once, probe);
     if (g_ndev <= 0) return fail(HDX_E_DEVICE, "no HIP device visible (this library has no CPU path)");
     int dev = want;
@@ -154,41 +147,11 @@ static hdx_status bind_device(int want /* -1: current */) {
     return HDX_OK;
 }
 
-static hdx_status thread_stream(hipStream_t* out) {
+hdx_status thread_stream(hipStream_t* out) {
     hdx_status st = bind_device(-1);
     if (st != HDX_OK) return st;
     if (!t_state.stream) HIP_TRY(hipStreamCreateWithFlags(&t_state.stream, hipStreamNonBlocking));
     *out = t_state.stream;
-    return HDX_OK;
-}
-
-template <typename T>
-static hdx_status grow_dev(T** p, size_t* cap, size_t need) {
-    if (need <= *cap) return HDX_OK;
-    size_t n = std::max(need, *cap * 3 / 2);
-    (void)hipFree(*p);
-    *p = nullptr;
-    *cap = 0;
-    if (hipMalloc((void**)p, n * sizeof(T)) != hipSuccess) {
-        (void)hipGetLastError();
-        return fail(HDX_E_NOMEM, "hipMalloc(%zu) failed", n * sizeof(T));
-    }
-    *cap = n;
-    return HDX_OK;
-}
-
-template <typename T>
-static hdx_status grow_pinned(T** p, size_t* cap, size_t need) {
-    if (need <= *cap) return HDX_OK;
-    size_t n = std::max(need, *cap * 3 / 2);
-    (void)hipHostFree(*p);
-    *p = nullptr;
-    *cap = 0;
-    if (hipHostMalloc((void**)p, n * sizeof(T), hipHostMallocDefault) != hipSuccess) {
-        (void)hipGetLastError();
-        return fail(HDX_E_NOMEM, "hipHostMalloc(%zu) failed", n * sizeof(T));
-    }
-    *cap = n;
     return HDX_OK;
 }
 
@@ -536,14 +499,6 @@ HDX_EXPORT hdx_status hdx_synth_fill(const hdx_synth_rule* rules, uint32_t attrs
 
 // ---- region tables (hdx_regions.hip) ----------------------------------------
 
-struct hdx_region_table_s {
-    int device;
-    uint32_t D, R;
-    uint16_t attrs[16];
-    uint64_t* d_lower;
-    uint64_t* d_upper;
-    uint64_t* d_ids;
-};
 
 HDX_EXPORT hdx_status hdx_region_table_create(uint32_t dims, uint32_t regions, const uint16_t* attrs,
                                               const uint64_t* lower, const uint64_t* upper,

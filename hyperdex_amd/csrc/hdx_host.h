@@ -1,0 +1,76 @@
+// hdx_host.h — host-side helpers shared by the C-ABI translation units
+// (argument checking, error text, device binding, staging growth).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstddef>
+
+#include "hdx_internal.h"
+
+#define HDX_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace hdx {
+
+// Sets the calling thread's hdx_last_error() text and returns s.
+hdx_status fail(hdx_status s, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+hdx_status hip_fail(hipError_t e, const char* what);
+
+#define HIP_TRY(expr)                                     \
+    do {                                                  \
+        hipError_t e_ = (expr);                           \
+        if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+    } while (0)
+
+// hyperdatatype -> CODE_* (-1: the reference's lookup() returns NULL).
+int type_code(uint32_t t);
+// Validates a schema and fills codes_out[A] (may be NULL).
+hdx_status check_schema(const uint32_t* types, uint32_t A, uint8_t* codes_out);
+// Binds the calling thread to `want` (-1: its current device) after checking it is gfx950.
+hdx_status bind_device(int want);
+// The calling thread's library stream (created on first use).
+hdx_status thread_stream(hipStream_t* out);
+
+template <typename T>
+inline hdx_status grow_dev(T** p, size_t* cap, size_t need) {
+    if (need <= *cap) return HDX_OK;
+    size_t n = std::max(need, *cap * 3 / 2);
+    (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc((void**)p, n * sizeof(T)) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(HDX_E_NOMEM, "hipMalloc(%zu) failed", n * sizeof(T));
+    }
+    *cap = n;
+    return HDX_OK;
+}
+
+template <typename T>
+inline hdx_status grow_pinned(T** p, size_t* cap, size_t need) {
+    if (need <= *cap) return HDX_OK;
+    size_t n = std::max(need, *cap * 3 / 2);
+    (void)hipHostFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipHostMalloc((void**)p, n * sizeof(T), hipHostMallocDefault) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(HDX_E_NOMEM, "hipHostMalloc(%zu) failed", n * sizeof(T));
+    }
+    *cap = n;
+    return HDX_OK;
+}
+
+}  // namespace hdx
+
+// Device copy of one subspace's region table (include/hdxhash.h).
+struct hdx_region_table_s {
+    int device;
+    uint32_t D, R;
+    uint16_t attrs[16];
+    uint64_t* d_lower;
+    uint64_t* d_upper;
+    uint64_t* d_ids;
+};
+

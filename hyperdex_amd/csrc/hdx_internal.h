@@ -78,6 +78,39 @@ struct EncodedArgs {
 
 hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream);
 
+// Index-key encoding (hdx_index.hip): n values of one INT64 / FLOAT /
+// TIMESTAMP_* attribute at blob + off[i], len[i] bytes; out holds n entries
+// of 8 B (16 B for CODE_FLOAT).
+struct IndexArgs {
+    const uint8_t* blob;
+    const uint64_t* off;
+    const uint32_t* len;
+    uint8_t* out;
+    uint32_t* status;  // may be NULL
+    uint64_t n;
+    uint32_t code;     // CODE_INT64 or CODE_FLOAT (timestamps encode as int64)
+};
+
+hipError_t launch_index_encode(const IndexArgs& a, hipStream_t stream);
+
+// Search pruning (hdx_index.hip) over one subspace's region table: m ranges
+// that name a subspace attribute, in the order lookup_search visits them.
+enum : uint8_t { SEARCH_NONE = 0, SEARCH_STRING_EQ = 1, SEARCH_ORDERED = 2 };
+constexpr uint32_t kMaxSearchRanges = 16;  // one range per subspace dimension
+struct SearchArgs {
+    const uint64_t* lower;   // [R*D]
+    const uint64_t* upper;   // [R*D]
+    const uint64_t* hashes;  // [2*m]: hash of start, hash of end
+    uint8_t* include;        // [R]
+    uint32_t* cleared;       // set when the reference would clear the server list
+    uint32_t R, D, m;
+    uint8_t dim[kMaxSearchRanges];
+    uint8_t kind[kMaxSearchRanges];
+    uint8_t flags[kMaxSearchRanges];  // bit 0 has_start, bit 1 has_end
+};
+
+hipError_t launch_search_regions(const SearchArgs& a, hipStream_t stream);
+
 struct SynthArgs {
     uint64_t seed;
     uint64_t first;

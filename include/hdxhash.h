@@ -172,6 +172,51 @@ hdx_status hdx_lookup_region_device(hdx_region_table table, const uint64_t* coor
                                     uint32_t attrs_sz, uint64_t n, uint64_t* region_ids,
                                     hdx_stream stream);
 
+/* ---- secondary-index keys and search pruning ------------ */
+
+/* Bytes of one index key for `type`: 8 for INT64 and TIMESTAMP_*, 16 for
+ * FLOAT, 0 for types whose index key is not a fixed-size hash encoding. */
+size_t hdx_index_key_size(uint32_t type);
+/* index_encoding_{int64,timestamp,float}::encode (daemon/index_int64.cc:76-79,
+ * daemon/index_timestamp.cc:79-82, daemon/index_float.cc:75-90) for n values
+ * of one attribute: value i is len[i] bytes at blob + off[i]; key i is
+ * written at out + i * hdx_index_key_size(type):
+ *   INT64, TIMESTAMP_*: big-endian ordered_encode_int64 (the int64 hash);
+ *   FLOAT:              big-endian ordered_encode_double ++ the double's
+ *                       little-endian bytes (0.0 when the value is empty).
+ * A value whose size is not 0 or 8 gets an all-zero key and sets bit
+ * (1 << HDX_E_BADSIZE) in *status_dev (the reference asserts).  Device
+ * pointers; asynchronous on `stream`. */
+hdx_status hdx_index_encode_device(uint32_t type, const uint8_t* blob, const uint64_t* off,
+                                   const uint32_t* len, uint64_t n, uint8_t* out,
+                                   uint32_t* status_dev, hdx_stream stream);
+
+/* One range of a search, as range_searches() leaves it (common/range.h:40-55,
+ * common/range_searches.cc:151-202): inclusive, at most one per attribute. */
+typedef struct hdx_range {
+    uint32_t attr;        /* schema attribute index */
+    uint32_t type;        /* hyperdatatype of the attribute */
+    const uint8_t* start; /* host bytes */
+    uint64_t start_len;
+    const uint8_t* end;
+    uint64_t end_len;
+    uint32_t has_start;
+    uint32_t has_end;
+    uint32_t invalid;
+    uint32_t reserved;
+} hdx_range;
+/* The region test of configuration::lookup_search (common/configuration.cc:
+ * 736-858) for one subspace: include[r] = 0 when a range excludes region r
+ * of `table` (a STRING range with start == end whose hash lies outside the
+ * region's box on that dimension; an INT64/FLOAT range whose hashed start is
+ * above the box or hashed end below it), else 1.  *cleared = 1 when the
+ * reference would return an empty server list (an invalid range, or a region
+ * box with lower > upper on a ranged dimension); include[] is then all 0.
+ * Regions without replicas are the caller's to skip, as the reference does.
+ * Endpoint hashes are computed on the device.  Host pointers; synchronous. */
+hdx_status hdx_search_regions(hdx_region_table table, const hdx_range* ranges, uint32_t nranges,
+                              uint8_t* include, int* cleared);
+
 /* ---- pinned host memory ------------------------------------------------- */
 
 hdx_status hdx_alloc_pinned(size_t bytes, void** out);

@@ -445,3 +445,84 @@ int64_t hdxo_hash_encoded(const uint32_t* types, uint32_t A, const uint8_t* keys
     }
     return nbad;
 }
+
+/* ---- secondary-index keys (daemon/index_*.cc) --------------------------- */
+
+static void put_be64(uint8_t* o, uint64_t v) {
+    for (int i = 0; i < 8; ++i) o[i] = (uint8_t)(v >> (56 - 8 * i));
+}
+
+size_t hdxo_index_encode(uint32_t type, const uint8_t* p, size_t len, uint8_t* out, int* err) {
+    int is_float = type == 9219;
+    int is_int = type == 9218 || (type >= 9473 && type <= 9478); /* index_info.cc:87-93 */
+    *err = 0;
+    if (!is_float && !is_int) return 0;
+    const size_t size = is_float ? 16 : 8;
+    memset(out, 0, size);
+    if (len != 0 && len != 8) {
+        *err = 2;
+        return size;
+    }
+    /* index_int64.cc:76-79 and index_timestamp.cc:79-82 (m_iei is the int64
+     * encoding, so timestamps are keyed by hash(INT64, v), not the calendar
+     * hash) */
+    int e = 0;
+    const uint64_t h = hdxo_hash_value(is_float ? 9219 : 9218, p, len, &e);
+    put_be64(out, h);
+    if (is_float && len == 8) memcpy(out + 8, p, 8); /* packdoublele(number) */
+    return size;
+}
+
+/* ---- search pruning (common/configuration.cc:736-858) ------------------- */
+
+static int slice_eq(const uint8_t* a, uint64_t al, const uint8_t* b, uint64_t bl) {
+    return al == bl && (al == 0 || memcmp(a, b, al) == 0);
+}
+
+int hdxo_search_regions(uint32_t D, uint32_t R, const uint16_t* attrs, const uint64_t* lower,
+                        const uint64_t* upper, const hdxo_range* ranges, uint32_t nranges,
+                        uint8_t* include) {
+    for (uint32_t i = 0; i < nranges; ++i) /* :761-768 */
+        if (ranges[i].invalid) {
+            memset(include, 0, R);
+            return 1;
+        }
+    for (uint32_t j = 0; j < R; ++j) { /* :777 */
+        int exclude = 0;
+        for (uint32_t k = 0; !exclude && k < nranges; ++k) { /* :789 */
+            const hdxo_range* rg = &ranges[k];
+            uint32_t attr = UINT16_MAX;
+            for (uint32_t l = 0; l < D; ++l) /* :794-801 */
+                if (attrs[l] == rg->attr) {
+                    attr = l;
+                    break;
+                }
+            if (attr == UINT16_MAX) continue;
+            const uint64_t lo = lower[(uint64_t)j * D + attr], hi = upper[(uint64_t)j * D + attr];
+            if (lo > hi) { /* :810-815 */
+                memset(include, 0, R);
+                return 1;
+            }
+            int e = 0;
+            if (rg->type == 9217 && rg->has_start && rg->has_end &&
+                slice_eq(rg->start, rg->start_len, rg->end, rg->end_len)) { /* :817-829 */
+                const uint64_t h = hdxo_hash_value(9217, rg->start, rg->start_len, &e);
+                if (lo > h || hi < h) exclude = 1;
+            }
+            if (rg->type == 9218 || rg->type == 9219) { /* :831-852 */
+                if (rg->has_start) {
+                    const uint64_t h = hdxo_hash_value(rg->type, rg->start, rg->start_len, &e);
+                    if (e) return -1;
+                    if (hi < h) exclude = 1;
+                }
+                if (rg->has_end) {
+                    const uint64_t h = hdxo_hash_value(rg->type, rg->end, rg->end_len, &e);
+                    if (e) return -1;
+                    if (lo > h) exclude = 1;
+                }
+            }
+        }
+        include[j] = exclude ? 0 : 1;
+    }
+    return 0;
+}

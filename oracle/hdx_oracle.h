@@ -74,6 +74,33 @@ int64_t hdxo_hash_encoded(const uint32_t* types, uint32_t A, const uint8_t* keys
                           const uint64_t* val_off, const uint32_t* val_len, uint64_t n,
                           uint64_t* coords, uint64_t* versions, uint8_t* bad);
 
+/* daemon/index_int64.cc:76-79, index_timestamp.cc:79-82, index_float.cc:75-90:
+ * the secondary-index key of one value.  INT64 and TIMESTAMP_* write 8 bytes
+ * (big-endian hash(INT64, v)); FLOAT writes 16 (big-endian hash(FLOAT, v),
+ * then the double's little-endian bytes or 0.0 when not 8 bytes long).
+ * Returns the key size, 0 for other types; *err = 2 (and an all-zero key)
+ * when the value's size is not 0 or 8 (the reference asserts). */
+size_t hdxo_index_encode(uint32_t type, const uint8_t* p, size_t len, uint8_t* out, int* err);
+
+/* common/range.h:40-55 after range_searches(); same layout as hdx_range. */
+typedef struct hdxo_range {
+    uint32_t attr, type;
+    const uint8_t* start;
+    uint64_t start_len;
+    const uint8_t* end;
+    uint64_t end_len;
+    uint32_t has_start, has_end, invalid, reserved;
+} hdxo_range;
+
+/* common/configuration.cc:736-858 (lookup_search), the region loop of one
+ * subspace whose attributes are attrs[D] and boxes lower/upper[R*D]:
+ * include[r] = 1 unless a range excludes region r.  Returns 1 (and all-zero
+ * include) when the reference clears the server list, else 0; -1 when a
+ * numeric endpoint's size is not 0 or 8. */
+int hdxo_search_regions(uint32_t D, uint32_t R, const uint16_t* attrs, const uint64_t* lower,
+                        const uint64_t* upper, const hdxo_range* ranges, uint32_t nranges,
+                        uint8_t* include);
+
 #ifdef __cplusplus
 }
 #endif

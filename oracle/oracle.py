@@ -44,6 +44,10 @@ def lib():
         L.hdxo_lookup_region.argtypes = [u32, u32, vp, vp, vp, vp, vp, u32, u64, vp]
         L.hdxo_lookup_region.restype = None
         L.hdxo_hash_encoded.argtypes = [vp, u32, vp, vp, vp, vp, vp, vp, u64, vp, vp, vp]
+        L.hdxo_index_encode.restype = sz
+        L.hdxo_index_encode.argtypes = [u32, vp, sz, vp, ctypes.POINTER(ctypes.c_int)]
+        L.hdxo_search_regions.restype = ctypes.c_int
+        L.hdxo_search_regions.argtypes = [u32, u32, vp, vp, vp, vp, u32, vp]
         L.hdxo_hash_encoded.restype = ctypes.c_int64
         _LIB = L
     return _LIB
@@ -139,3 +143,49 @@ def hash_encoded(types, keys, key_off, key_len, vals, val_off, val_len):
                                 bad.ctypes.data)
     assert r >= 0
     return coords.reshape(n, A), versions[:n], bad[:n].astype(bool)
+
+
+def index_encode(type_id: int, data: bytes):
+    """Secondary-index key of one value -> (key bytes, err); b"" for other types."""
+    buf = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+    out = ctypes.create_string_buffer(16)
+    err = ctypes.c_int(0)
+    k = lib().hdxo_index_encode(type_id, buf, len(data), out, ctypes.byref(err))
+    return out.raw[:k], err.value
+
+
+class Range(ctypes.Structure):
+    """common/range.h after range_searches (layout of hdx_range / hdxo_range)."""
+    _fields_ = [("attr", ctypes.c_uint32), ("type", ctypes.c_uint32),
+                ("start", ctypes.c_char_p), ("start_len", ctypes.c_uint64),
+                ("end", ctypes.c_char_p), ("end_len", ctypes.c_uint64),
+                ("has_start", ctypes.c_uint32), ("has_end", ctypes.c_uint32),
+                ("invalid", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+def make_ranges(ranges):
+    """[(attr, type, start|None, end|None[, invalid])] -> ctypes array of Range."""
+    arr = (Range * max(len(ranges), 1))()
+    for k, r in enumerate(ranges):
+        attr, t, start, end = r[:4]
+        arr[k].attr, arr[k].type = attr, t
+        arr[k].has_start, arr[k].has_end = start is not None, end is not None
+        arr[k].start, arr[k].start_len = (start or b""), len(start or b"")
+        arr[k].end, arr[k].end_len = (end or b""), len(end or b"")
+        arr[k].invalid = bool(r[4]) if len(r) > 4 else False
+    return arr
+
+
+def search_regions(attrs, lower, upper, ranges):
+    """lookup_search's region loop for one subspace -> (include u8[R], cleared)."""
+    attrs = np.ascontiguousarray(attrs, np.uint16)
+    lower = np.ascontiguousarray(lower, np.uint64)
+    upper = np.ascontiguousarray(upper, np.uint64)
+    R = lower.shape[0] if lower.ndim == 2 else lower.size // max(len(attrs), 1)
+    include = np.zeros(max(R, 1), np.uint8)
+    arr = make_ranges(ranges)
+    rc = lib().hdxo_search_regions(len(attrs), R, attrs.ctypes.data, lower.ctypes.data,
+                                   upper.ctypes.data, arr, len(ranges), include.ctypes.data)
+    if rc < 0:
+        raise ValueError("numeric endpoint not 0 or 8 bytes")
+    return include[:R], bool(rc)
