@@ -217,6 +217,48 @@ typedef struct hdx_range {
 hdx_status hdx_search_regions(hdx_region_table table, const hdx_range* ranges, uint32_t nranges,
                               uint8_t* include, int* cleared);
 
+/* ---- daemon batching shim --------------------------------- */
+
+/* key_state::hash_objects (daemon/key_state.cc:1455-1543) hashes one or two
+ * objects per replicated op, from every daemon::loop thread at once.  A
+ * batcher coalesces those concurrent per-object calls into device batches:
+ * each caller copies its object into a pinned staging buffer and blocks; a
+ * flush thread ships a batch when it is full or `max_delay_us` after its first
+ * object, runs the hash kernel (and the region lookups of the batcher's
+ * tables) and wakes the callers.  One batcher per space (schema). */
+typedef struct hdx_batcher_s* hdx_batcher;
+typedef struct hdx_batcher_config {
+    uint32_t max_objects;    /* objects per device batch; 0 = 4096 */
+    uint32_t max_delay_us;   /* flush a partial batch this long after its first object; 0 = 50 */
+    uint64_t max_bytes;      /* payload bytes per device batch; 0 = 8 MiB */
+    uint32_t slots;          /* staging buffers in rotation (>= 2); 0 = 4 */
+    int32_t device;          /* -1 = the creating thread's current device */
+    const hdx_region_table* tables; /* optional: subspaces to look every object up in */
+    uint32_t ntables;        /* <= 16 */
+    uint32_t reserved;
+} hdx_batcher_config;
+typedef struct hdx_batcher_stats {
+    uint64_t objects;        /* objects hashed */
+    uint64_t batches;        /* device batches shipped */
+    uint64_t full_batches;   /* batches shipped because they were full */
+    uint64_t direct;         /* objects larger than max_bytes, hashed on their own */
+} hdx_batcher_stats;
+/* cfg may be NULL (all defaults).  The tables must outlive the batcher. */
+hdx_status hdx_batcher_create(const uint32_t* types, uint32_t attrs_sz, const hdx_batcher_config* cfg,
+                              hdx_batcher* out);
+/* Waits for in-flight batches, then frees everything.  No call may be in
+ * progress on the batcher. */
+hdx_status hdx_batcher_destroy(hdx_batcher b);
+/* hdx_hash_object through the batcher: blocks until the object's batch has
+ * run.  Thread-safe; any number of threads.  When the batcher has tables,
+ * region_ids[t] receives lookup_region(tables[t], hs) (region_ids may be NULL
+ * to skip).  A numeric attribute whose size is not 0 or 8 returns
+ * HDX_E_BADSIZE before the object is queued. */
+hdx_status hdx_batcher_hash_object(hdx_batcher b, const uint8_t* key, size_t key_len,
+                                   const uint8_t* const* values, const size_t* value_lens,
+                                   uint64_t* hs, uint64_t* region_ids);
+hdx_status hdx_batcher_get_stats(hdx_batcher b, hdx_batcher_stats* out);
+
 /* ---- pinned host memory ------------------------------------------------- */
 
 hdx_status hdx_alloc_pinned(size_t bytes, void** out);

@@ -1,0 +1,41 @@
+"""Daemon batching shim (hdx_batcher_*): concurrent callers of
+key_state::hash_objects coalesced into device batches.  tests/cpp/batcher_test.cc
+drives it from many threads and checks every coordinate and region id against
+the oracle; here we build it (CPU) and run it under several batch shapes (GPU)."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "cpp", "batcher_test")
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "liboracle.so"])
+    subprocess.check_call([
+        "g++", "-std=c++17", "-O2", "-Wall", "-Werror", "-pthread",
+        "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "oracle"),
+        os.path.join(ROOT, "tests", "cpp", "batcher_test.cc"), "-o", EXE,
+        "-L", os.path.join(ROOT, "hyperdex_amd"), "-lhdxhash",
+        "-L", os.path.join(ROOT, "oracle"), "-loracle",
+        "-Wl,-rpath," + os.path.join(ROOT, "hyperdex_amd") + ":" + os.path.join(ROOT, "oracle")])
+
+
+def test_batcher_test_builds():
+    build()
+    assert os.path.exists(EXE)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("args", [
+    ("16", "1500", "0", "0", "0"),      # defaults: 4096 objects, 4 slots, 50 us
+    ("8", "600", "7", "2", "10"),       # tiny batches, two slots: constant sealing/reuse
+    ("1", "200", "0", "0", "2000"),     # one caller: every batch ships on the deadline
+    ("48", "300", "64", "3", "100"),    # more callers than a batch holds
+])
+def test_batcher_concurrent_callers_match_oracle(args):
+    build()
+    r = subprocess.run([EXE, *args], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "batcher ok" in r.stdout
