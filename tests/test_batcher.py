@@ -39,3 +39,40 @@ def test_batcher_concurrent_callers_match_oracle(args):
     r = subprocess.run([EXE, *args], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "batcher ok" in r.stdout
+
+
+@pytest.mark.gpu
+def test_batcher_python_threads_match_oracle(oracle):
+    """The Python wrapper from 8 threads: every object equals the oracle."""
+    import threading
+
+    import numpy as np
+
+    import hyperdex_amd as hdx
+    types = [9217, 9218, 9219, 9217, 9474]
+    lo, up = oracle.partition(1, 64)
+    table = hdx.RegionTable([0], lo, up, np.arange(1, 65, dtype=np.uint64))
+    errors = []
+    with hdx.Batcher(types, tables=[table], max_delay_us=200) as b:
+        def worker(t):
+            rng = np.random.default_rng(t)
+            for _ in range(150):
+                key = bytes(rng.integers(0, 256, int(rng.integers(0, 120)), dtype=np.uint8))
+                vals = [bytes(rng.integers(0, 256, 8, dtype=np.uint8)) for _ in range(2)]
+                vals.append(bytes(rng.integers(0, 256, int(rng.integers(0, 70)), dtype=np.uint8)))
+                vals.append(bytes(rng.integers(0, 256, 8, dtype=np.uint8)))
+                hs, rid = b.hash_object(key, vals)
+                want = [oracle.hash_value(t_, v)[0] for t_, v in zip(types, [key] + vals)]
+                wr = oracle.lookup_region([0], lo, up, np.arange(1, 65, dtype=np.uint64),
+                                          np.array([want], np.uint64))[0]
+                if hs != want or rid != [wr]:
+                    errors.append((t, hs, want, rid, wr))
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        st = b.stats()
+    table.close()
+    assert not errors, errors[:2]
+    assert st["objects"] == 8 * 150 and st["batches"] >= 1
