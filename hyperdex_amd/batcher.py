@@ -18,7 +18,7 @@ class _Config(ctypes.Structure):
     _fields_ = [("max_objects", ctypes.c_uint32), ("max_delay_us", ctypes.c_uint32),
                 ("max_bytes", ctypes.c_uint64), ("slots", ctypes.c_uint32),
                 ("device", ctypes.c_int32), ("tables", ctypes.c_void_p),
-                ("ntables", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+                ("ntables", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
 
 
 class _Stats(ctypes.Structure):
@@ -32,13 +32,14 @@ class Batcher:
 
     def __init__(self, types: Sequence[int], tables: Sequence[RegionTable] = (),
                  max_objects: int = 0, max_delay_us: int = 0, max_bytes: int = 0,
-                 slots: int = 0, device: int = -1):
+                 slots: int = 0, device: int = -1, stage_device: bool = False):
         self.types = np.ascontiguousarray(np.asarray(types, np.uint32))
         self.A = len(self.types)
         self._tables = list(tables)  # keep the handles alive
         self._handles = (ctypes.c_void_p * max(len(tables), 1))(*[t.handle.value for t in tables])
         cfg = _Config(max_objects, max_delay_us, max_bytes, slots, device,
-                      ctypes.cast(self._handles, ctypes.c_void_p) if tables else None, len(tables), 0)
+                      ctypes.cast(self._handles, ctypes.c_void_p) if tables else None, len(tables),
+                      1 if stage_device else 0)
         h = ctypes.c_void_p()
         check(lib().hdx_batcher_create(self.types.ctypes.data, self.A, ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h

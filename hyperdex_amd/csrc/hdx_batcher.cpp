@@ -9,17 +9,25 @@
 //   caller threads    reserve (object index, byte offset) in the FILLING slot
 //                     under the lock, copy key + values into its pinned staging
 //                     outside the lock, then sleep on the slot's generation;
-//   flush thread      seals the FILLING slot when it is full or max_delay after
-//                     its first object, waits for the slot's writers to finish,
-//                     then issues H2D, the hash kernel, one lookup kernel per
-//                     table and D2H on the slot's own stream;
+//   flush thread      seals the FILLING slot as soon as no batch is in flight,
+//                     when it is full, or max_delay after its first object;
+//                     waits for the slot's writers to finish, then launches the
+//                     hash kernel and one lookup kernel for all tables on the
+//                     slot's own stream.  By default the kernels read the
+//                     pinned staging and write coordinates / region ids into
+//                     pinned memory in place (two launches per batch, no
+//                     copies); HDX_BATCHER_STAGE_DEVICE stages through HBM
+//                     (H2D, kernels, D2H) instead;
 //   completion thread waits for each shipped slot's stream in order, publishes
 //                     the status and wakes the slot's callers, who copy their
 //                     rows out; the last reader frees the slot.
 //
-// With `slots` >= 2 buffers in rotation, filling, transfer and kernels of
-// consecutive batches overlap.  Objects above max_bytes go through a private
-// slot of their own size on the caller's thread.
+// Shipping as soon as the pipeline is idle keeps a lone caller's latency at
+// one round trip, while concurrent callers pile into the next batch during
+// the current one (batch size adapts to load).  With `slots` >= 2 buffers in
+// rotation, filling, transfer and kernels of consecutive batches overlap.
+// Objects above max_bytes go through a private slot of their own size on the
+// caller's thread.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -47,11 +55,13 @@ struct Slot {
     uint32_t* h_len = nullptr;
     uint64_t* h_out = nullptr;  // coords [max_obj*A] then regions [T][max_obj]
     uint32_t* h_status = nullptr;
+    // device buffers (HDX_BATCHER_STAGE_DEVICE) or device views of the pinned ones
     uint8_t* d_blob = nullptr;
     uint64_t* d_base = nullptr;
     uint32_t* d_len = nullptr;
     uint64_t* d_out = nullptr;
     uint32_t* d_status = nullptr;
+    bool owns_device = false;
     hipStream_t stream = nullptr;
     uint32_t cap_obj = 0;
     uint64_t cap_bytes = 0;
@@ -76,6 +86,7 @@ struct hdx_batcher_s {
     uint8_t codes[HDX_MAX_ATTRS];
     uint32_t max_obj = 0;
     uint64_t max_bytes = 0;
+    bool stage_device = false;
     std::chrono::microseconds delay{50};
     std::vector<hdx_region_table> tables;
     std::vector<Slot> slots;
@@ -89,6 +100,7 @@ struct hdx_batcher_s {
     std::condition_variable cv_ship;   // completer: a slot was shipped
     int cur = -1;                      // FILLING slot, or -1 when none is free
     std::deque<int> sealed, inflight;
+    uint32_t pending = 0;              // sealed or shipped, not yet completed
     bool stop = false, flusher_done = false;
     std::thread flusher, completer;
 
@@ -105,46 +117,70 @@ void free_slot(Slot& s) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     (void)hipHostFree(s.h_blob); (void)hipHostFree(s.h_base); (void)hipHostFree(s.h_len);
     (void)hipHostFree(s.h_out); (void)hipHostFree(s.h_status);
-    (void)hipFree(s.d_blob); (void)hipFree(s.d_base); (void)hipFree(s.d_len);
-    (void)hipFree(s.d_out); (void)hipFree(s.d_status);
+    if (s.owns_device) {
+        (void)hipFree(s.d_blob); (void)hipFree(s.d_base); (void)hipFree(s.d_len);
+        (void)hipFree(s.d_out); (void)hipFree(s.d_status);
+    }
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Slot{};
+}
+
+template <typename T>
+bool device_view(T* host, T** dev) {
+    void* p = nullptr;
+    if (hipHostGetDevicePointer(&p, host, 0) != hipSuccess) return false;
+    *dev = static_cast<T*>(p);
+    return true;
 }
 
 hdx_status alloc_slot(hdx_batcher_s* b, Slot& s, uint32_t cap_obj, uint64_t cap_bytes) {
     free_slot(s);
     const size_t words = out_words(b, cap_obj);
     const size_t blob = cap_bytes + 64;  // the kernel's aligned 16-byte reads may touch the tail
-    if (hipHostMalloc((void**)&s.h_blob, blob, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&s.h_base, (size_t)cap_obj * 8, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&s.h_len, (size_t)cap_obj * b->A * 4, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&s.h_out, words * 8, hipHostMallocDefault) != hipSuccess ||
-        hipHostMalloc((void**)&s.h_status, 64, hipHostMallocDefault) != hipSuccess ||
-        hipMalloc((void**)&s.d_blob, blob) != hipSuccess ||
-        hipMalloc((void**)&s.d_base, (size_t)cap_obj * 8) != hipSuccess ||
-        hipMalloc((void**)&s.d_len, (size_t)cap_obj * b->A * 4) != hipSuccess ||
-        hipMalloc((void**)&s.d_out, words * 8) != hipSuccess ||
-        hipMalloc((void**)&s.d_status, 64) != hipSuccess ||
-        hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) != hipSuccess) {
+    const unsigned fl = hipHostMallocMapped;
+    bool ok = hipHostMalloc((void**)&s.h_blob, blob, fl) == hipSuccess &&
+              hipHostMalloc((void**)&s.h_base, (size_t)cap_obj * 8, fl) == hipSuccess &&
+              hipHostMalloc((void**)&s.h_len, (size_t)cap_obj * b->A * 4, fl) == hipSuccess &&
+              hipHostMalloc((void**)&s.h_out, words * 8, fl) == hipSuccess &&
+              hipHostMalloc((void**)&s.h_status, 64, fl) == hipSuccess &&
+              hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking) == hipSuccess;
+    if (ok && b->stage_device) {
+        s.owns_device = true;
+        ok = hipMalloc((void**)&s.d_blob, blob) == hipSuccess &&
+             hipMalloc((void**)&s.d_base, (size_t)cap_obj * 8) == hipSuccess &&
+             hipMalloc((void**)&s.d_len, (size_t)cap_obj * b->A * 4) == hipSuccess &&
+             hipMalloc((void**)&s.d_out, words * 8) == hipSuccess &&
+             hipMalloc((void**)&s.d_status, 64) == hipSuccess;
+    } else if (ok) {
+        ok = device_view(s.h_blob, &s.d_blob) && device_view(s.h_base, &s.d_base) &&
+             device_view(s.h_len, &s.d_len) && device_view(s.h_out, &s.d_out);
+        s.d_status = nullptr;  // sizes are validated on the host before staging
+    }
+    if (!ok) {
         (void)hipGetLastError();
         free_slot(s);
         return fail(HDX_E_NOMEM, "batcher staging (%u objects, %llu bytes)", cap_obj,
                     (unsigned long long)cap_bytes);
     }
+    if (s.h_status) *s.h_status = 0;
     s.cap_obj = cap_obj;
     s.cap_bytes = cap_bytes;
     return HDX_OK;
 }
 
-// H2D, hash kernel, lookups, D2H on the slot's stream (asynchronous).
+// Hash kernel + one lookup kernel for all tables on the slot's stream
+// (asynchronous), with H2D / D2H around them when staging through HBM.
 hipError_t ship(hdx_batcher_s* b, Slot& s) {
     hipError_t e;
     const uint32_t n = s.nobj;
+    const bool dev = s.owns_device;
 #define SHIP_TRY(x) if ((e = (x)) != hipSuccess) return e
-    SHIP_TRY(hipMemcpyAsync(s.d_blob, s.h_blob, s.nbytes, hipMemcpyHostToDevice, s.stream));
-    SHIP_TRY(hipMemcpyAsync(s.d_base, s.h_base, (size_t)n * 8, hipMemcpyHostToDevice, s.stream));
-    SHIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, (size_t)n * b->A * 4, hipMemcpyHostToDevice, s.stream));
-    SHIP_TRY(hipMemsetAsync(s.d_status, 0, 4, s.stream));
+    if (dev) {
+        SHIP_TRY(hipMemcpyAsync(s.d_blob, s.h_blob, s.nbytes, hipMemcpyHostToDevice, s.stream));
+        SHIP_TRY(hipMemcpyAsync(s.d_base, s.h_base, (size_t)n * 8, hipMemcpyHostToDevice, s.stream));
+        SHIP_TRY(hipMemcpyAsync(s.d_len, s.h_len, (size_t)n * b->A * 4, hipMemcpyHostToDevice, s.stream));
+        SHIP_TRY(hipMemsetAsync(s.d_status, 0, 4, s.stream));
+    }
     BatchArgs a{};
     a.blob = s.d_blob;
     a.obj_base = s.d_base;
@@ -157,27 +193,33 @@ hipError_t ship(hdx_batcher_s* b, Slot& s) {
     finalize_args(a);
     SHIP_TRY(launch_hash_batch(a, s.stream));
     const size_t region_base = (size_t)s.cap_obj * b->A;
-    for (size_t t = 0; t < b->tables.size(); ++t) {
-        const hdx_region_table tb = b->tables[t];
-        RegionArgs r{};
-        r.lower = tb->d_lower;
-        r.upper = tb->d_upper;
-        r.ids = tb->d_ids;
+    if (!b->tables.empty()) {
+        MultiRegionArgs r{};
         r.coords = s.d_out;
-        r.out = s.d_out + region_base + t * s.cap_obj;
+        r.out = s.d_out + region_base;
         r.n = n;
+        r.out_stride = s.cap_obj;
         r.A = b->A;
-        r.D = tb->D;
-        r.R = tb->R;
-        std::memcpy(r.attrs, tb->attrs, sizeof r.attrs);
-        SHIP_TRY(launch_lookup_region(r, s.stream));
+        r.T = (uint32_t)b->tables.size();
+        for (uint32_t t = 0; t < r.T; ++t) {
+            const hdx_region_table tb = b->tables[t];
+            r.t[t].lower = tb->d_lower;
+            r.t[t].upper = tb->d_upper;
+            r.t[t].ids = tb->d_ids;
+            r.t[t].D = tb->D;
+            r.t[t].R = tb->R;
+            std::memcpy(r.t[t].attrs, tb->attrs, sizeof r.t[t].attrs);
+        }
+        SHIP_TRY(launch_lookup_regions_multi(r, s.stream));
     }
-    SHIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, (size_t)n * b->A * 8, hipMemcpyDeviceToHost, s.stream));
-    if (!b->tables.empty())
-        SHIP_TRY(hipMemcpyAsync(s.h_out + region_base, s.d_out + region_base,
-                                ((b->tables.size() - 1) * s.cap_obj + n) * 8, hipMemcpyDeviceToHost,
-                                s.stream));
-    SHIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, 4, hipMemcpyDeviceToHost, s.stream));
+    if (dev) {
+        SHIP_TRY(hipMemcpyAsync(s.h_out, s.d_out, (size_t)n * b->A * 8, hipMemcpyDeviceToHost, s.stream));
+        if (!b->tables.empty())
+            SHIP_TRY(hipMemcpyAsync(s.h_out + region_base, s.d_out + region_base,
+                                    ((b->tables.size() - 1) * s.cap_obj + n) * 8, hipMemcpyDeviceToHost,
+                                    s.stream));
+        SHIP_TRY(hipMemcpyAsync(s.h_status, s.d_status, 4, hipMemcpyDeviceToHost, s.stream));
+    }
 #undef SHIP_TRY
     return hipSuccess;
 }
@@ -219,6 +261,7 @@ void copy_out(const hdx_batcher_s* b, const Slot& s, uint32_t idx, uint64_t* hs,
 void seal_locked(hdx_batcher_s* b) {
     Slot& s = b->slots[b->cur];
     s.st = SEALED;
+    ++b->pending;
     b->sealed.push_back(b->cur);
     b->cur = -1;
     for (size_t i = 0; i < b->slots.size(); ++i)
@@ -257,7 +300,7 @@ void flusher_main(hdx_batcher_s* b) {
         }
         if (b->cur >= 0 && b->slots[b->cur].nobj > 0) {
             const Clock::time_point deadline = b->slots[b->cur].first + b->delay;
-            if (b->stop || Clock::now() >= deadline) {
+            if (b->stop || b->pending == 0 || Clock::now() >= deadline) {
                 seal_locked(b);
                 continue;
             }
@@ -289,6 +332,7 @@ void completer_main(hdx_batcher_s* b) {
         s.readers = s.nobj;
         s.st = DONE;
         s.done_gen = s.gen;
+        if (--b->pending == 0) b->cv_flush.notify_one();  // the pipeline is idle: ship the next batch now
         b->cv_done.notify_all();
     }
 }
@@ -316,6 +360,7 @@ HDX_EXPORT hdx_status hdx_batcher_create(const uint32_t* types, uint32_t attrs_s
     b->max_obj = c.max_objects ? c.max_objects : 4096;
     b->max_bytes = c.max_bytes ? c.max_bytes : (8ull << 20);
     b->delay = std::chrono::microseconds(c.max_delay_us ? c.max_delay_us : 50);
+    b->stage_device = (c.flags & HDX_BATCHER_STAGE_DEVICE) != 0;
     const uint32_t nslots = c.slots ? std::max(c.slots, 2u) : 4;
     for (uint32_t t = 0; t < c.ntables; ++t) {
         if (!c.tables[t]) {

@@ -59,6 +59,25 @@ struct RegionArgs {
 
 hipError_t launch_lookup_region(const RegionArgs& a, hipStream_t stream);
 
+// Several subspaces at once (the batcher's prev/this/next lookups): table t's
+// region ids for object i go to out[t * out_stride + i].
+constexpr uint32_t kMaxMultiTables = 16;
+struct MultiRegionArgs {
+    const uint64_t* coords;  // [n*A]
+    uint64_t* out;
+    uint64_t n, out_stride;
+    uint32_t A, T;
+    struct Table {
+        const uint64_t* lower;
+        const uint64_t* upper;
+        const uint64_t* ids;
+        uint32_t D, R;
+        uint16_t attrs[16];
+    } t[kMaxMultiTables];
+};
+
+hipError_t launch_lookup_regions_multi(const MultiRegionArgs& a, hipStream_t stream);
+
 // Stored-object sweep (hdx_encoded.hip): device arrays.
 struct EncodedArgs {
     const uint8_t* keys;

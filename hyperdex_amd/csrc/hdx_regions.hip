@@ -71,4 +71,40 @@ hipError_t launch_lookup_region(const RegionArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
+// One lane per (table, object): small batches from the daemon shim, where a
+// launch per table would cost more than the lookups.  Tables are read from
+// global memory (L2-resident after the first wave).
+__global__ void __launch_bounds__(256) lookup_regions_multi_kernel(const MultiRegionArgs a) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t t = g / a.n, i = g - t * a.n;
+    if (t >= a.T) return;
+    const MultiRegionArgs::Table& tb = a.t[t];
+    const uint64_t* row = a.coords + i * a.A;
+    uint64_t h[kMaxLookupDims];
+#pragma unroll
+    for (uint32_t d = 0; d < kMaxLookupDims; ++d)
+        if (d < tb.D) h[d] = row[tb.attrs[d]];
+    uint64_t rid = 0;
+    for (uint32_t r = 0; r < tb.R; ++r) {
+        bool match = true;
+#pragma unroll
+        for (uint32_t d = 0; d < kMaxLookupDims; ++d)
+            if (d < tb.D) match &= tb.lower[r * tb.D + d] <= h[d] && h[d] <= tb.upper[r * tb.D + d];
+        if (match) {
+            rid = tb.ids[r];
+            break;
+        }
+    }
+    a.out[t * a.out_stride + i] = rid;
+}
+
+hipError_t launch_lookup_regions_multi(const MultiRegionArgs& a, hipStream_t stream) {
+    const uint64_t work = a.n * a.T;
+    if (work == 0) return hipSuccess;
+    const uint64_t blocks = (work + 255) / 256;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(lookup_regions_multi_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
 }  // namespace hdx

@@ -223,9 +223,10 @@ hdx_status hdx_search_regions(hdx_region_table table, const hdx_range* ranges, u
  * objects per replicated op, from every daemon::loop thread at once.  A
  * batcher coalesces those concurrent per-object calls into device batches:
  * each caller copies its object into a pinned staging buffer and blocks; a
- * flush thread ships a batch when it is full or `max_delay_us` after its first
- * object, runs the hash kernel (and the region lookups of the batcher's
- * tables) and wakes the callers.  One batcher per space (schema). */
+ * flush thread ships a batch as soon as the previous one has completed, when
+ * it is full, or `max_delay_us` after its first object, runs the hash kernel
+ * (and the region lookups of the batcher's tables) and wakes the callers.
+ * One batcher per space (schema). */
 typedef struct hdx_batcher_s* hdx_batcher;
 typedef struct hdx_batcher_config {
     uint32_t max_objects;    /* objects per device batch; 0 = 4096 */
@@ -235,8 +236,12 @@ typedef struct hdx_batcher_config {
     int32_t device;          /* -1 = the creating thread's current device */
     const hdx_region_table* tables; /* optional: subspaces to look every object up in */
     uint32_t ntables;        /* <= 16 */
-    uint32_t reserved;
+    uint32_t flags;          /* HDX_BATCHER_* */
 } hdx_batcher_config;
+/* Stage batches through device memory (H2D, kernels, D2H) instead of letting
+ * the kernels read and write the pinned staging buffers in place (default,
+ * fewer operations per batch; best for the small batches of a daemon). */
+#define HDX_BATCHER_STAGE_DEVICE 1u
 typedef struct hdx_batcher_stats {
     uint64_t objects;        /* objects hashed */
     uint64_t batches;        /* device batches shipped */

@@ -1,7 +1,7 @@
 // Daemon batching shim under concurrent callers, checked
 // against the oracle (test infrastructure: oracle/hdx_oracle.c).
 //
-//   batcher_test <threads> <objects per thread> <max_objects> <slots> <delay_us>
+//   batcher_test <threads> <objects per thread> <max_objects> <slots> <delay_us> [flags]
 //
 // Every thread hashes random objects of a mixed schema (every CityHash regime,
 // int64/float with special values, timestamps, a non-hashable attribute)
@@ -55,6 +55,7 @@ int main(int argc, char** argv) {
     cfg.max_objects = argc > 3 ? (uint32_t)atoi(argv[3]) : 0;
     cfg.slots = argc > 4 ? (uint32_t)atoi(argv[4]) : 0;
     cfg.max_delay_us = argc > 5 ? (uint32_t)atoi(argv[5]) : 0;
+    cfg.flags = argc > 6 ? (uint32_t)atoi(argv[6]) : 0;
     cfg.max_bytes = 64 << 10;  // objects above 64 KiB take the direct path
     cfg.device = -1;
     if (hdx_init(0) != HDX_OK) {

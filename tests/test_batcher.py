@@ -33,6 +33,7 @@ def test_batcher_test_builds():
     ("8", "600", "7", "2", "10"),       # tiny batches, two slots: constant sealing/reuse
     ("1", "200", "0", "0", "2000"),     # one caller: every batch ships on the deadline
     ("48", "300", "64", "3", "100"),    # more callers than a batch holds
+    ("16", "800", "0", "0", "0", "1"),  # staged through HBM (HDX_BATCHER_STAGE_DEVICE)
 ])
 def test_batcher_concurrent_callers_match_oracle(args):
     build()

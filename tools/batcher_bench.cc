@@ -1,6 +1,6 @@
 // Throughput and latency of the daemon batching shim.
 //
-//   batcher_bench [threads] [seconds] [max_objects] [delay_us] [tables]
+//   batcher_bench [threads] [seconds] [max_objects] [delay_us] [tables] [flags]
 //
 // `threads` callers (daemon::loop threads) each hash config-3b objects (key
 // STRING 64 B; 10 STRING U{0..195}; 3 INT64; 3 FLOAT) through
@@ -58,6 +58,7 @@ int main(int argc, char** argv) {
     cfg.max_objects = argc > 3 ? (uint32_t)atoi(argv[3]) : 0;
     cfg.max_delay_us = argc > 4 ? (uint32_t)atoi(argv[4]) : 0;
     const uint32_t ntables = argc > 5 ? (uint32_t)atoi(argv[5]) : 3;
+    cfg.flags = argc > 6 ? (uint32_t)atoi(argv[6]) : 0;
     cfg.device = -1;
     if (hdx_init(0) != HDX_OK) {
         fprintf(stderr, "init: %s\n", hdx_last_error());
@@ -145,11 +146,11 @@ int main(int argc, char** argv) {
     const double objs_s = (double)(s1.objects - s0.objects) / el;
     const double batches = (double)(s1.batches - s0.batches);
     printf("{\"tool\": \"batcher_bench\", \"threads\": %d, \"tables\": %u, \"max_objects\": %u, "
-           "\"max_delay_us\": %u, \"objects_per_s\": %.0f, \"batches_per_s\": %.0f, "
+           "\"max_delay_us\": %u, \"flags\": %u, \"objects_per_s\": %.0f, \"batches_per_s\": %.0f, "
            "\"mean_batch\": %.1f, \"full_batches\": %llu, \"lat_us_p50\": %.1f, \"lat_us_p90\": %.1f, "
            "\"lat_us_p99\": %.1f, \"lat_us_max\": %.1f, \"errors\": %ld}\n",
            threads, cfg.ntables, cfg.max_objects ? cfg.max_objects : 4096,
-           cfg.max_delay_us ? cfg.max_delay_us : 50, objs_s, batches / el,
+           cfg.max_delay_us ? cfg.max_delay_us : 50, cfg.flags, objs_s, batches / el,
            batches > 0 ? (double)(s1.objects - s0.objects) / batches : 0.0,
            (unsigned long long)(s1.full_batches - s0.full_batches), pct(0.5), pct(0.9), pct(0.99),
            pct(1.0), errors.load());
