@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-allgather", action="store_true")
+    ap.add_argument("--no-regions", action="store_true",
+                    help="skip the coordinates -> region ids step (SURVEY §8f-1)")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip timing the host-resident (PCIe-inclusive) path")
     ap.add_argument("--traffic", default=latest_traffic_file(),
@@ -160,13 +162,16 @@ def main():
                      "traffic": measured_traffic(args.traffic, cfg, n),
                      "kernel_ms": round(kernel_ms, 4),
                      "algorithmic_bytes_per_launch": algo_bytes,
-                     "kernel": "hdx::hash_chunk_kernel / hash_pipelined_kernel (auto per schema)"},
+                     "kernel": hdx.hashing.kernel_for(types, n)[1]},
     }
 
     if cfg == "cfg5":
         result["roofline"]["kernel"] = "hdx::hash_encoded_kernel (decode_value + hash)"
     if world > 1 and not args.no_allgather:
         result["allgather"] = time_allgather(coords, world, dev, backend, max_over_ranks)
+    if not args.no_regions:
+        result["regions"] = time_regions(coords, world, dev, backend, max_over_ranks, stream,
+                                         gather=world > 1 and not args.no_allgather)
 
     if not args.no_host_path and rank == 0 and world == 1 and cfg != "cfg5":
         result["host_path"] = time_host_path(types, blob, base, lens, A)
@@ -205,6 +210,74 @@ def time_allgather(coords, world, dev, backend, max_over_ranks, reps=3):
     nbytes = out.numel() * 8
     return {"ms": round(dt * 1e3, 3), "bytes": nbytes, "backend": backend,
             "busbw_GBps": round(nbytes * (world - 1) / world / dt / 1e9, 2)}
+
+
+def key_subspace_tables(A):
+    """Region tables of a space like the reference's default: the key subspace
+    (attrs {0}) in 64 equal intervals (admin/partition.cc for 1 attribute, 64
+    servers) and a 3-attribute subspace {1, 2, 3} in 4 x 4 x 4 cells
+    (partition(3, 64) -> 64 regions)."""
+    import numpy as np
+
+    from hyperdex_amd import RegionTable
+    i = np.arange(64, dtype=np.uint64)
+    lo1 = (i << np.uint64(58)).reshape(64, 1)
+    up1 = (lo1 + np.uint64((1 << 58) - 1))
+    tables = [RegionTable([0], lo1, up1, i + np.uint64(1))]
+    if A >= 4:
+        c = np.arange(4, dtype=np.uint64)
+        cells = np.array([(x, y, z) for x in c for y in c for z in c], np.uint64)
+        lo3 = cells << np.uint64(62)
+        up3 = lo3 + np.uint64((1 << 62) - 1)
+        tables.append(RegionTable([1, 2, 3], lo3, up3, np.arange(65, 129, dtype=np.uint64)))
+    return tables
+
+
+def time_regions(coords, world, dev, backend, max_over_ranks, stream, gather, reps=10):
+    """configuration::lookup_region for every object (hdx_lookup_region_device)
+    on the key subspace and a 3-attribute subspace, and — multi-GPU — the
+    all-gather of the region ids instead of the coordinates."""
+    import torch
+    import torch.distributed as dist
+
+    from hyperdex_amd import lookup_region
+    n, A = coords.shape
+    tables = key_subspace_tables(A)
+    outs = [torch.empty(n, dtype=torch.int64, device=dev) for _ in tables]
+    res = {"objects": n, "tables": [{"dims": int(len(t.attrs)), "regions": int(len(t.ids))}
+                                    for t in tables]}
+    for t, o in zip(tables, outs):
+        lookup_region(t, coords, out=o, stream=stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    torch.cuda.synchronize()
+    for s, e in ev:
+        s.record(stream)
+        for t, o in zip(tables, outs):
+            lookup_region(t, coords, out=o, stream=stream)
+        e.record(stream)
+    torch.cuda.synchronize()
+    (ms,) = max_over_ranks(float(np.mean([s.elapsed_time(e) for s, e in ev])))
+    res["lookup_ms"] = round(ms, 4)
+    res["lookup_mobjects_per_s"] = round(n * world / (ms / 1e3) / 1e6, 1)
+    if gather:
+        from hyperdex_amd.dist import allgather_coords
+        ids = torch.stack(outs, 1).contiguous()
+        src = ids if backend == "nccl" else ids[: min(n, 1_000_000)].cpu()
+        counts = [src.shape[0]] * world
+        allgather_coords(src, counts)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            out = allgather_coords(src, counts)
+        torch.cuda.synchronize()
+        (dt,) = max_over_ranks((time.perf_counter() - t0) / 3)
+        res["allgather_ids_ms"] = round(dt * 1e3, 3)
+        res["allgather_ids_bytes"] = out.numel() * 8
+    for t in tables:
+        t.close()
+    return res
 
 
 def latest_traffic_file():

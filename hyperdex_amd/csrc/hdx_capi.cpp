@@ -572,3 +572,14 @@ HDX_EXPORT hdx_status hdx_lookup_region_device(hdx_region_table t, const uint64_
 
 HDX_EXPORT int hdxdbg_set_kernel_variant(int variant) { return set_hash_variant(variant); }
 HDX_EXPORT int hdxdbg_kernel_variant(void) { return hash_variant(); }
+
+HDX_EXPORT int hdxdbg_kernel_for(const uint32_t* types, uint32_t attrs_sz, uint64_t n, const char** name) {
+    BatchArgs a{};
+    if (check_schema(types, attrs_sz, a.codes) != HDX_OK) return -2;
+    a.A = attrs_sz;
+    a.n = n;
+    finalize_args(a);
+    const int v = chosen_variant(a);
+    if (name) *name = variant_kernel_name(v);
+    return v;
+}

@@ -43,6 +43,9 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
 // The variant launch_hash_batch uses: HDX_KERNEL_VARIANT (tuning knob) or the default.
 int hash_variant();
 int set_hash_variant(int v);  // -2 if unknown, else the previous selection (-1 = auto)
+// The variant launch_hash_batch would run for args, and its kernel's symbol.
+int chosen_variant(const BatchArgs& args);
+const char* variant_kernel_name(int v);
 
 // Region lookup (hdx_regions.hip): table pointers are device memory owned by
 // an hdx_region_table handle; attrs[] holds the subspace's attribute indices.

@@ -365,4 +365,25 @@ hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream) {
     return launch_hash_batch_variant(args, stream, v < 0 ? auto_variant(args) : v);
 }
 
+int chosen_variant(const BatchArgs& args) {
+    const int v = hash_variant();
+    return v < 0 ? auto_variant(args) : v;
+}
+
+// The kernel symbol a variant launches, as rocprofv3 prints it.
+const char* variant_kernel_name(int v) {
+    switch (v) {
+        case 12: return "void hdx::hash_chunk_kernel<true>(hdx::BatchArgs)";
+        case 18: return "void hdx::hash_regroup_kernel<4, true, true, true>(hdx::BatchArgs)";
+        case 19: return "void hdx::hash_regroup_kernel<8, true, true, true>(hdx::BatchArgs)";
+        case 20: return "void hdx::hash_regroup_kernel<8, true, false, true>(hdx::BatchArgs)";
+        case 21: return "void hdx::hash_regroup_kernel<4, true, false, true>(hdx::BatchArgs)";
+        case 22: return "void hdx::hash_regroup_kernel<16, true, false, true>(hdx::BatchArgs)";
+        case 23: return "void hdx::hash_regroup_kernel<8, true, false, false>(hdx::BatchArgs)";
+        case 24: return "void hdx::hash_regroup_kernel<4, true, false, false>(hdx::BatchArgs)";
+        case 25: return "void hdx::hash_regroup_kernel<16, true, false, false>(hdx::BatchArgs)";
+        default: return "";
+    }
+}
+
 }  // namespace hdx

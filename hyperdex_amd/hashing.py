@@ -136,3 +136,11 @@ def hash_encoded(types, keys, key_off, key_len, vals, val_off, val_len, coords=N
         versions.data_ptr() if versions is not None else None,
         status.data_ptr() if status is not None else None, handle))
     return coords
+
+
+def kernel_for(types, n: int):
+    """(variant, kernel symbol) hash_batch would launch for this schema and n."""
+    t = _u32_array(types)
+    name = ctypes.c_char_p()
+    v = lib().hdxdbg_kernel_for(t.ctypes.data, len(t), n, ctypes.byref(name))
+    return v, (name.value or b"").decode()

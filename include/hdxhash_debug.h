@@ -5,6 +5,8 @@
 #ifndef HDXHASH_DEBUG_H
 #define HDXHASH_DEBUG_H
 
+#include <stdint.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -15,6 +17,10 @@ extern "C" {
  * changed). */
 int hdxdbg_set_kernel_variant(int variant);
 int hdxdbg_kernel_variant(void);
+/* The variant hdx_hash_batch_device would launch for this schema and object
+ * count (under the current selection), and the kernel's symbol as rocprofv3
+ * reports it (*name; static string).  Returns -2 on a bad schema. */
+int hdxdbg_kernel_for(const uint32_t* types, uint32_t attrs_sz, uint64_t n, const char** name);
 
 #ifdef __cplusplus
 }

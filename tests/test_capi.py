@@ -104,3 +104,16 @@ def test_variant_hook():
     assert lib.hdxdbg_set_kernel_variant(0) == -2  # retired variant
     assert lib.hdxdbg_set_kernel_variant(12) == cur
     assert lib.hdxdbg_set_kernel_variant(cur) == 12
+
+
+def test_kernel_for_reports_the_auto_policy():
+    """hdxdbg_kernel_for: the variant/kernel the automatic policy picks per
+    schema, with no device needed."""
+    from hyperdex_amd import synth
+    from hyperdex_amd.hashing import kernel_for
+    want = {"cfg1": 12, "cfg2": 21, "cfg3a": 25, "cfg3b": 12, "mixed": 19}
+    for cfg, v in want.items():
+        got, name = kernel_for([r.type for r in synth.CONFIGS[cfg]], 10_000_000)
+        assert got == v and name.startswith("void hdx::hash_"), (cfg, got, name)
+    assert kernel_for([9217] * 17, 1000)[0] == 12  # small grids keep the one-chunk kernel
+    assert kernel_for([12345], 10)[0] == -2
