@@ -306,13 +306,15 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 23: return launch_regroup<8, true, false, false>(args, stream);
         case 24: return launch_regroup<4, true, false, false>(args, stream);
         case 25: return launch_regroup<16, true, false, false>(args, stream);
+        case 26: return launch_regroup<2, true>(args, stream);
+        case 27: return launch_regroup<2, true, false>(args, stream);
         default: return hipErrorInvalidValue;
     }
 }
 
 static constexpr int kDefaultVariant = -1;  // automatic
 // 33 selects the stored-object sweep with its phase-0 line touch (hdx_encoded.hip).
-static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 25) || v == 33; }
+static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 27) || v == 33; }
 
 static int g_variant = [] {
     const char* e = getenv("HDX_KERNEL_VARIANT");
@@ -382,6 +384,8 @@ const char* variant_kernel_name(int v) {
         case 23: return "void hdx::hash_regroup_kernel<8, true, false, false>(hdx::BatchArgs)";
         case 24: return "void hdx::hash_regroup_kernel<4, true, false, false>(hdx::BatchArgs)";
         case 25: return "void hdx::hash_regroup_kernel<16, true, false, false>(hdx::BatchArgs)";
+        case 26: return "void hdx::hash_regroup_kernel<2, true, true, true>(hdx::BatchArgs)";
+        case 27: return "void hdx::hash_regroup_kernel<2, true, false, true>(hdx::BatchArgs)";
         default: return "";
     }
 }

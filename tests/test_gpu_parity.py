@@ -267,3 +267,29 @@ def test_full_size_sampled(oracle, torch_dev, cfg):
     assert np.array_equal(got, want)
     del blob, base, lens, c1, c2
     torch.cuda.empty_cache()
+
+
+VARIANTS = [12, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27]
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+def test_every_kernel_variant_matches_oracle(oracle, torch_dev, variant):
+    """The automatic policy picks among these per schema and size (DESIGN.md
+    §4.3), and scripts/ab_variants.py times them: each must be bit-exact on
+    every config, on ragged object counts and on shuffled objects."""
+    torch, dev = torch_dev
+    lib = _lib.lib()
+    prev = lib.hdxdbg_set_kernel_variant(variant)
+    assert prev != -2
+    try:
+        for cfg, n in [("cfg1", 777), ("cfg2", 1001), ("cfg3a", 257), ("cfg3b", 1500),
+                       ("mixed", 900), ("wide", 131), ("keyonly_long", 70)]:
+            types, blob, base, lens = synth.make_batch_host(cfg, n, seed=variant * 100 + n)
+            check_batch(oracle, torch, dev, types, blob, base, lens)
+        types, blob, base, lens = synth.make_batch_host("cfg3b", 999, seed=5)
+        perm = np.random.default_rng(variant).permutation(999)
+        A = len(types)
+        check_batch(oracle, torch, dev, types, blob, base[perm],
+                    lens.reshape(999, A)[perm].reshape(-1))
+    finally:
+        lib.hdxdbg_set_kernel_variant(prev)
