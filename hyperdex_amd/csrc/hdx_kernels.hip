@@ -19,6 +19,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "hdx_device_hash.h"
 #include "hdx_internal.h"
 #include "hdx_loads.h"
@@ -136,11 +138,21 @@ struct RegroupLds {
     SlotDesc desc[4][C * 64];   // reused for the coordinates in phase 2
     uint16_t perm[4][C * 64];
 };
+// STAGE: each slot's four 16-byte pieces (Blk) are loaded in slot order in
+// phase 1 and parked in LDS, so the class-sorted passes read them from LDS
+// instead of gathering from global memory out of order.
+template <int C>
+struct RegroupStageLds {
+    SlotDesc desc[4][C * 64];
+    uint16_t perm[4][C * 64];
+    Blk blk[4][C * 64];
+};
 
-template <int C, bool NT_STORE, bool SORT = true, bool DIRECT = true>
+template <int C, bool NT_STORE, bool SORT = true, bool DIRECT = true, bool STAGE = false>
 __global__ void __launch_bounds__(256)
 hash_regroup_kernel(const BatchArgs args) {
-    __shared__ RegroupLds<C> lds;
+    typedef typename std::conditional<STAGE, RegroupStageLds<C>, RegroupLds<C>>::type Lds;
+    __shared__ Lds lds;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     SlotDesc* desc = lds.desc[w];
@@ -171,6 +183,11 @@ hash_regroup_kernel(const BatchArgs args) {
 
     // ---- phase 1: descriptors + classes -------------------------------------
     uint32_t cls[C];
+    Blk staged[STAGE ? C : 1];
+    auto lds_blk = [&](uint32_t s) -> Blk& {
+        if constexpr (STAGE) return lds.blk[w][s];
+        else return staged[0];
+    };
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const uint32_t t = j0 + (uint32_t)(c * 64 + lane);
@@ -195,6 +212,11 @@ hash_regroup_kernel(const BatchArgs args) {
         d.code_slot = code | ((uint32_t)(c * 64 + lane) << 8);
         desc[c * 64 + lane] = d;
         cls[c] = work_class(code, L, valid);
+        if constexpr (STAGE) staged[c] = issue_block(code, d.p, L);
+    }
+    if constexpr (STAGE) {
+#pragma unroll
+        for (int c = 0; c < C; ++c) lds_blk(c * 64 + lane) = staged[c];
     }
 
     // ---- counting sort by class (wave-local) ---------------------------------
@@ -233,7 +255,8 @@ hash_regroup_kernel(const BatchArgs args) {
     auto load_pass = [&](int t, Pass& P) {
         const uint32_t s = uniform ? (uint32_t)(t * 64 + lane) : perm[t * 64 + lane];
         P.d = desc[s];
-        P.blk = issue_block(P.d.code_slot & 0xffu, P.d.p, P.d.n);
+        if constexpr (STAGE) P.blk = lds_blk(s);
+        else P.blk = issue_block(P.d.code_slot & 0xffu, P.d.p, P.d.n);
     };
     bool bad = false;
     Pass P0, P1;
@@ -275,13 +298,14 @@ hash_regroup_kernel(const BatchArgs args) {
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <int C, bool NT, bool SORT = true, bool DIRECT = true>
+template <int C, bool NT, bool SORT = true, bool DIRECT = true, bool STAGE = false>
 static hipError_t launch_regroup(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT, DIRECT>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT, DIRECT, STAGE>), dim3((uint32_t)blocks), dim3(256), 0, stream,
+                       args);
     return hipGetLastError();
 }
 
@@ -308,13 +332,15 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 25: return launch_regroup<16, true, false, false>(args, stream);
         case 26: return launch_regroup<2, true>(args, stream);
         case 27: return launch_regroup<2, true, false>(args, stream);
+        case 28: return launch_regroup<2, true, true, true, true>(args, stream);
+        case 29: return launch_regroup<4, true, true, true, true>(args, stream);
         default: return hipErrorInvalidValue;
     }
 }
 
 static constexpr int kDefaultVariant = -1;  // automatic
 // 33 selects the stored-object sweep with its phase-0 line touch (hdx_encoded.hip).
-static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 27) || v == 33; }
+static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 29) || v == 33; }
 
 static int g_variant = [] {
     const char* e = getenv("HDX_KERNEL_VARIANT");
@@ -386,6 +412,8 @@ const char* variant_kernel_name(int v) {
         case 25: return "void hdx::hash_regroup_kernel<16, true, false, false>(hdx::BatchArgs)";
         case 26: return "void hdx::hash_regroup_kernel<2, true, true, true>(hdx::BatchArgs)";
         case 27: return "void hdx::hash_regroup_kernel<2, true, false, true>(hdx::BatchArgs)";
+        case 28: return "void hdx::hash_regroup_kernel<2, true, true, true, true>(hdx::BatchArgs)";
+        case 29: return "void hdx::hash_regroup_kernel<4, true, true, true, true>(hdx::BatchArgs)";
         default: return "";
     }
 }
