@@ -35,6 +35,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -70,10 +71,15 @@ struct Slot {
     uint32_t nobj = 0;
     uint64_t nbytes = 0;
     uint32_t writers = 0;
-    uint32_t readers = 0;
     uint64_t gen = 0;       // bumped each time the slot starts filling
-    uint64_t done_gen = 0;  // == gen once the slot's batch has completed
     hdx_status result = HDX_OK;
+    // completion, published without the batcher's mutex: callers spin briefly
+    // on done_gen, then sleep on the slot's own condition variable, and copy
+    // their rows out lock-free; the last reader frees the slot
+    std::atomic<uint64_t> done_gen{0};  // == gen once the slot's batch has completed
+    std::atomic<uint32_t> readers{0};
+    std::mutex done_mu;
+    std::condition_variable done_cv;
     Clock::time_point first;
     bool full = false;
 };
@@ -89,13 +95,13 @@ struct hdx_batcher_s {
     bool stage_device = false;
     std::chrono::microseconds delay{50};
     std::vector<hdx_region_table> tables;
-    std::vector<Slot> slots;
+    std::unique_ptr<Slot[]> slots;  // fixed at creation (Slot holds atomics and a mutex)
+    uint32_t nslots = 0;
     Slot direct;  // oversized objects, under direct_mu
     std::mutex direct_mu;
 
     std::mutex mu;
     std::condition_variable cv_flush;  // flusher: new object, seal, last writer done, stop
-    std::condition_variable cv_done;   // callers: a slot completed
     std::condition_variable cv_free;   // callers: a slot became FILLING
     std::condition_variable cv_ship;   // completer: a slot was shipped
     int cur = -1;                      // FILLING slot, or -1 when none is free
@@ -122,7 +128,12 @@ void free_slot(Slot& s) {
         (void)hipFree(s.d_out); (void)hipFree(s.d_status);
     }
     if (s.stream) (void)hipStreamDestroy(s.stream);
-    s = Slot{};
+    s.h_blob = nullptr; s.h_base = nullptr; s.h_len = nullptr; s.h_out = nullptr; s.h_status = nullptr;
+    s.d_blob = nullptr; s.d_base = nullptr; s.d_len = nullptr; s.d_out = nullptr; s.d_status = nullptr;
+    s.owns_device = false;
+    s.stream = nullptr;
+    s.cap_obj = 0;
+    s.cap_bytes = 0;
 }
 
 template <typename T>
@@ -264,7 +275,7 @@ void seal_locked(hdx_batcher_s* b) {
     ++b->pending;
     b->sealed.push_back(b->cur);
     b->cur = -1;
-    for (size_t i = 0; i < b->slots.size(); ++i)
+    for (uint32_t i = 0; i < b->nslots; ++i)
         if (b->slots[i].st == FREE) {
             Slot& f = b->slots[i];
             f.st = FILLING;
@@ -329,11 +340,14 @@ void completer_main(hdx_batcher_s* b) {
         hdx_status st = finish(s, shipped == HDX_OK ? hipSuccess : hipErrorUnknown);
         lk.lock();
         s.result = st;
-        s.readers = s.nobj;
         s.st = DONE;
-        s.done_gen = s.gen;
+        s.readers.store(s.nobj, std::memory_order_relaxed);
+        {
+            std::lock_guard<std::mutex> dl(s.done_mu);
+            s.done_gen.store(s.gen, std::memory_order_release);
+        }
+        s.done_cv.notify_all();
         if (--b->pending == 0) b->cv_flush.notify_one();  // the pipeline is idle: ship the next batch now
-        b->cv_done.notify_all();
     }
 }
 
@@ -380,10 +394,11 @@ HDX_EXPORT hdx_status hdx_batcher_create(const uint32_t* types, uint32_t attrs_s
             }
         b->tables.push_back(c.tables[t]);
     }
-    b->slots.resize(nslots);
-    for (auto& s : b->slots)
-        if ((st = alloc_slot(b, s, b->max_obj, b->max_bytes)) != HDX_OK) {
-            for (auto& f : b->slots) free_slot(f);
+    b->slots.reset(new Slot[nslots]);
+    b->nslots = nslots;
+    for (uint32_t i = 0; i < nslots; ++i)
+        if ((st = alloc_slot(b, b->slots[i], b->max_obj, b->max_bytes)) != HDX_OK) {
+            for (uint32_t f = 0; f < nslots; ++f) free_slot(b->slots[f]);
             delete b;
             return st;
         }
@@ -406,7 +421,7 @@ HDX_EXPORT hdx_status hdx_batcher_destroy(hdx_batcher b) {
     b->flusher.join();
     b->completer.join();
     (void)hipSetDevice(b->device);
-    for (auto& s : b->slots) free_slot(s);
+    for (uint32_t i = 0; i < b->nslots; ++i) free_slot(b->slots[i]);
     free_slot(b->direct);
     delete b;
     return HDX_OK;
@@ -499,10 +514,20 @@ HDX_EXPORT hdx_status hdx_batcher_hash_object(hdx_batcher b, const uint8_t* key,
 
     lk.lock();
     if (--s.writers == 0 && s.st == SEALED) b->cv_flush.notify_one();
-    b->cv_done.wait(lk, [&] { return s.done_gen == gen; });
+    lk.unlock();
+
+    // wait for the batch: spin for about one round trip, then sleep
+    const Clock::time_point spin_until = Clock::now() + std::chrono::microseconds(100);
+    while (s.done_gen.load(std::memory_order_acquire) != gen && Clock::now() < spin_until)
+        __builtin_ia32_pause();
+    if (s.done_gen.load(std::memory_order_acquire) != gen) {
+        std::unique_lock<std::mutex> dl(s.done_mu);
+        s.done_cv.wait(dl, [&] { return s.done_gen.load(std::memory_order_acquire) == gen; });
+    }
     const hdx_status st = s.result;
     if (st == HDX_OK) copy_out(b, s, idx, hs, region_ids);
-    if (--s.readers == 0) {
+    if (s.readers.fetch_sub(1, std::memory_order_acq_rel) == 1) {
+        lk.lock();
         s.st = FREE;
         if (b->cur < 0) {
             s.st = FILLING;
@@ -513,8 +538,8 @@ HDX_EXPORT hdx_status hdx_batcher_hash_object(hdx_batcher b, const uint8_t* key,
             b->cur = si;
         }
         b->cv_free.notify_all();
+        lk.unlock();
     }
-    lk.unlock();
     b->n_objects.fetch_add(1, std::memory_order_relaxed);
     if (st == HDX_E_DEVICE) return fail(st, "batcher: device error");
     if (st == HDX_E_BADSIZE) return fail(st, "batcher: numeric value of bad size");

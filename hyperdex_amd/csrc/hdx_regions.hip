@@ -72,13 +72,51 @@ hipError_t launch_lookup_region(const RegionArgs& a, hipStream_t stream) {
 }
 
 // One lane per (table, object): small batches from the daemon shim, where a
-// launch per table would cost more than the lookups.  Tables are read from
-// global memory (L2-resident after the first wave).
+// launch per table would cost more than the lookups.  Every table's boxes
+// and ids are staged in LDS per workgroup (the walk is then LDS broadcasts,
+// as in lookup_region_kernel); tables too large for that are walked in global
+// memory.
+struct MultiLayout {
+    uint32_t lower[kMaxMultiTables], upper[kMaxMultiTables], ids[kMaxMultiTables];  // u64 offsets
+    uint32_t words;
+};
+
+__host__ __device__ inline MultiLayout multi_layout(const MultiRegionArgs& a) {
+    MultiLayout l{};
+    uint32_t w = 0;
+    for (uint32_t t = 0; t < a.T; ++t) {
+        const uint32_t box = a.t[t].R * a.t[t].D;
+        l.lower[t] = w;
+        l.upper[t] = w + box;
+        l.ids[t] = w + 2 * box;
+        w += 2 * box + a.t[t].R;
+    }
+    l.words = w;
+    return l;
+}
+
+template <bool IN_LDS>
 __global__ void __launch_bounds__(256) lookup_regions_multi_kernel(const MultiRegionArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    const MultiLayout l = multi_layout(a);
+    if (IN_LDS) {
+        for (uint32_t t = 0; t < a.T; ++t) {
+            const uint32_t box = a.t[t].R * a.t[t].D;
+            for (uint32_t k = threadIdx.x; k < box; k += blockDim.x) {
+                smem[l.lower[t] + k] = a.t[t].lower[k];
+                smem[l.upper[t] + k] = a.t[t].upper[k];
+            }
+            for (uint32_t k = threadIdx.x; k < a.t[t].R; k += blockDim.x) smem[l.ids[t] + k] = a.t[t].ids[k];
+        }
+        __syncthreads();
+    }
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t t = g / a.n, i = g - t * a.n;
     if (t >= a.T) return;
     const MultiRegionArgs::Table& tb = a.t[t];
+    const uint64_t* lower = IN_LDS ? smem + l.lower[t] : tb.lower;
+    const uint64_t* upper = IN_LDS ? smem + l.upper[t] : tb.upper;
+    const uint64_t* ids = IN_LDS ? smem + l.ids[t] : tb.ids;
     const uint64_t* row = a.coords + i * a.A;
     uint64_t h[kMaxLookupDims];
 #pragma unroll
@@ -89,9 +127,9 @@ __global__ void __launch_bounds__(256) lookup_regions_multi_kernel(const MultiRe
         bool match = true;
 #pragma unroll
         for (uint32_t d = 0; d < kMaxLookupDims; ++d)
-            if (d < tb.D) match &= tb.lower[r * tb.D + d] <= h[d] && h[d] <= tb.upper[r * tb.D + d];
+            if (d < tb.D) match &= lower[r * tb.D + d] <= h[d] && h[d] <= upper[r * tb.D + d];
         if (match) {
-            rid = tb.ids[r];
+            rid = ids[r];
             break;
         }
     }
@@ -103,7 +141,11 @@ hipError_t launch_lookup_regions_multi(const MultiRegionArgs& a, hipStream_t str
     if (work == 0) return hipSuccess;
     const uint64_t blocks = (work + 255) / 256;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(lookup_regions_multi_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+    const size_t lds = (size_t)multi_layout(a).words * 8;
+    if (lds <= 48 * 1024)
+        hipLaunchKernelGGL(lookup_regions_multi_kernel<true>, dim3((uint32_t)blocks), dim3(256), lds, stream, a);
+    else
+        hipLaunchKernelGGL(lookup_regions_multi_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
