@@ -111,7 +111,10 @@ struct hdx_batcher_s {
     std::thread flusher, completer;
 
     std::atomic<uint64_t> n_objects{0}, n_batches{0}, n_full{0}, n_direct{0};
+    std::atomic<int> spinners{0};
 };
+
+static constexpr int kMaxSpinners = 2;
 
 namespace {
 
@@ -516,10 +519,15 @@ HDX_EXPORT hdx_status hdx_batcher_hash_object(hdx_batcher b, const uint8_t* key,
     if (--s.writers == 0 && s.st == SEALED) b->cv_flush.notify_one();
     lk.unlock();
 
-    // wait for the batch: spin for about one round trip, then sleep
-    const Clock::time_point spin_until = Clock::now() + std::chrono::microseconds(100);
-    while (s.done_gen.load(std::memory_order_acquire) != gen && Clock::now() < spin_until)
-        __builtin_ia32_pause();
+    // wait for the batch: a few callers spin for about one round trip (the
+    // rest sleep at once, so spinners never starve the flush and completion
+    // threads of CPU), then sleep
+    if (b->spinners.fetch_add(1, std::memory_order_relaxed) < kMaxSpinners) {
+        const Clock::time_point spin_until = Clock::now() + std::chrono::microseconds(100);
+        while (s.done_gen.load(std::memory_order_acquire) != gen && Clock::now() < spin_until)
+            __builtin_ia32_pause();
+    }
+    b->spinners.fetch_sub(1, std::memory_order_relaxed);
     if (s.done_gen.load(std::memory_order_acquire) != gen) {
         std::unique_lock<std::mutex> dl(s.done_mu);
         s.done_cv.wait(dl, [&] { return s.done_gen.load(std::memory_order_acquire) == gen; });

@@ -150,7 +150,12 @@ __device__ __forceinline__ uint64_t city_gt64_reg(const uint8_t* s, uint32_t n, 
     u64x2 b0 = gld16(s), b1 = gld16(s + 16), b2 = gld16(s + 32), b3 = gld16(s + 48);
     x = x * K1 + b0.x;
     const uint32_t blocks = (n - 1) >> 6;
+    // software-pipelined: block k+1 is in flight while block k is mixed (the
+    // last iteration re-reads its own block, so the loads stay unconditional)
+    const uint8_t* last = s + 64 * (blocks - 1);
     for (uint32_t k = 0;;) {
+        const uint8_t* ns = s + 64 < last ? s + 64 : last;
+        const u64x2 n0 = gld16(ns), n1 = gld16(ns + 16), n2 = gld16(ns + 32), n3 = gld16(ns + 48);
         x = ror(x + y + v0 + b0.y, 37) * K1;
         y = ror(y + v1 + b3.x, 42) * K1;
         x ^= w1;
@@ -162,8 +167,8 @@ __device__ __forceinline__ uint64_t city_gt64_reg(const uint8_t* s, uint32_t n, 
         v0 = nv0; v1 = nv1; w0 = nw0; w1 = nw1;
         const uint64_t tt = z; z = x; x = tt;
         if (++k == blocks) break;
-        s += 64;
-        b0 = gld16(s); b1 = gld16(s + 16); b2 = gld16(s + 32); b3 = gld16(s + 48);
+        s = ns;
+        b0 = n0; b1 = n1; b2 = n2; b3 = n3;
     }
     return mix16(mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z, mix16(v1, w1, KMUL) + x, KMUL);
 }
