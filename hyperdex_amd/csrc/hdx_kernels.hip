@@ -55,7 +55,7 @@ __device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
     return __builtin_amdgcn_readlane(wave_scan_dpp(v), 63);
 }
 
-template <bool NT_STORE>
+template <bool NT_STORE, bool PIPE = false>
 __global__ void __launch_bounds__(256)
 hash_chunk_kernel(const BatchArgs args) {
     const int lane = threadIdx.x & 63;
@@ -101,7 +101,7 @@ hash_chunk_kernel(const BatchArgs args) {
     const Blk blk = issue_block(valid ? code : (uint32_t)CODE_ZERO, p, L);
     if (valid) {
         bool bad = false;
-        const uint64_t h = hash_blk(code, p, L, blk, bad);
+        const uint64_t h = hash_blk<PIPE>(code, p, L, blk, bad);
         if (NT_STORE) __builtin_nontemporal_store(h, args.coords + q0 + lane);
         else args.coords[q0 + lane] = h;
         if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
@@ -309,13 +309,13 @@ static hipError_t launch_regroup(const BatchArgs& args, hipStream_t stream) {
     return hipGetLastError();
 }
 
-template <bool NT>
+template <bool NT, bool PIPE = false>
 static hipError_t launch_chunk(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + 63) / 64;
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_chunk_kernel<NT>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_chunk_kernel<NT, PIPE>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
     return hipGetLastError();
 }
 
@@ -334,13 +334,14 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 27: return launch_regroup<2, true, false>(args, stream);
         case 28: return launch_regroup<2, true, true, true, true>(args, stream);
         case 29: return launch_regroup<4, true, true, true, true>(args, stream);
+        case 30: return launch_chunk<true, true>(args, stream);
         default: return hipErrorInvalidValue;
     }
 }
 
 static constexpr int kDefaultVariant = -1;  // automatic
 // 33 selects the stored-object sweep with its phase-0 line touch (hdx_encoded.hip).
-static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 29) || v == 33; }
+static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 30) || v == 33; }
 
 static int g_variant = [] {
     const char* e = getenv("HDX_KERNEL_VARIANT");
@@ -401,7 +402,8 @@ int chosen_variant(const BatchArgs& args) {
 // The kernel symbol a variant launches, as rocprofv3 prints it.
 const char* variant_kernel_name(int v) {
     switch (v) {
-        case 12: return "void hdx::hash_chunk_kernel<true>(hdx::BatchArgs)";
+        case 12: return "void hdx::hash_chunk_kernel<true, false>(hdx::BatchArgs)";
+        case 30: return "void hdx::hash_chunk_kernel<true, true>(hdx::BatchArgs)";
         case 18: return "void hdx::hash_regroup_kernel<4, true, true, true>(hdx::BatchArgs)";
         case 19: return "void hdx::hash_regroup_kernel<8, true, true, true>(hdx::BatchArgs)";
         case 20: return "void hdx::hash_regroup_kernel<8, true, false, true>(hdx::BatchArgs)";

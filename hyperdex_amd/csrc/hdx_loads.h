@@ -139,6 +139,9 @@ __device__ __forceinline__ uint64_t city_le16_reg(const u64x2& w, uint32_t n) {
 
 // city.cc:361-397 for n > 64 with the tail block in registers; the first
 // 64-byte block is loaded up front (its first word is Fetch64(s) of :380).
+// PIPE: block k+1 is in flight while block k is mixed (the last iteration
+// re-reads its own block, so the loads stay unconditional).
+template <bool PIPE>
 __device__ __forceinline__ uint64_t city_gt64_reg(const uint8_t* s, uint32_t n, const Blk& t) {
     const u64x2 e0 = t.v0, e1 = t.v1, e2 = t.v2, e3 = t.v3;
     uint64_t x = e1.y;
@@ -150,12 +153,13 @@ __device__ __forceinline__ uint64_t city_gt64_reg(const uint8_t* s, uint32_t n, 
     u64x2 b0 = gld16(s), b1 = gld16(s + 16), b2 = gld16(s + 32), b3 = gld16(s + 48);
     x = x * K1 + b0.x;
     const uint32_t blocks = (n - 1) >> 6;
-    // software-pipelined: block k+1 is in flight while block k is mixed (the
-    // last iteration re-reads its own block, so the loads stay unconditional)
     const uint8_t* last = s + 64 * (blocks - 1);
     for (uint32_t k = 0;;) {
+        u64x2 n0, n1, n2, n3;
         const uint8_t* ns = s + 64 < last ? s + 64 : last;
-        const u64x2 n0 = gld16(ns), n1 = gld16(ns + 16), n2 = gld16(ns + 32), n3 = gld16(ns + 48);
+        if (PIPE) {
+            n0 = gld16(ns); n1 = gld16(ns + 16); n2 = gld16(ns + 32); n3 = gld16(ns + 48);
+        }
         x = ror(x + y + v0 + b0.y, 37) * K1;
         y = ror(y + v1 + b3.x, 42) * K1;
         x ^= w1;
@@ -168,16 +172,21 @@ __device__ __forceinline__ uint64_t city_gt64_reg(const uint8_t* s, uint32_t n, 
         const uint64_t tt = z; z = x; x = tt;
         if (++k == blocks) break;
         s = ns;
-        b0 = n0; b1 = n1; b2 = n2; b3 = n3;
+        if (PIPE) {
+            b0 = n0; b1 = n1; b2 = n2; b3 = n3;
+        } else {
+            b0 = gld16(s); b1 = gld16(s + 16); b2 = gld16(s + 32); b3 = gld16(s + 48);
+        }
     }
     return mix16(mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z, mix16(v1, w1, KMUL) + x, KMUL);
 }
 
+template <bool PIPE = false>
 __device__ __forceinline__ uint64_t hash_blk(uint32_t code, const uint8_t* p, uint32_t n, const Blk& b,
                                              bool& bad) {
     const uint32_t sh = (uint32_t)(uintptr_t)p & 15;
     if (code == CODE_STRING) {
-        if (n > 64) return city_gt64_reg(p, n, b);
+        if (n > 64) return city_gt64_reg<PIPE>(p, n, b);
         if (n > 32) return city_33to64(b.v0, b.v1, b.v2, b.v3, n);
         if (n > 16) return city_17to32(b.v0, b.v1, n);
         return city_le16_reg(n == 16 ? b.v0 : window16(b.v0, b.v1, sh), n);
