@@ -404,16 +404,16 @@ const char* variant_kernel_name(int v) {
     switch (v) {
         case 12: return "void hdx::hash_chunk_kernel<true, false>(hdx::BatchArgs)";
         case 30: return "void hdx::hash_chunk_kernel<true, true>(hdx::BatchArgs)";
-        case 18: return "void hdx::hash_regroup_kernel<4, true, true, true>(hdx::BatchArgs)";
-        case 19: return "void hdx::hash_regroup_kernel<8, true, true, true>(hdx::BatchArgs)";
-        case 20: return "void hdx::hash_regroup_kernel<8, true, false, true>(hdx::BatchArgs)";
-        case 21: return "void hdx::hash_regroup_kernel<4, true, false, true>(hdx::BatchArgs)";
-        case 22: return "void hdx::hash_regroup_kernel<16, true, false, true>(hdx::BatchArgs)";
-        case 23: return "void hdx::hash_regroup_kernel<8, true, false, false>(hdx::BatchArgs)";
-        case 24: return "void hdx::hash_regroup_kernel<4, true, false, false>(hdx::BatchArgs)";
-        case 25: return "void hdx::hash_regroup_kernel<16, true, false, false>(hdx::BatchArgs)";
-        case 26: return "void hdx::hash_regroup_kernel<2, true, true, true>(hdx::BatchArgs)";
-        case 27: return "void hdx::hash_regroup_kernel<2, true, false, true>(hdx::BatchArgs)";
+        case 18: return "void hdx::hash_regroup_kernel<4, true, true, true, false>(hdx::BatchArgs)";
+        case 19: return "void hdx::hash_regroup_kernel<8, true, true, true, false>(hdx::BatchArgs)";
+        case 20: return "void hdx::hash_regroup_kernel<8, true, false, true, false>(hdx::BatchArgs)";
+        case 21: return "void hdx::hash_regroup_kernel<4, true, false, true, false>(hdx::BatchArgs)";
+        case 22: return "void hdx::hash_regroup_kernel<16, true, false, true, false>(hdx::BatchArgs)";
+        case 23: return "void hdx::hash_regroup_kernel<8, true, false, false, false>(hdx::BatchArgs)";
+        case 24: return "void hdx::hash_regroup_kernel<4, true, false, false, false>(hdx::BatchArgs)";
+        case 25: return "void hdx::hash_regroup_kernel<16, true, false, false, false>(hdx::BatchArgs)";
+        case 26: return "void hdx::hash_regroup_kernel<2, true, true, true, false>(hdx::BatchArgs)";
+        case 27: return "void hdx::hash_regroup_kernel<2, true, false, true, false>(hdx::BatchArgs)";
         case 28: return "void hdx::hash_regroup_kernel<2, true, true, true, true>(hdx::BatchArgs)";
         case 29: return "void hdx::hash_regroup_kernel<4, true, true, true, true>(hdx::BatchArgs)";
         default: return "";

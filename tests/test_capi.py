@@ -117,3 +117,22 @@ def test_kernel_for_reports_the_auto_policy():
         assert got == v and name.startswith("void hdx::hash_"), (cfg, got, name)
     assert kernel_for([9217] * 17, 1000)[0] == 12  # small grids keep the one-chunk kernel
     assert kernel_for([12345], 10)[0] == -2
+
+
+def test_kernel_names_match_the_built_symbols():
+    """The names hdxdbg_kernel_for reports are demangled symbols of kernels in
+    the library's gfx950 code object (what rocprofv3 prints), so bench.py's
+    roofline.kernel can be matched against the committed rocprof summaries."""
+    import re
+    import subprocess
+
+    from hyperdex_amd._lib import LIB_PATH
+    from hyperdex_amd.hashing import kernel_for
+    raw = open(LIB_PATH, "rb").read()
+    mangled = sorted(set(m.decode() for m in re.findall(rb"_ZN3hdx\w+kernel\w+BatchArgsE", raw)))
+    demangled = set(subprocess.run(["c++filt"], input="\n".join(mangled), capture_output=True,
+                                   text=True).stdout.split("\n"))
+    for types in ([9217] * 17, [9217, 9218, 9218, 9218, 9218], [9217], [9217, 9473]):
+        for n in (1000, 10_000_000):
+            _, name = kernel_for(types, n)
+            assert name in demangled, (name, sorted(demangled)[:5])
