@@ -133,3 +133,35 @@ def test_gpu_encoded_partial_last_pass(oracle, A, n):
     got = hdx.hash_encoded(types, *_to_dev(torch, torch.device("cuda", 0), enc))
     torch.cuda.synchronize()
     assert np.array_equal(got.cpu().numpy().view(np.uint64), want)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [-1, 33, 34, 35, 36, 37])
+def test_gpu_encoded_every_variant(oracle, variant):
+    """Every stored-object sweep kernel (hdx_encoded.hip: 33 line touch, 34-37
+    the LDS-staged sweep at several group sizes) is bit-exact on every config,
+    on corrupt values, on ragged object counts, and on objects whose values do
+    not fit the stage (wide / keyonly_long fall back to global reads)."""
+    import torch
+
+    import hyperdex_amd as hdx
+    dev = torch.device("cuda", 0)
+    lib = hdx.lib()
+    prev = lib.hdxdbg_set_kernel_variant(variant)
+    assert prev != -2
+    try:
+        cases = [("cfg3b", 1001), ("cfg2", 997), ("mixed", 500), ("cfg1", 33), ("wide", 61),
+                 ("keyonly_long", 40), ("cfg3b", 1), ("cfg3b", 15), ("cfg3b", 16)]
+        for cfg, n in cases:
+            types, blob, base, lens = synth.make_batch_host(cfg, n, seed=n * 7 + 1)
+            enc = synth.encode_values_host(types, blob, base, lens, first_version=5)
+            if cfg == "cfg3b" and n > 100:
+                enc, _ = _corrupt(enc, np.random.default_rng(variant + 10))
+            want, wver, _ = oracle.hash_encoded(types, *enc)
+            versions = torch.zeros(n, dtype=torch.int64, device=dev)
+            got = hdx.hash_encoded(types, *_to_dev(torch, dev, enc), versions=versions)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy().view(np.uint64), want), (cfg, n)
+            assert np.array_equal(versions.cpu().numpy().view(np.uint64), wver), (cfg, n)
+    finally:
+        lib.hdxdbg_set_kernel_variant(prev)
