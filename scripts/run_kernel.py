@@ -23,10 +23,16 @@ def main():
     if a.variant >= 0:
         assert hdx.lib().hdxdbg_set_kernel_variant(a.variant) >= -1
     dev = torch.device("cuda", 0)
-    types, blob, base, lens = synth.make_batch_device(a.config, a.objects, device=dev)
-    coords = torch.empty((a.objects, len(types)), dtype=torch.int64, device=dev)
-    for _ in range(a.launches):
-        hdx.hash_batch(types, blob, base, lens, coords=coords)
+    if a.config == "cfg5":  # stored-object sweep over config-3b objects
+        types, *enc = synth.make_encoded_device("cfg3b", a.objects, device=dev)
+        coords = torch.empty((a.objects, len(types)), dtype=torch.int64, device=dev)
+        for _ in range(a.launches):
+            hdx.hash_encoded(types, *enc, coords=coords)
+    else:
+        types, blob, base, lens = synth.make_batch_device(a.config, a.objects, device=dev)
+        coords = torch.empty((a.objects, len(types)), dtype=torch.int64, device=dev)
+        for _ in range(a.launches):
+            hdx.hash_batch(types, blob, base, lens, coords=coords)
     torch.cuda.synchronize()
 
 
