@@ -161,198 +161,8 @@ hash_encoded_kernel(const EncodedArgs a) {
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-// ===========================================================================
-// Staged sweep: one wave = G objects.  (1) The wave's 2G segments (each
-// object's value and key) are copied into its LDS with streaming, aligned
-// 16-byte loads — every byte read from HBM once, in address order within a
-// segment.  (2) Lane j walks object j's length prefixes in LDS.  (3)
-// ceil(G*A / 64) passes hash the slots straight out of LDS; coordinates leave
-// in one coalesced store per pass.  Segments that do not fit in the stage
-// buffer (W bytes) are decoded and hashed from global memory instead.
-// G is chosen so that G*A fills whole passes (G = 15 for A = 17: 255 of 256
-// lanes busy).
-// ===========================================================================
-constexpr uint32_t kNotStaged = 0xffffffffu;
-
-typedef const __attribute__((address_space(3))) uint32_t* lds_u32_ptr;
-
-// Bytes [off, off+4) of the stage as a little-endian u32 (two aligned reads).
-__device__ __forceinline__ uint32_t lds_u32(lds_cptr base, uint32_t off) {
-    const uint32_t a = off & ~3u;
-    const uint32_t d0 = *(lds_u32_ptr)(base + a), d1 = *(lds_u32_ptr)(base + a + 4);
-    return __builtin_amdgcn_alignbyte(d1, d0, off & 3u);
-}
-
-template <int G>
-__host__ __device__ constexpr size_t staged_meta_bytes(uint32_t A) {
-    // sstart/slds [2G] u32, ssrc [2G] u64, sskew [2G] u32, codes [256], desc [G*A]
-    return (size_t)2 * G * (4 + 4 + 8 + 4) + 256 + (size_t)G * A * sizeof(EncDesc);
-}
-
-template <int G>
-__global__ void __launch_bounds__(64)
-hash_encoded_staged_kernel(const EncodedArgs a, uint32_t W) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
-    const uint32_t A = a.A;
-    const int lane = threadIdx.x;
-    uint8_t* stage = smem_raw;                                        // [W] + 16 slack
-    uint32_t* sstart = reinterpret_cast<uint32_t*>(smem_raw + W + 16);  // [2G] stage offset (prefix)
-    uint32_t* slds = sstart + 2 * G;                                  // [2G] stage offset or kNotStaged
-    uint64_t* ssrc = reinterpret_cast<uint64_t*>(slds + 2 * G);       // [2G] 16-aligned global start
-    uint32_t* sskew = reinterpret_cast<uint32_t*>(ssrc + 2 * G);      // [2G] segment start & 15
-    uint8_t* codes = reinterpret_cast<uint8_t*>(sskew + 2 * G);       // [256]
-    EncDesc* desc = reinterpret_cast<EncDesc*>(codes + 256);          // [G*A]
-    const lds_cptr lstage = (lds_cptr)stage;
-
-    const uint64_t o0 = (uint64_t)blockIdx.x * G;
-    if (o0 >= a.n) return;
-    const uint32_t nobj = (uint32_t)min<uint64_t>(G, a.n - o0);
-    for (uint32_t j = lane; j < A; j += 64) codes[j] = a.codes[j];
-
-    // (1) segment table: lanes [0, G) values, [G, 2G) keys
-    const bool isval = lane < G;
-    const uint32_t jo = isval ? (uint32_t)lane : (uint32_t)lane - G;
-    const bool segv = lane < 2 * G && jo < nobj;
-    const uint64_t io = o0 + (segv ? jo : 0);
-    const uint8_t* sp = isval ? a.vals + a.val_off[io] : a.keys + a.key_off[io];
-    const uint32_t slen = segv ? (isval ? a.val_len[io] : a.key_len[io]) : 0u;
-    const uint32_t skew = addr_lo(sp) & 15;
-    const uint32_t bytes = slen ? (skew + slen + 15) & ~15u : 0u;
-    const uint32_t end = wave_scan_dpp(bytes);
-    const uint32_t start = end - bytes;
-    const bool staged = segv && end <= W;
-    uint32_t total = staged ? end : 0u;
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) total = max(total, (uint32_t)__shfl_xor((int)total, m, 64));
-    if (lane < 2 * G) {
-        sstart[lane] = start;
-        slds[lane] = staged ? start : kNotStaged;
-        ssrc[lane] = (uint64_t)(uintptr_t)(sp - skew);
-        sskew[lane] = skew;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-    // (2) copy the staged byte range [0, total) chunk by chunk, 4 chunks per
-    // lane in flight; each chunk's segment by binary search over the starts
-    const uint32_t nch = total >> 4;
-    for (uint32_t q0 = 0; q0 < nch; q0 += 256) {
-        u64x2 v[4];
-        uint32_t dst[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t q = min(q0 + u * 64 + (uint32_t)lane, nch - 1);
-            const uint32_t byte = q << 4;
-            uint32_t lo = 0, hi = 2 * G;
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (sstart[mid] <= byte) lo = mid;
-                else hi = mid;
-            }
-            const uint8_t* src = reinterpret_cast<const uint8_t*>(ssrc[lo]) + (byte - sstart[lo]);
-            v[u] = gld16(src);
-            dst[u] = byte;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (q0 + u * 64 + (uint32_t)lane < nch) *reinterpret_cast<u64x2*>(stage + dst[u]) = v[u];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-    // (3) decode_value (datalayer_encodings.cc:168-217), lane = object
-    bool any_bad = false;
-    if ((uint32_t)lane < nobj) {
-        const uint32_t vl = slds[lane];
-        const uint32_t vpos = vl + sskew[lane];  // stage offset of value byte 0 (if staged)
-        const uint8_t* v = reinterpret_cast<const uint8_t*>(ssrc[lane]) + sskew[lane];
-        const uint32_t vlen = a.val_len[o0 + lane], klen = a.key_len[o0 + lane];
-        auto be32 = [&](uint32_t pos) -> uint32_t {
-            return vl != kNotStaged ? __builtin_bswap32(lds_u32(lstage, vpos + pos)) : load_be32(v + pos);
-        };
-        bool ok = vlen >= 10;
-        uint64_t version = 0;
-        if (ok) {
-            version = ((uint64_t)be32(0) << 32) | be32(4);
-            ok = (be32(6) & 0xffffu) == A - 1;  // u16 BE count at byte 8
-        }
-        desc[lane * A] = EncDesc{0u, klen};
-        uint32_t pos = 10;
-        for (uint32_t k = 0; k + 1 < A; ++k) {
-            uint32_t len = 0;
-            if (ok) {
-                if (vlen - pos < 4) {
-                    ok = false;
-                } else {
-                    len = be32(pos);
-                    pos += 4;
-                    if (len > vlen - pos) ok = false;
-                }
-            }
-            desc[lane * A + 1 + k] = EncDesc{ok ? pos : kZeroSlot, ok ? len : 0u};
-            if (ok) pos += len;
-        }
-        if (!ok)
-            for (uint32_t j = 0; j < A; ++j) desc[lane * A + j] = EncDesc{kZeroSlot, 0u};
-        if (a.versions) a.versions[o0 + lane] = ok ? version : 0;
-        any_bad = !ok;
-    }
-    any_bad = __any(any_bad);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-    // (4) hash G*A slots (object-major) out of the stage
-    const uint32_t nslots = nobj * A;
-    uint64_t* out = a.coords + o0 * A;
-    bool bad = false;
-    for (uint32_t t = 0; t * 64 < nslots; ++t) {
-        const uint32_t s = t * 64 + (uint32_t)lane;
-        const uint32_t sc = min(s, nslots - 1);
-        const uint32_t obj = sc / A, j = sc - obj * A;
-        const EncDesc d = desc[sc];
-        const bool zero = d.off == kZeroSlot || s >= nslots;
-        const uint32_t code = zero ? (uint32_t)CODE_ZERO : (uint32_t)codes[j];
-        const uint32_t n = zero ? 0u : d.len;
-        const uint32_t k = j == 0 ? G + obj : obj;  // key or value segment
-        const uint32_t l = slds[k];
-        const uint32_t rel = sskew[k] + (zero ? 0u : d.off);
-        uint64_t h;
-        if (zero || l != kNotStaged) {
-            const lds_cptr p = lstage + (zero ? 0u : l + rel);
-            const Blk blk = issue_block_t<lds_cptr>(code, p, n, lstage);
-            h = hash_blk<false, lds_cptr>(code, p, n, blk, bad);
-        } else {
-            const uint8_t* p = reinterpret_cast<const uint8_t*>(ssrc[k]) + rel;
-            const Blk blk = issue_block(code, p, n);
-            h = hash_blk(code, p, n, blk, bad);
-        }
-        if (s < nslots) __builtin_nontemporal_store(h, out + s);
-    }
-    if (a.status && lane == 0 && any_bad) atomicOr(a.status, 1u << 6 /* HDX_E_BADENC */);
-    if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
-}
-
-template <int G>
-static hipError_t launch_staged(const EncodedArgs& a, uint32_t W, hipStream_t stream) {
-    const uint64_t blocks = (a.n + G - 1) / G;
-    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    const size_t lds = W + 16 + staged_meta_bytes<G>(a.A);
-    hipLaunchKernelGGL((hash_encoded_staged_kernel<G>), dim3((uint32_t)blocks), dim3(64), lds, stream, a, W);
-    return hipGetLastError();
-}
-
 hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
-    switch (hash_variant()) {
-        case 34: return launch_staged<15>(a, 24576, stream);
-        case 35: return launch_staged<11>(a, 18432, stream);
-        case 36: return launch_staged<7>(a, 12288, stream);
-        case 37: return launch_staged<15>(a, 20480, stream);
-        default: break;
-    }
     // 4 waves per workgroup while they fit in 64 KiB of LDS (A <= 28), else 1
     const uint32_t waves_per_block = 4 * encoded_lds_per_wave(a.A) <= 65536 ? 4 : 1;
     const uint64_t waves = (a.n + 63) / 64;

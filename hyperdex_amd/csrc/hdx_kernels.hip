@@ -340,10 +340,8 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
 }
 
 static constexpr int kDefaultVariant = -1;  // automatic
-// 33 selects the stored-object sweep with its phase-0 line touch; 34-37 the
-// staged sweep with (objects per wave, stage bytes) = (15, 24 K), (11, 18 K),
-// (7, 12 K), (15, 20 K) (hdx_encoded.hip).
-static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 30) || (v >= 33 && v <= 37); }
+// 33 selects the stored-object sweep with its phase-0 line touch (hdx_encoded.hip).
+static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 30) || v == 33; }
 
 static int g_variant = [] {
     const char* e = getenv("HDX_KERNEL_VARIANT");

@@ -50,42 +50,27 @@ typedef u64x2 __attribute__((aligned(1))) u64x2_u;
 typedef const __attribute__((address_space(1))) u64x2_u* gvec_ptr;
 __device__ __forceinline__ u64x2 gld16(const uint8_t* p) { return *(gvec_ptr)p; }
 
-// The same 16-byte read from LDS (staged bytes, hdx_encoded.hip).  An access
-// off 16-byte alignment is replayed by the LDS pipe (slower, still exact);
-// the short-value path only issues aligned ones.
-typedef const __attribute__((address_space(3))) uint8_t* lds_cptr;
-typedef const __attribute__((address_space(3))) u64x2_u* lvec_ptr;
-__device__ __forceinline__ u64x2 ld16(const uint8_t* p) { return gld16(p); }
-__device__ __forceinline__ u64x2 ld16(lds_cptr p) { return *(lvec_ptr)p; }
-__device__ __forceinline__ uint32_t addr_lo(const uint8_t* p) { return (uint32_t)(uintptr_t)p; }
-__device__ __forceinline__ uint32_t addr_lo(lds_cptr p) { return (uint32_t)(uintptr_t)p; }
-
 struct Blk {
     u64x2 v0, v1, v2, v3;
 };
 
-// PT: const uint8_t* (global) or lds_cptr (LDS); D: a readable 64-byte dummy.
-template <typename PT>
-__device__ __forceinline__ Blk issue_block_t(uint32_t code, PT p, uint32_t n, PT D) {
+__device__ __forceinline__ Blk issue_block(uint32_t code, const uint8_t* p, uint32_t n) {
+    const uint8_t* D = g_zero_pad;
     const bool str = code == CODE_STRING;
     const bool shortv = (str && n > 0 && n < 16) || (code >= CODE_INT64 && n == 8);
-    const PT lo = p - (addr_lo(p) & 15);  // pointer arithmetic keeps provenance
-    const PT hi = (p + n - 1) - (addr_lo(p + n - 1) & 15);
+    const uint8_t* lo = p - ((uintptr_t)p & 15);  // pointer arithmetic keeps provenance
+    const uint8_t* hi = (p + n - 1) - ((uintptr_t)(p + n - 1) & 15);
     const bool g64 = str && n > 64, g32 = str && n > 32 && n <= 64, g16 = str && n >= 16 && n <= 32;
-    const PT a0 = g64 ? p + n - 64 : (g32 || g16) ? p : shortv ? lo : D;
-    const PT a1 = g64 ? p + n - 48 : g32 ? p + 16 : g16 ? p + n - 16 : shortv ? hi : D;
-    const PT a2 = g64 || g32 ? p + n - 32 : D;
-    const PT a3 = g64 || g32 ? p + n - 16 : D;
+    const uint8_t* a0 = g64 ? p + n - 64 : (g32 || g16) ? p : shortv ? lo : D;
+    const uint8_t* a1 = g64 ? p + n - 48 : g32 ? p + 16 : g16 ? p + n - 16 : shortv ? hi : D;
+    const uint8_t* a2 = g64 || g32 ? p + n - 32 : D;
+    const uint8_t* a3 = g64 || g32 ? p + n - 16 : D;
     Blk b;
-    b.v0 = ld16(a0);
-    b.v1 = ld16(a1);
-    b.v2 = ld16(a2);
-    b.v3 = ld16(a3);
+    b.v0 = gld16(a0);
+    b.v1 = gld16(a1);
+    b.v2 = gld16(a2);
+    b.v3 = gld16(a3);
     return b;
-}
-
-__device__ __forceinline__ Blk issue_block(uint32_t code, const uint8_t* p, uint32_t n) {
-    return issue_block_t<const uint8_t*>(code, p, n, g_zero_pad);
 }
 
 __device__ __forceinline__ uint32_t dw(const u64x2& v, int k) {
@@ -156,8 +141,8 @@ __device__ __forceinline__ uint64_t city_le16_reg(const u64x2& w, uint32_t n) {
 // 64-byte block is loaded up front (its first word is Fetch64(s) of :380).
 // PIPE: block k+1 is in flight while block k is mixed (the last iteration
 // re-reads its own block, so the loads stay unconditional).
-template <bool PIPE, typename PT = const uint8_t*>
-__device__ __forceinline__ uint64_t city_gt64_reg(PT s, uint32_t n, const Blk& t) {
+template <bool PIPE>
+__device__ __forceinline__ uint64_t city_gt64_reg(const uint8_t* s, uint32_t n, const Blk& t) {
     const u64x2 e0 = t.v0, e1 = t.v1, e2 = t.v2, e3 = t.v3;
     uint64_t x = e1.y;
     uint64_t y = e3.x + e0.y;
@@ -165,15 +150,15 @@ __device__ __forceinline__ uint64_t city_gt64_reg(PT s, uint32_t n, const Blk& t
     uint64_t v0, v1, w0, w1;
     weak32(e0.x, e0.y, e1.x, e1.y, n, z, v0, v1);
     weak32(e2.x, e2.y, e3.x, e3.y, y + K1, x, w0, w1);
-    u64x2 b0 = ld16(s), b1 = ld16(s + 16), b2 = ld16(s + 32), b3 = ld16(s + 48);
+    u64x2 b0 = gld16(s), b1 = gld16(s + 16), b2 = gld16(s + 32), b3 = gld16(s + 48);
     x = x * K1 + b0.x;
     const uint32_t blocks = (n - 1) >> 6;
-    const PT last = s + 64 * (blocks - 1);
+    const uint8_t* last = s + 64 * (blocks - 1);
     for (uint32_t k = 0;;) {
         u64x2 n0, n1, n2, n3;
-        const PT ns = s + 64 < last ? s + 64 : last;
+        const uint8_t* ns = s + 64 < last ? s + 64 : last;
         if (PIPE) {
-            n0 = ld16(ns); n1 = ld16(ns + 16); n2 = ld16(ns + 32); n3 = ld16(ns + 48);
+            n0 = gld16(ns); n1 = gld16(ns + 16); n2 = gld16(ns + 32); n3 = gld16(ns + 48);
         }
         x = ror(x + y + v0 + b0.y, 37) * K1;
         y = ror(y + v1 + b3.x, 42) * K1;
@@ -190,17 +175,18 @@ __device__ __forceinline__ uint64_t city_gt64_reg(PT s, uint32_t n, const Blk& t
         if (PIPE) {
             b0 = n0; b1 = n1; b2 = n2; b3 = n3;
         } else {
-            b0 = ld16(s); b1 = ld16(s + 16); b2 = ld16(s + 32); b3 = ld16(s + 48);
+            b0 = gld16(s); b1 = gld16(s + 16); b2 = gld16(s + 32); b3 = gld16(s + 48);
         }
     }
     return mix16(mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z, mix16(v1, w1, KMUL) + x, KMUL);
 }
 
-template <bool PIPE = false, typename PT = const uint8_t*>
-__device__ __forceinline__ uint64_t hash_blk(uint32_t code, PT p, uint32_t n, const Blk& b, bool& bad) {
-    const uint32_t sh = addr_lo(p) & 15;
+template <bool PIPE = false>
+__device__ __forceinline__ uint64_t hash_blk(uint32_t code, const uint8_t* p, uint32_t n, const Blk& b,
+                                             bool& bad) {
+    const uint32_t sh = (uint32_t)(uintptr_t)p & 15;
     if (code == CODE_STRING) {
-        if (n > 64) return city_gt64_reg<PIPE, PT>(p, n, b);
+        if (n > 64) return city_gt64_reg<PIPE>(p, n, b);
         if (n > 32) return city_33to64(b.v0, b.v1, b.v2, b.v3, n);
         if (n > 16) return city_17to32(b.v0, b.v1, n);
         return city_le16_reg(n == 16 ? b.v0 : window16(b.v0, b.v1, sh), n);

@@ -136,12 +136,11 @@ def test_gpu_encoded_partial_last_pass(oracle, A, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [-1, 33, 34, 35, 36, 37])
+@pytest.mark.parametrize("variant", [-1, 33])
 def test_gpu_encoded_every_variant(oracle, variant):
-    """Every stored-object sweep kernel (hdx_encoded.hip: 33 line touch, 34-37
-    the LDS-staged sweep at several group sizes) is bit-exact on every config,
-    on corrupt values, on ragged object counts, and on objects whose values do
-    not fit the stage (wide / keyonly_long fall back to global reads)."""
+    """Every stored-object sweep kernel (hdx_encoded.hip; 33 adds the line
+    touch) is bit-exact on every config, on corrupt values, on ragged object
+    counts and on large values (wide, keyonly_long)."""
     import torch
 
     import hyperdex_amd as hdx
