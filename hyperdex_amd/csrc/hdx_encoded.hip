@@ -54,7 +54,7 @@ __host__ __device__ constexpr size_t encoded_lds_per_wave(uint32_t A) {
     return 64 * 16 + 256 + (size_t)64 * A * sizeof(EncDesc);
 }
 
-template <bool TOUCH>
+template <bool TOUCH, bool A4 = false>
 __global__ void __launch_bounds__(256)
 hash_encoded_kernel(const EncodedArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
@@ -125,7 +125,7 @@ hash_encoded_kernel(const EncodedArgs a) {
     struct Pass {
         const uint8_t* p;
         uint32_t n, code;
-        Blk blk;
+        Raw blk;
     };
     auto load_pass = [&](uint32_t t, Pass& P) {
         const uint32_t s = min(t * 64 + (uint32_t)lane, nslots - 1);
@@ -136,7 +136,7 @@ hash_encoded_kernel(const EncodedArgs a) {
         P.code = zero ? (uint32_t)CODE_ZERO : (uint32_t)codes[j];
         P.n = zero ? 0u : d.len;
         P.p = zero ? g_zero_pad : (j == 0 ? a.keys : a.vals) + base + d.off;
-        P.blk = issue_block(P.code, P.p, P.n);
+        P.blk = issue_any<A4>(P.code, P.p, P.n);
     };
     bool bad = false;
     Pass P0, P1;
@@ -144,14 +144,14 @@ hash_encoded_kernel(const EncodedArgs a) {
     for (uint32_t t = 0;; t += 2) {
         if (t + 1 < A) load_pass(t + 1, P1);
         {
-            const uint64_t h = hash_blk(P0.code, P0.p, P0.n, P0.blk, bad);
+            const uint64_t h = hash_blk<false, false, A4>(P0.code, P0.p, P0.n, consume_any<A4>(P0.blk), bad);
             const uint32_t s = t * 64 + lane;
             if (s < nslots) __builtin_nontemporal_store(h, out + s);
         }
         if (t + 1 >= A) break;
         if (t + 2 < A) load_pass(t + 2, P0);
         {
-            const uint64_t h = hash_blk(P1.code, P1.p, P1.n, P1.blk, bad);
+            const uint64_t h = hash_blk<false, false, A4>(P1.code, P1.p, P1.n, consume_any<A4>(P1.blk), bad);
             const uint32_t s = (t + 1) * 64 + lane;
             if (s < nslots) __builtin_nontemporal_store(h, out + s);
         }
@@ -169,12 +169,17 @@ hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream) {
     const uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
     const size_t lds = (size_t)waves_per_block * encoded_lds_per_wave(a.A);
-    // variant 33 adds the phase-0 line touch (measured 11% slower, r1u)
-    if (hash_variant() == 33)
+    // default: dword-aligned loads (5.49 vs 6.14 ms per 10 M config-3b objects,
+    // profiles/r1/ab_a4_cfg5.jsonl); variant 43 = byte-addressed loads, variant
+    // 33 adds the phase-0 line touch to those (measured 11 % slower, r1u)
+    if (hash_variant() == 43)
+        hipLaunchKernelGGL((hash_encoded_kernel<false, false>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
+                           lds, stream, a);
+    else if (hash_variant() == 33)
         hipLaunchKernelGGL((hash_encoded_kernel<true>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
                            lds, stream, a);
     else
-        hipLaunchKernelGGL((hash_encoded_kernel<false>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
+        hipLaunchKernelGGL((hash_encoded_kernel<false, true>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
                            lds, stream, a);
     return hipGetLastError();
 }

@@ -55,7 +55,11 @@ __device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
     return __builtin_amdgcn_readlane(wave_scan_dpp(v), 63);
 }
 
-template <bool NT_STORE, bool PIPE = false>
+// SHAPE (debug variants only): 0 = the real kernel; 1 = its loads without the
+// hash arithmetic (variant 40); 2 = its arithmetic without the byte loads
+// (variant 41).  Shapes 1 and 2 write wrong coordinates: they bound the
+// kernel's time by its memory and its VALU work.
+template <bool NT_STORE, bool PIPE = false, int SHAPE = 0, bool A4 = false>
 __global__ void __launch_bounds__(256)
 hash_chunk_kernel(const BatchArgs args) {
     const int lane = threadIdx.x & 63;
@@ -98,10 +102,12 @@ hash_chunk_kernel(const BatchArgs args) {
     const uint32_t off = head >= 0 ? Sx - head_sx : carry + Sx;
     const uint8_t* p = args.blob + base + off;
 
-    const Blk blk = issue_block(valid ? code : (uint32_t)CODE_ZERO, p, L);
+    const Blk blk = SHAPE == 2 ? fake_block(p, L)
+                               : consume_any<A4>(issue_any<A4>(valid ? code : (uint32_t)CODE_ZERO, p, L));
     if (valid) {
         bool bad = false;
-        const uint64_t h = hash_blk<PIPE>(code, p, L, blk, bad);
+        const uint64_t h = SHAPE == 1 ? touch_blk(code, p, L, blk)
+                                      : hash_blk<PIPE, SHAPE == 2, A4>(code, p, L, blk, bad);
         if (NT_STORE) __builtin_nontemporal_store(h, args.coords + q0 + lane);
         else args.coords[q0 + lane] = h;
         if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
@@ -148,7 +154,8 @@ struct RegroupStageLds {
     Blk blk[4][C * 64];
 };
 
-template <int C, bool NT_STORE, bool SORT = true, bool DIRECT = true, bool STAGE = false>
+template <int C, bool NT_STORE, bool SORT = true, bool DIRECT = true, bool STAGE = false, bool A4 = false,
+          bool PIPE = false>
 __global__ void __launch_bounds__(256)
 hash_regroup_kernel(const BatchArgs args) {
     typedef typename std::conditional<STAGE, RegroupStageLds<C>, RegroupLds<C>>::type Lds;
@@ -250,13 +257,13 @@ hash_regroup_kernel(const BatchArgs args) {
     // which exactly one lane has already read (each slot is in one pass).
     struct Pass {
         SlotDesc d;
-        Blk blk;
+        Raw blk;
     };
     auto load_pass = [&](int t, Pass& P) {
         const uint32_t s = uniform ? (uint32_t)(t * 64 + lane) : perm[t * 64 + lane];
         P.d = desc[s];
-        if constexpr (STAGE) P.blk = lds_blk(s);
-        else P.blk = issue_block(P.d.code_slot & 0xffu, P.d.p, P.d.n);
+        if constexpr (STAGE) P.blk.b = lds_blk(s);
+        else P.blk = issue_any<A4>(P.d.code_slot & 0xffu, P.d.p, P.d.n);
     };
     bool bad = false;
     Pass P0, P1;
@@ -266,7 +273,8 @@ hash_regroup_kernel(const BatchArgs args) {
         Pass& cur = (t & 1) ? P1 : P0;
         Pass& nxt = (t & 1) ? P0 : P1;
         if (t + 1 < C) load_pass(t + 1, nxt);
-        const uint64_t h = hash_blk(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n, cur.blk, bad);
+        const uint64_t h = hash_blk<PIPE, false, A4 && !STAGE>(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n,
+                                                                STAGE ? cur.blk.b : consume_any<A4>(cur.blk), bad);
         if (DIRECT && uniform) {  // pass t is chunk t in slot order: store straight to HBM
             const uint64_t q = qw + t * 64 + lane;
             if (q < nslots) {
@@ -298,24 +306,25 @@ hash_regroup_kernel(const BatchArgs args) {
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <int C, bool NT, bool SORT = true, bool DIRECT = true, bool STAGE = false>
+template <int C, bool NT, bool SORT = true, bool DIRECT = true, bool STAGE = false, bool A4 = false,
+          bool PIPE = false>
 static hipError_t launch_regroup(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT, DIRECT, STAGE>), dim3((uint32_t)blocks), dim3(256), 0, stream,
+    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT, DIRECT, STAGE, A4, PIPE>), dim3((uint32_t)blocks), dim3(256), 0, stream,
                        args);
     return hipGetLastError();
 }
 
-template <bool NT, bool PIPE = false>
+template <bool NT, bool PIPE = false, int SHAPE = 0, bool A4 = false>
 static hipError_t launch_chunk(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + 63) / 64;
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_chunk_kernel<NT, PIPE>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_chunk_kernel<NT, PIPE, SHAPE, A4>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
     return hipGetLastError();
 }
 
@@ -335,29 +344,45 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 28: return launch_regroup<2, true, true, true, true>(args, stream);
         case 29: return launch_regroup<4, true, true, true, true>(args, stream);
         case 30: return launch_chunk<true, true>(args, stream);
+        case 31: return launch_chunk<true, false, 0, true>(args, stream);
+        case 32: return launch_regroup<4, true, false, true, false, true>(args, stream);
+        case 34: return launch_regroup<8, true, true, true, false, true>(args, stream);
+        case 35: return launch_regroup<2, true, true, true, false, true>(args, stream);
+        case 36: return launch_regroup<4, true, true, true, false, true>(args, stream);
+        case 37: return launch_regroup<2, true, true, true, false, true, true>(args, stream);
+        case 38: return launch_regroup<3, true, true, true, false, true>(args, stream);
+        case 39: return launch_regroup<2, true, true, false, false, true>(args, stream);
+        case 40: return launch_chunk<true, false, 1>(args, stream);
+        case 41: return launch_chunk<true, false, 2>(args, stream);
         default: return hipErrorInvalidValue;
     }
 }
 
 static constexpr int kDefaultVariant = -1;  // automatic
-// 33 selects the stored-object sweep with its phase-0 line touch (hdx_encoded.hip).
-static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 30) || v == 33; }
+// 33 / 43 select the stored-object sweep's line-touch and byte-addressed forms
+// (hdx_encoded.hip).
+static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 43); }
 
 static int g_variant = [] {
     const char* e = getenv("HDX_KERNEL_VARIANT");
     return e && *e ? atoi(e) : kDefaultVariant;
 }();
 
-// Automatic choice (interleaved A/B on one MI355X, profiles/r1/ab_variants_*.jsonl):
+// Automatic choice (interleaved A/B on one MI355X, profiles/r1/ab_variants_*.jsonl
+// and profiles/r1/ab_a4_*.jsonl):
 //  * schemas with timestamps or non-hashable attributes: regroup kernel with the
-//    class sort, 8 chunks per wave (19) — their diverse paths dominate (mixed: -26 %);
+//    class sort, 8 chunks per wave (19) — their diverse paths dominate (mixed:
+//    2.64 vs 3.58 ms for the chunk kernel, 3.56 for 35);
 //  * mostly numerics: regroup unsorted, 4 chunks per wave, direct stores (21)
 //    (config 2: 0.31 vs 0.42 ms);
 //  * one code everywhere (all strings): regroup unsorted with 16 chunks per wave
 //    and burst stores (25) when the grid keeps >= 64 K waves, 8 chunks (20) from
 //    32 M slots (config 3a: 2.24 vs 2.38 ms), else the one-chunk kernel (12)
 //    (config 1);
-//  * otherwise (strings + int64/float, config 3b): one-chunk kernel (12).
+//  * otherwise (strings + int64/float, config 3b): regroup with the class sort
+//    over 2 chunks and dword-aligned loads (35): 3.51 vs 4.22 ms for the chunk
+//    kernel — byte-misaligned 16-byte loads had made the texture-address unit
+//    the bound.
 static int auto_variant(const BatchArgs& args) {
     uint32_t numeric = 0;
     bool complex_types = false;
@@ -372,8 +397,9 @@ static int auto_variant(const BatchArgs& args) {
     if (args.uniform_code != 0xffu) {
         if (slots >= (64ull << 20)) return 25;
         if (slots >= (32ull << 20)) return 20;
+        return 12;
     }
-    return 12;
+    return 35;
 }
 
 int hash_variant() { return __atomic_load_n(&g_variant, __ATOMIC_RELAXED); }
@@ -402,20 +428,28 @@ int chosen_variant(const BatchArgs& args) {
 // The kernel symbol a variant launches, as rocprofv3 prints it.
 const char* variant_kernel_name(int v) {
     switch (v) {
-        case 12: return "void hdx::hash_chunk_kernel<true, false>(hdx::BatchArgs)";
-        case 30: return "void hdx::hash_chunk_kernel<true, true>(hdx::BatchArgs)";
-        case 18: return "void hdx::hash_regroup_kernel<4, true, true, true, false>(hdx::BatchArgs)";
-        case 19: return "void hdx::hash_regroup_kernel<8, true, true, true, false>(hdx::BatchArgs)";
-        case 20: return "void hdx::hash_regroup_kernel<8, true, false, true, false>(hdx::BatchArgs)";
-        case 21: return "void hdx::hash_regroup_kernel<4, true, false, true, false>(hdx::BatchArgs)";
-        case 22: return "void hdx::hash_regroup_kernel<16, true, false, true, false>(hdx::BatchArgs)";
-        case 23: return "void hdx::hash_regroup_kernel<8, true, false, false, false>(hdx::BatchArgs)";
-        case 24: return "void hdx::hash_regroup_kernel<4, true, false, false, false>(hdx::BatchArgs)";
-        case 25: return "void hdx::hash_regroup_kernel<16, true, false, false, false>(hdx::BatchArgs)";
-        case 26: return "void hdx::hash_regroup_kernel<2, true, true, true, false>(hdx::BatchArgs)";
-        case 27: return "void hdx::hash_regroup_kernel<2, true, false, true, false>(hdx::BatchArgs)";
-        case 28: return "void hdx::hash_regroup_kernel<2, true, true, true, true>(hdx::BatchArgs)";
-        case 29: return "void hdx::hash_regroup_kernel<4, true, true, true, true>(hdx::BatchArgs)";
+        case 12: return "void hdx::hash_chunk_kernel<true, false, 0, false>(hdx::BatchArgs)";
+        case 30: return "void hdx::hash_chunk_kernel<true, true, 0, false>(hdx::BatchArgs)";
+        case 31: return "void hdx::hash_chunk_kernel<true, false, 0, true>(hdx::BatchArgs)";
+        case 32: return "void hdx::hash_regroup_kernel<4, true, false, true, false, true, false>(hdx::BatchArgs)";
+        case 34: return "void hdx::hash_regroup_kernel<8, true, true, true, false, true, false>(hdx::BatchArgs)";
+        case 35: return "void hdx::hash_regroup_kernel<2, true, true, true, false, true, false>(hdx::BatchArgs)";
+        case 36: return "void hdx::hash_regroup_kernel<4, true, true, true, false, true, false>(hdx::BatchArgs)";
+        case 37: return "void hdx::hash_regroup_kernel<2, true, true, true, false, true, true>(hdx::BatchArgs)";
+        case 38: return "void hdx::hash_regroup_kernel<3, true, true, true, false, true, false>(hdx::BatchArgs)";
+        case 39: return "void hdx::hash_regroup_kernel<2, true, true, false, false, true, false>(hdx::BatchArgs)";
+        case 18: return "void hdx::hash_regroup_kernel<4, true, true, true, false, false, false>(hdx::BatchArgs)";
+        case 19: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, false>(hdx::BatchArgs)";
+        case 20: return "void hdx::hash_regroup_kernel<8, true, false, true, false, false, false>(hdx::BatchArgs)";
+        case 21: return "void hdx::hash_regroup_kernel<4, true, false, true, false, false, false>(hdx::BatchArgs)";
+        case 22: return "void hdx::hash_regroup_kernel<16, true, false, true, false, false, false>(hdx::BatchArgs)";
+        case 23: return "void hdx::hash_regroup_kernel<8, true, false, false, false, false, false>(hdx::BatchArgs)";
+        case 24: return "void hdx::hash_regroup_kernel<4, true, false, false, false, false, false>(hdx::BatchArgs)";
+        case 25: return "void hdx::hash_regroup_kernel<16, true, false, false, false, false, false>(hdx::BatchArgs)";
+        case 26: return "void hdx::hash_regroup_kernel<2, true, true, true, false, false, false>(hdx::BatchArgs)";
+        case 27: return "void hdx::hash_regroup_kernel<2, true, false, true, false, false, false>(hdx::BatchArgs)";
+        case 28: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, false>(hdx::BatchArgs)";
+        case 29: return "void hdx::hash_regroup_kernel<4, true, true, true, true, false, false>(hdx::BatchArgs)";
         default: return "";
     }
 }

@@ -73,6 +73,91 @@ __device__ __forceinline__ Blk issue_block(uint32_t code, const uint8_t* p, uint
     return b;
 }
 
+// ---------------------------------------------------------------------------
+// Dword-aligned form (A4).  A 16-byte load at a byte-misaligned address costs
+// the texture-address unit about twice an aligned one (tools/gldbench.hip:
+// 4.37 vs 5.45 TB/s, TA 97 % busy), and packed variable-length values are
+// byte-misaligned three times in four.  A4 loads every piece at the dword
+// floor of its address, plus the dword after it, and funnel-shifts the bytes
+// into place with v_alignbyte (4 VALU per 16 bytes).  Pieces, as issue_block's
+// but with the 16..32-byte and short / numeric regimes in slots 1 and 3:
+//   P0 P1 | P2 P3, P1's next dword E1, P3's next dword E3,
+//   shift ra for P0/P1 (contiguous: P0's next dword is P1's first), rb for P2/P3.
+// Every dword loaded holds at least one byte of the value (or is in the zero
+// pad), so no load leaves the value's pages.
+// ---------------------------------------------------------------------------
+struct Raw {
+    Blk b;
+    uint32_t e1, e3, ra, rb;
+};
+
+__device__ __forceinline__ uint32_t gld4(const uint8_t* p) {
+    return *(const __attribute__((address_space(1))) uint32_t*)p;
+}
+__device__ __forceinline__ const uint8_t* dw_floor(const uint8_t* p) { return p - ((uintptr_t)p & 3); }
+
+__device__ __forceinline__ Raw issue_block_a4(uint32_t code, const uint8_t* p, uint32_t n) {
+    const uint8_t* D = g_zero_pad;
+    const bool str = code == CODE_STRING;
+    const bool shortv = (str && n > 0 && n < 16) || (code >= CODE_INT64 && n == 8);
+    const uint8_t* lo = p - ((uintptr_t)p & 15);
+    const uint8_t* hi = (p + n - 1) - ((uintptr_t)(p + n - 1) & 15);
+    const bool g64 = str && n > 64, g32 = str && n > 32 && n <= 64, g16 = str && n >= 16 && n <= 32;
+    const uint8_t* x0 = g64 ? p + n - 64 : g32 ? p : D;
+    const uint8_t* x1 = g64 ? p + n - 48 : g32 ? p + 16 : g16 ? p : shortv ? lo : D;
+    const uint8_t* x2 = g64 || g32 ? p + n - 32 : D;
+    const uint8_t* x3 = g64 ? p + n - 16 : g32 ? p + n - 16 : g16 ? p + n - 16 : shortv ? hi : D;
+    Raw r;
+    r.ra = (uint32_t)(uintptr_t)x1 & 3;
+    r.rb = (uint32_t)(uintptr_t)x3 & 3;
+    const uint8_t* a1 = dw_floor(x1);
+    const uint8_t* a3 = dw_floor(x3);
+    r.b.v0 = gld16(dw_floor(x0));
+    r.b.v1 = gld16(a1);
+    r.b.v2 = gld16(dw_floor(x2));
+    r.b.v3 = gld16(a3);
+    r.e1 = gld4(r.ra ? a1 + 16 : a1);  // only used when the piece is misaligned
+    r.e3 = gld4(r.rb ? a3 + 16 : a3);
+    return r;
+}
+
+// Bytes [r, r+16) of the 20 bytes v || next (r in 0..3).
+__device__ __forceinline__ u64x2 funnel16(const u64x2& v, uint32_t next, uint32_t r) {
+    const uint32_t d0 = (uint32_t)v.x, d1 = (uint32_t)(v.x >> 32), d2 = (uint32_t)v.y, d3 = (uint32_t)(v.y >> 32);
+    u64x2 w;
+    w.x = ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, r) << 32) | __builtin_amdgcn_alignbyte(d1, d0, r);
+    w.y = ((uint64_t)__builtin_amdgcn_alignbyte(next, d3, r) << 32) | __builtin_amdgcn_alignbyte(d3, d2, r);
+    return w;
+}
+
+__device__ __forceinline__ Blk funnel_raw(const Raw& r) {
+    Blk b;
+    b.v0 = funnel16(r.b.v0, (uint32_t)r.b.v1.x, r.ra);
+    b.v1 = funnel16(r.b.v1, r.e1, r.ra);
+    b.v2 = funnel16(r.b.v2, (uint32_t)r.b.v3.x, r.rb);
+    b.v3 = funnel16(r.b.v3, r.e3, r.rb);
+    return b;
+}
+
+// issue / consume in either form: A4 = dword-aligned pieces, funnelled when
+// consumed (so the next pass's loads stay in flight); else issue_block's.
+template <bool A4>
+__device__ __forceinline__ Raw issue_any(uint32_t code, const uint8_t* p, uint32_t n) {
+    if constexpr (A4) {
+        return issue_block_a4(code, p, n);
+    } else {
+        Raw r;
+        r.b = issue_block(code, p, n);
+        r.e1 = r.e3 = r.ra = r.rb = 0;
+        return r;
+    }
+}
+template <bool A4>
+__device__ __forceinline__ Blk consume_any(const Raw& r) {
+    if constexpr (A4) return funnel_raw(r);
+    else return r.b;
+}
+
 __device__ __forceinline__ uint32_t dw(const u64x2& v, int k) {
     return (uint32_t)((k & 2 ? v.y : v.x) >> (32 * (k & 1)));
 }
@@ -141,7 +226,54 @@ __device__ __forceinline__ uint64_t city_le16_reg(const u64x2& w, uint32_t n) {
 // 64-byte block is loaded up front (its first word is Fetch64(s) of :380).
 // PIPE: block k+1 is in flight while block k is mixed (the last iteration
 // re-reads its own block, so the loads stay unconditional).
-template <bool PIPE>
+// FAKE (debug variant 41 only): the loop's loads are replaced by values made
+// from the address, so a kernel built with it runs the arithmetic alone.
+template <bool FAKE>
+__device__ __forceinline__ u64x2 ld16(const uint8_t* s) {
+    if constexpr (FAKE) {
+        u64x2 v;
+        v.x = (uint64_t)(uintptr_t)s;
+        v.y = v.x * 3;
+        return v;
+    } else {
+        return gld16(s);
+    }
+}
+
+// One 64-byte loop block at s: four 16-byte loads, or (A4) four at the dword
+// floor of s plus the dword after them, funnel-shifted by s & 3.  Every loop
+// block ends at least one byte before the value does, so the extra dword
+// holds value bytes.
+struct Blk64 {
+    Blk b;
+    uint32_t e;
+};
+template <bool A4, bool FAKE>
+__device__ __forceinline__ Blk64 ld64(const uint8_t* s) {
+    Blk64 r;
+    const uint8_t* a = A4 ? dw_floor(s) : s;
+    r.b.v0 = ld16<FAKE>(a);
+    r.b.v1 = ld16<FAKE>(a + 16);
+    r.b.v2 = ld16<FAKE>(a + 32);
+    r.b.v3 = ld16<FAKE>(a + 48);
+    r.e = A4 && !FAKE ? gld4(a + 64) : 0u;
+    return r;
+}
+template <bool A4>
+__device__ __forceinline__ Blk use64(const Blk64& r, uint32_t sh) {
+    if constexpr (!A4) {
+        return r.b;
+    } else {
+        Blk b;
+        b.v0 = funnel16(r.b.v0, (uint32_t)r.b.v1.x, sh);
+        b.v1 = funnel16(r.b.v1, (uint32_t)r.b.v2.x, sh);
+        b.v2 = funnel16(r.b.v2, (uint32_t)r.b.v3.x, sh);
+        b.v3 = funnel16(r.b.v3, r.e, sh);
+        return b;
+    }
+}
+
+template <bool PIPE, bool FAKE = false, bool A4 = false>
 __device__ __forceinline__ uint64_t city_gt64_reg(const uint8_t* s, uint32_t n, const Blk& t) {
     const u64x2 e0 = t.v0, e1 = t.v1, e2 = t.v2, e3 = t.v3;
     uint64_t x = e1.y;
@@ -150,16 +282,16 @@ __device__ __forceinline__ uint64_t city_gt64_reg(const uint8_t* s, uint32_t n, 
     uint64_t v0, v1, w0, w1;
     weak32(e0.x, e0.y, e1.x, e1.y, n, z, v0, v1);
     weak32(e2.x, e2.y, e3.x, e3.y, y + K1, x, w0, w1);
-    u64x2 b0 = gld16(s), b1 = gld16(s + 16), b2 = gld16(s + 32), b3 = gld16(s + 48);
+    const uint32_t sh = (uint32_t)(uintptr_t)s & 3;
+    Blk cur = use64<A4>(ld64<A4, FAKE>(s), sh);
+    u64x2 b0 = cur.v0, b1 = cur.v1, b2 = cur.v2, b3 = cur.v3;
     x = x * K1 + b0.x;
     const uint32_t blocks = (n - 1) >> 6;
     const uint8_t* last = s + 64 * (blocks - 1);
     for (uint32_t k = 0;;) {
-        u64x2 n0, n1, n2, n3;
+        Blk64 nx;
         const uint8_t* ns = s + 64 < last ? s + 64 : last;
-        if (PIPE) {
-            n0 = gld16(ns); n1 = gld16(ns + 16); n2 = gld16(ns + 32); n3 = gld16(ns + 48);
-        }
+        if (PIPE) nx = ld64<A4, FAKE>(ns);
         x = ror(x + y + v0 + b0.y, 37) * K1;
         y = ror(y + v1 + b3.x, 42) * K1;
         x ^= w1;
@@ -172,34 +304,61 @@ __device__ __forceinline__ uint64_t city_gt64_reg(const uint8_t* s, uint32_t n, 
         const uint64_t tt = z; z = x; x = tt;
         if (++k == blocks) break;
         s = ns;
-        if (PIPE) {
-            b0 = n0; b1 = n1; b2 = n2; b3 = n3;
-        } else {
-            b0 = gld16(s); b1 = gld16(s + 16); b2 = gld16(s + 32); b3 = gld16(s + 48);
-        }
+        if (!PIPE) nx = ld64<A4, FAKE>(s);
+        cur = use64<A4>(nx, sh);
+        b0 = cur.v0; b1 = cur.v1; b2 = cur.v2; b3 = cur.v3;
     }
     return mix16(mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z, mix16(v1, w1, KMUL) + x, KMUL);
 }
 
-template <bool PIPE = false>
+// A4: the block comes from issue_block_a4 (16..32-byte, short and numeric
+// pieces in slots 1 and 3).
+template <bool PIPE = false, bool FAKE = false, bool A4 = false>
 __device__ __forceinline__ uint64_t hash_blk(uint32_t code, const uint8_t* p, uint32_t n, const Blk& b,
                                              bool& bad) {
     const uint32_t sh = (uint32_t)(uintptr_t)p & 15;
+    const u64x2& f = A4 ? b.v1 : b.v0;  // first piece of the 16..32-byte / short regimes
+    const u64x2& g = A4 ? b.v3 : b.v1;  // second piece
     if (code == CODE_STRING) {
-        if (n > 64) return city_gt64_reg<PIPE>(p, n, b);
+        if (n > 64) return city_gt64_reg<PIPE, FAKE, A4>(p, n, b);
         if (n > 32) return city_33to64(b.v0, b.v1, b.v2, b.v3, n);
-        if (n > 16) return city_17to32(b.v0, b.v1, n);
-        return city_le16_reg(n == 16 ? b.v0 : window16(b.v0, b.v1, sh), n);
+        if (n > 16) return city_17to32(f, g, n);
+        return city_le16_reg(n == 16 ? f : window16(f, g, sh), n);
     }
     if (code == CODE_ZERO) return 0;
     uint64_t bits = 0;
     if (n == 8) {
-        bits = window8(b.v0, b.v1, sh);
+        bits = window8(f, g, sh);
     } else if (n != 0) {
         bad = true;
         return 0;
     }
     return hash_numeric(code, bits);
+}
+
+// Debug shapes (variants 40/41).  touch_blk: the loads a slot's
+// hash issues (its block plus every > 64-byte loop block), folded by XOR, no
+// hash arithmetic.  fake_block: a block made from the address, no loads.
+__device__ __forceinline__ uint64_t touch_blk(uint32_t code, const uint8_t* p, uint32_t n, const Blk& b) {
+    uint64_t h = b.v0.x ^ b.v0.y ^ b.v1.x ^ b.v1.y ^ b.v2.x ^ b.v2.y ^ b.v3.x ^ b.v3.y;
+    if (code == CODE_STRING && n > 64) {
+        const uint32_t blocks = (n - 1) >> 6;
+        for (uint32_t k = 0; k < blocks; ++k) {
+            const u64x2 a0 = gld16(p + 64 * k), a1 = gld16(p + 64 * k + 16);
+            const u64x2 a2 = gld16(p + 64 * k + 32), a3 = gld16(p + 64 * k + 48);
+            h ^= a0.x ^ a0.y ^ a1.x ^ a1.y ^ a2.x ^ a2.y ^ a3.x ^ a3.y;
+        }
+    }
+    return h;
+}
+
+__device__ __forceinline__ Blk fake_block(const uint8_t* p, uint32_t n) {
+    Blk b;
+    b.v0 = ld16<true>(p);
+    b.v1 = ld16<true>(p + n);
+    b.v2 = ld16<true>(p + 2 * n);
+    b.v3 = ld16<true>(p + 3 * n);
+    return b;
 }
 
 // Inclusive wave64 prefix sum on DPP (row_shr within 16-lane rows, then the

@@ -111,7 +111,7 @@ def test_kernel_for_reports_the_auto_policy():
     schema, with no device needed."""
     from hyperdex_amd import synth
     from hyperdex_amd.hashing import kernel_for
-    want = {"cfg1": 12, "cfg2": 21, "cfg3a": 25, "cfg3b": 12, "mixed": 19}
+    want = {"cfg1": 12, "cfg2": 21, "cfg3a": 25, "cfg3b": 35, "mixed": 19}
     for cfg, v in want.items():
         got, name = kernel_for([r.type for r in synth.CONFIGS[cfg]], 10_000_000)
         assert got == v and name.startswith("void hdx::hash_"), (cfg, got, name)
@@ -132,7 +132,8 @@ def test_kernel_names_match_the_built_symbols():
     mangled = sorted(set(m.decode() for m in re.findall(rb"_ZN3hdx\w+kernel\w+BatchArgsE", raw)))
     demangled = set(subprocess.run(["c++filt"], input="\n".join(mangled), capture_output=True,
                                    text=True).stdout.split("\n"))
-    for types in ([9217] * 17, [9217, 9218, 9218, 9218, 9218], [9217], [9217, 9473]):
+    for types in ([9217] * 17, [9217, 9218, 9218, 9218, 9218], [9217], [9217, 9473],
+                  [9217] * 11 + [9218] * 3 + [9219] * 3):
         for n in (1000, 10_000_000):
             _, name = kernel_for(types, n)
             assert name in demangled, (name, sorted(demangled)[:5])

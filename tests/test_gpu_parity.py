@@ -269,7 +269,7 @@ def test_full_size_sampled(oracle, torch_dev, cfg):
     torch.cuda.empty_cache()
 
 
-VARIANTS = [12, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30]
+VARIANTS = [12, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 34, 35, 36, 37, 38, 39]
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
@@ -286,6 +286,13 @@ def test_every_kernel_variant_matches_oracle(oracle, torch_dev, variant):
                        ("mixed", 900), ("wide", 131), ("keyonly_long", 70)]:
             types, blob, base, lens = synth.make_batch_host(cfg, n, seed=variant * 100 + n)
             check_batch(oracle, torch, dev, types, blob, base, lens)
+        # every string length 0..200 (all regimes, 1..3 loop blocks) at every
+        # byte alignment, the last value ending at the blob's last byte
+        rng = np.random.default_rng(variant)
+        L = np.repeat(np.arange(201, dtype=np.uint32), 16)
+        base = np.arange(len(L), dtype=np.uint64) * 224 + np.tile(np.arange(16, dtype=np.uint64), 201)
+        blob = rng.integers(0, 256, int(base[-1]) + 200, dtype=np.uint8)
+        check_batch(oracle, torch, dev, [dt.HYPERDATATYPE_STRING], blob, base, L)
         types, blob, base, lens = synth.make_batch_host("cfg3b", 999, seed=5)
         perm = np.random.default_rng(variant).permutation(999)
         A = len(types)
