@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libhdxhash.so")
+LIB_PATH = os.environ.get("HDX_LIB_PATH") or os.path.join(_HERE, "libhdxhash.so")
 
 HDX_OK = 0
 HDX_E_BADTYPE = 1

@@ -26,8 +26,30 @@ constexpr uint64_t KMUL = 0x9ddfea08eb382d69ULL;
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ uint64_t ror(uint64_t v, int r) { return (v >> r) | (v << (64 - r)); }
-__device__ __forceinline__ uint64_t shiftmix(uint64_t v) { return v ^ (v >> 47); }
+
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+// (lo, hi) -> u64 as a register pair (a shift-or would be rewritten into adds)
+__device__ __forceinline__ uint64_t pack64(uint32_t lo, uint32_t hi) {
+    const u32x2 t = {lo, hi};
+    return __builtin_bit_cast(uint64_t, t);
+}
+
+// Rotate right by a constant 1..63 as two v_alignbit_b32 (the compiler's
+// 64-bit funnel lowering takes three instructions).
+__device__ __forceinline__ uint64_t ror(uint64_t v, int r) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    if (r >= 32) {
+        const uint32_t t = lo; lo = hi; hi = t;
+        r -= 32;
+    }
+    if (r == 0) return pack64(lo, hi);
+    return pack64(__builtin_amdgcn_alignbit(hi, lo, r), __builtin_amdgcn_alignbit(lo, hi, r));
+}
+// v ^ (v >> 47): only the low word changes.
+__device__ __forceinline__ uint64_t shiftmix(uint64_t v) {
+    const uint32_t hi = (uint32_t)(v >> 32);
+    return pack64((uint32_t)v ^ (hi >> 15), hi);
+}
 __device__ __forceinline__ uint64_t bswap(uint64_t v) { return __builtin_bswap64(v); }
 
 // city.cc:268-276 (and Hash128to64 with mul = KMUL)

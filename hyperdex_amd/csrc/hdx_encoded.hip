@@ -50,33 +50,43 @@ struct alignas(8) EncDesc {
 };
 constexpr uint32_t kZeroSlot = 0xffffffffu;
 
-__host__ __device__ constexpr size_t encoded_lds_per_wave(uint32_t A) {
-    return 64 * 16 + 256 + (size_t)64 * A * sizeof(EncDesc);
+// Wave-private LDS: G object bases {value, key}, the code table, descriptors
+// and, when sorting, the class-sorted slot order and its counters.
+__host__ __device__ constexpr size_t encoded_lds_per_wave(uint32_t A, uint32_t G = 64, bool sort = false) {
+    return ((size_t)G * 16 + 256 + (size_t)G * A * sizeof(EncDesc) +
+            (sort ? (size_t)G * A * 2 + 2 * 16 * 4 : 0) + 15) & ~(size_t)15;
 }
 
-template <bool TOUCH, bool A4 = false>
+// G objects per wave (one lane each walks its value's length prefixes); SORT:
+// the wave's G*A slots are hashed in passes sorted by work class (LDS
+// fetch-add counting sort), so a pass runs few CityHash regimes.
+template <bool TOUCH, bool A4 = false, int G = 64, bool SORT = false>
 __global__ void __launch_bounds__(256)
 hash_encoded_kernel(const EncodedArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     const uint32_t A = a.A;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    // wave-private LDS: 64 object bases {value, key}, the code table, descriptors
-    uint8_t* wsmem = smem_raw + (size_t)w * encoded_lds_per_wave(A);
-    uint64_t* bases = reinterpret_cast<uint64_t*>(wsmem);           // [64][2]
-    uint8_t* codes = wsmem + 64 * 16;                                // [256]
-    EncDesc* desc = reinterpret_cast<EncDesc*>(wsmem + 64 * 16 + 256);
-    const uint64_t o0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + w) * 64;
+    uint8_t* wsmem = smem_raw + (size_t)w * encoded_lds_per_wave(A, G, SORT);
+    uint64_t* bases = reinterpret_cast<uint64_t*>(wsmem);           // [G][2]
+    uint8_t* codes = wsmem + G * 16;                                 // [256]
+    EncDesc* desc = reinterpret_cast<EncDesc*>(wsmem + G * 16 + 256);
+    uint16_t* perm = reinterpret_cast<uint16_t*>(desc + G * A);      // [G*A] (SORT)
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(perm + G * A);       // [16] (SORT), 4-aligned: G*A*2 even
+    uint32_t* cursor = cnt + 16;
+    const uint64_t o0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + w) * G;
     if (o0 >= a.n) return;  // no workgroup barrier: waves are independent
-    const uint32_t nobj = (uint32_t)min<uint64_t>(64, a.n - o0);
+    const uint32_t nobj = (uint32_t)min<uint64_t>(G, a.n - o0);
     const bool valid = (uint32_t)lane < nobj;
     const uint64_t i = o0 + (valid ? lane : 0);
 
-    const uint64_t voff = a.val_off[i], koff = a.key_off[i];
+    const uint64_t voff = valid ? a.val_off[i] : 0, koff = valid ? a.key_off[i] : 0;
     const uint32_t vlen = valid ? a.val_len[i] : 0u, klen = valid ? a.key_len[i] : 0u;
     const uint8_t* v = a.vals + voff;
-    bases[2 * lane] = voff;
-    bases[2 * lane + 1] = koff;
+    if (lane < G) {
+        bases[2 * lane] = voff;
+        bases[2 * lane + 1] = koff;
+    }
     for (uint32_t j = lane; j < A; j += 64) codes[j] = a.codes[j];
 
     // phase 0: pull the value's lines toward L2 (independent loads, consumed late)
@@ -91,7 +101,7 @@ hash_encoded_kernel(const EncodedArgs a) {
     bool ok = valid && vlen >= 10;
     const uint64_t version = ok ? load_be64(v) : 0;
     ok = ok && load_be16(v + 8) == A - 1;
-    desc[lane * A] = EncDesc{0u, klen};
+    if (valid) desc[lane * A] = EncDesc{0u, klen};
     uint32_t pos = 10;
     for (uint32_t k = 0; k + 1 < A; ++k) {
         uint32_t len = 0;
@@ -104,10 +114,10 @@ hash_encoded_kernel(const EncodedArgs a) {
                 if (len > vlen - pos) ok = false;  // the reference does not check this (:201-213)
             }
         }
-        desc[lane * A + 1 + k] = EncDesc{ok ? pos : kZeroSlot, ok ? len : 0u};
+        if (valid) desc[lane * A + 1 + k] = EncDesc{ok ? pos : kZeroSlot, ok ? len : 0u};
         if (ok) pos += len;
     }
-    if (!ok)  // undecodable (or past the batch end): every coordinate of the object is 0
+    if (valid && !ok)  // undecodable: every coordinate of the object is 0
         for (uint32_t j = 0; j < A; ++j) desc[lane * A + j] = EncDesc{kZeroSlot, 0u};
     if (valid && a.versions) a.versions[i] = ok ? version : 0;
     const bool any_bad = __any(valid && !ok);
@@ -116,23 +126,53 @@ hash_encoded_kernel(const EncodedArgs a) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    // phase 2: A passes of 64 slots, slot s = object * A + attribute.  The
-    // object's bases and the attribute's code are read from LDS, not from other
-    // lanes: in a partial pass the lanes past the batch end are inactive, and a
-    // ds_bpermute from an inactive lane returns 0.
     const uint32_t nslots = nobj * A;
+    if constexpr (SORT) {
+        // counting sort of the slots by work class: counts, exclusive scan
+        // into cursors, then one fetch-add per slot for its position
+        if (lane < 16) cnt[lane] = 0;
+        auto class_of = [&](uint32_t s) {
+            const uint32_t j = s - (s / A) * A;
+            const EncDesc d = desc[s];
+            return d.off == kZeroSlot ? 0u : work_class10(codes[j], d.len);
+        };
+        for (uint32_t s = lane; s < nslots; s += 64)
+            __hip_atomic_fetch_add(&cnt[class_of(s)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t c = lane < 16 ? cnt[lane] : 0u;
+        const uint32_t start = wave_scan_dpp(c) - c;
+        if (lane < 16) cursor[lane] = start;
+        for (uint32_t s = lane; s < nslots; s += 64) {
+            const uint32_t p = __hip_atomic_fetch_add(&cursor[class_of(s)], 1u, __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_WAVEFRONT);
+            perm[p] = (uint16_t)s;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+
+    // phase 2: passes of 64 slots (slot s = object * A + attribute; in class
+    // order when sorting).  The object's bases and the attribute's code are
+    // read from LDS, not from other lanes: in a partial pass the lanes past the
+    // batch end are inactive, and a ds_bpermute from an inactive lane returns 0.
+    const uint32_t npass = (nslots + 63) / 64;
     uint64_t* out = a.coords + o0 * A;
     struct Pass {
         const uint8_t* p;
-        uint32_t n, code;
+        uint32_t n, code, s;
         Raw blk;
     };
     auto load_pass = [&](uint32_t t, Pass& P) {
-        const uint32_t s = min(t * 64 + (uint32_t)lane, nslots - 1);
+        const uint32_t q = t * 64 + (uint32_t)lane;
+        const uint32_t s = SORT ? (q < nslots ? (uint32_t)perm[q] : nslots - 1) : min(q, nslots - 1);
         const uint32_t obj = s / A, j = s - obj * A;
         const EncDesc d = desc[s];
         const uint64_t base = bases[2 * obj + (j == 0)];
-        const bool zero = d.off == kZeroSlot || t * 64 + (uint32_t)lane >= nslots;
+        const bool zero = d.off == kZeroSlot || q >= nslots;
+        P.s = q < nslots ? s : 0xffffffffu;
         P.code = zero ? (uint32_t)CODE_ZERO : (uint32_t)codes[j];
         P.n = zero ? 0u : d.len;
         P.p = zero ? g_zero_pad : (j == 0 ? a.keys : a.vals) + base + d.off;
@@ -142,46 +182,50 @@ hash_encoded_kernel(const EncodedArgs a) {
     Pass P0, P1;
     load_pass(0, P0);
     for (uint32_t t = 0;; t += 2) {
-        if (t + 1 < A) load_pass(t + 1, P1);
+        if (t + 1 < npass) load_pass(t + 1, P1);
         {
             const uint64_t h = hash_blk<false, false, A4>(P0.code, P0.p, P0.n, consume_any<A4>(P0.blk), bad);
-            const uint32_t s = t * 64 + lane;
-            if (s < nslots) __builtin_nontemporal_store(h, out + s);
+            if (P0.s != 0xffffffffu) __builtin_nontemporal_store(h, out + P0.s);
         }
-        if (t + 1 >= A) break;
-        if (t + 2 < A) load_pass(t + 2, P0);
+        if (t + 1 >= npass) break;
+        if (t + 2 < npass) load_pass(t + 2, P0);
         {
             const uint64_t h = hash_blk<false, false, A4>(P1.code, P1.p, P1.n, consume_any<A4>(P1.blk), bad);
-            const uint32_t s = (t + 1) * 64 + lane;
-            if (s < nslots) __builtin_nontemporal_store(h, out + s);
+            if (P1.s != 0xffffffffu) __builtin_nontemporal_store(h, out + P1.s);
         }
-        if (t + 2 >= A) break;
+        if (t + 2 >= npass) break;
     }
     if (a.status && lane == 0 && any_bad) atomicOr(a.status, 1u << 6 /* HDX_E_BADENC */);
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream) {
-    if (a.n == 0) return hipSuccess;
-    // 4 waves per workgroup while they fit in 64 KiB of LDS (A <= 28), else 1
-    const uint32_t waves_per_block = 4 * encoded_lds_per_wave(a.A) <= 65536 ? 4 : 1;
-    const uint64_t waves = (a.n + 63) / 64;
+template <bool TOUCH, bool A4, int G, bool SORT>
+static hipError_t launch_encoded(const EncodedArgs& a, hipStream_t stream) {
+    // 4 waves per workgroup while they fit in 64 KiB of LDS, else 1
+    const size_t per_wave = encoded_lds_per_wave(a.A, G, SORT);
+    const uint32_t waves_per_block = 4 * per_wave <= 65536 ? 4 : 1;
+    const uint64_t waves = (a.n + G - 1) / G;
     const uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    const size_t lds = (size_t)waves_per_block * encoded_lds_per_wave(a.A);
+    hipLaunchKernelGGL((hash_encoded_kernel<TOUCH, A4, G, SORT>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
+                       waves_per_block * per_wave, stream, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream) {
+    if (a.n == 0) return hipSuccess;
     // default: dword-aligned loads (5.49 vs 6.14 ms per 10 M config-3b objects,
     // profiles/r1/ab_a4_cfg5.jsonl); variant 43 = byte-addressed loads, variant
-    // 33 adds the phase-0 line touch to those (measured 11 % slower, r1u)
-    if (hash_variant() == 43)
-        hipLaunchKernelGGL((hash_encoded_kernel<false, false>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
-                           lds, stream, a);
-    else if (hash_variant() == 33)
-        hipLaunchKernelGGL((hash_encoded_kernel<true>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
-                           lds, stream, a);
-    else
-        hipLaunchKernelGGL((hash_encoded_kernel<false, true>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
-                           lds, stream, a);
-    return hipGetLastError();
+    // 33 adds the phase-0 line touch to those (measured 11 % slower, r1u);
+    // 47-49: the class-sorted passes with 64 / 32 / 16 objects per wave
+    switch (hash_variant()) {
+        case 43: return launch_encoded<false, false, 64, false>(a, stream);
+        case 33: return launch_encoded<true, false, 64, false>(a, stream);
+        case 47: return launch_encoded<false, true, 64, true>(a, stream);
+        case 48: return launch_encoded<false, true, 32, true>(a, stream);
+        case 49: return launch_encoded<false, true, 16, true>(a, stream);
+        default: return launch_encoded<false, true, 64, false>(a, stream);
+    }
 }
 
 }  // namespace hdx

@@ -40,6 +40,8 @@ void finalize_args(BatchArgs& args);
 // registers, 3 +string-block prefetch, 4 = 3 without length prefetch, 5/6 = 2/3 with
 // non-temporal coordinate stores.
 hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, int variant);
+// The workgroup-window kernel (hdx_window.hip), variants 50 / 51.
+hipError_t launch_hash_window(const BatchArgs& args, hipStream_t stream, int variant);
 // The variant launch_hash_batch uses: HDX_KERNEL_VARIANT (tuning knob) or the default.
 int hash_variant();
 int set_hash_variant(int v);  // -2 if unknown, else the previous selection (-1 = auto)

@@ -40,21 +40,6 @@ namespace hdx {
 // neighbouring wave just pulled through L2).
 // ===========================================================================
 
-// Wave-uniform slot -> (object, attribute) split without a 64-bit integer
-// divide: q < 2^53, so the f64 quotient is off by at most one; fix it up.
-__device__ __forceinline__ void split_slot(uint64_t q, uint32_t A, uint64_t& i0, uint32_t& j0) {
-    uint64_t i = (uint64_t)((double)q * (1.0 / (double)A));
-    int64_t rem = (int64_t)(q - i * A);
-    if (rem < 0) { --i; rem += A; }
-    if (rem >= (int64_t)A) { ++i; rem -= A; }
-    i0 = i;
-    j0 = (uint32_t)rem;
-}
-
-__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
-    return __builtin_amdgcn_readlane(wave_scan_dpp(v), 63);
-}
-
 // SHAPE (debug variants only): 0 = the real kernel; 1 = its loads without the
 // hash arithmetic (variant 40); 2 = its arithmetic without the byte loads
 // (variant 41).  Shapes 1 and 2 write wrong coordinates: they bound the
@@ -155,7 +140,7 @@ struct RegroupStageLds {
 };
 
 template <int C, bool NT_STORE, bool SORT = true, bool DIRECT = true, bool STAGE = false, bool A4 = false,
-          bool PIPE = false>
+          bool PIPE = false, int WPE = 8>
 __global__ void __launch_bounds__(256)
 hash_regroup_kernel(const BatchArgs args) {
     typedef typename std::conditional<STAGE, RegroupStageLds<C>, RegroupLds<C>>::type Lds;
@@ -307,14 +292,18 @@ hash_regroup_kernel(const BatchArgs args) {
 }
 
 template <int C, bool NT, bool SORT = true, bool DIRECT = true, bool STAGE = false, bool A4 = false,
-          bool PIPE = false>
+          bool PIPE = false, int WPE = 8>
 static hipError_t launch_regroup(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT, DIRECT, STAGE, A4, PIPE>), dim3((uint32_t)blocks), dim3(256), 0, stream,
-                       args);
+    // WPE < 8 (A/B only): pad the workgroup's LDS so that at most WPE
+    // workgroups (= waves per SIMD) fit on a CU
+    typedef typename std::conditional<STAGE, RegroupStageLds<C>, RegroupLds<C>>::type Lds;
+    const size_t pad = WPE < 8 ? 163840 / WPE - sizeof(Lds) - 1024 : 0;
+    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT, DIRECT, STAGE, A4, PIPE, WPE>), dim3((uint32_t)blocks), dim3(256),
+                       pad, stream, args);
     return hipGetLastError();
 }
 
@@ -352,6 +341,12 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 37: return launch_regroup<2, true, true, true, false, true, true>(args, stream);
         case 38: return launch_regroup<3, true, true, true, false, true>(args, stream);
         case 39: return launch_regroup<2, true, true, false, false, true>(args, stream);
+        case 44: return launch_regroup<2, true, true, true, false, true, false, 5>(args, stream);
+        case 45: return launch_regroup<2, true, true, true, false, true, false, 4>(args, stream);
+        case 46: return launch_regroup<2, true, true, true, false, true, false, 3>(args, stream);
+        case 50:
+        case 51:
+        case 59: return launch_hash_window(args, stream, variant);
         case 40: return launch_chunk<true, false, 1>(args, stream);
         case 41: return launch_chunk<true, false, 2>(args, stream);
         default: return hipErrorInvalidValue;
@@ -359,9 +354,9 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
 }
 
 static constexpr int kDefaultVariant = -1;  // automatic
-// 33 / 43 select the stored-object sweep's line-touch and byte-addressed forms
-// (hdx_encoded.hip).
-static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 43); }
+// 33 / 43 select the stored-object sweep's line-touch and byte-addressed forms,
+// 47-49 its class-sorted forms (hdx_encoded.hip).
+static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 49) || v == 50 || v == 51 || v == 59; }
 
 static int g_variant = [] {
     const char* e = getenv("HDX_KERNEL_VARIANT");
@@ -431,25 +426,27 @@ const char* variant_kernel_name(int v) {
         case 12: return "void hdx::hash_chunk_kernel<true, false, 0, false>(hdx::BatchArgs)";
         case 30: return "void hdx::hash_chunk_kernel<true, true, 0, false>(hdx::BatchArgs)";
         case 31: return "void hdx::hash_chunk_kernel<true, false, 0, true>(hdx::BatchArgs)";
-        case 32: return "void hdx::hash_regroup_kernel<4, true, false, true, false, true, false>(hdx::BatchArgs)";
-        case 34: return "void hdx::hash_regroup_kernel<8, true, true, true, false, true, false>(hdx::BatchArgs)";
-        case 35: return "void hdx::hash_regroup_kernel<2, true, true, true, false, true, false>(hdx::BatchArgs)";
-        case 36: return "void hdx::hash_regroup_kernel<4, true, true, true, false, true, false>(hdx::BatchArgs)";
-        case 37: return "void hdx::hash_regroup_kernel<2, true, true, true, false, true, true>(hdx::BatchArgs)";
-        case 38: return "void hdx::hash_regroup_kernel<3, true, true, true, false, true, false>(hdx::BatchArgs)";
-        case 39: return "void hdx::hash_regroup_kernel<2, true, true, false, false, true, false>(hdx::BatchArgs)";
-        case 18: return "void hdx::hash_regroup_kernel<4, true, true, true, false, false, false>(hdx::BatchArgs)";
-        case 19: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, false>(hdx::BatchArgs)";
-        case 20: return "void hdx::hash_regroup_kernel<8, true, false, true, false, false, false>(hdx::BatchArgs)";
-        case 21: return "void hdx::hash_regroup_kernel<4, true, false, true, false, false, false>(hdx::BatchArgs)";
-        case 22: return "void hdx::hash_regroup_kernel<16, true, false, true, false, false, false>(hdx::BatchArgs)";
-        case 23: return "void hdx::hash_regroup_kernel<8, true, false, false, false, false, false>(hdx::BatchArgs)";
-        case 24: return "void hdx::hash_regroup_kernel<4, true, false, false, false, false, false>(hdx::BatchArgs)";
-        case 25: return "void hdx::hash_regroup_kernel<16, true, false, false, false, false, false>(hdx::BatchArgs)";
-        case 26: return "void hdx::hash_regroup_kernel<2, true, true, true, false, false, false>(hdx::BatchArgs)";
-        case 27: return "void hdx::hash_regroup_kernel<2, true, false, true, false, false, false>(hdx::BatchArgs)";
-        case 28: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, false>(hdx::BatchArgs)";
-        case 29: return "void hdx::hash_regroup_kernel<4, true, true, true, true, false, false>(hdx::BatchArgs)";
+        case 32: return "void hdx::hash_regroup_kernel<4, true, false, true, false, true, false, 8>(hdx::BatchArgs)";
+        case 34: return "void hdx::hash_regroup_kernel<8, true, true, true, false, true, false, 8>(hdx::BatchArgs)";
+        case 35: return "void hdx::hash_regroup_kernel<2, true, true, true, false, true, false, 8>(hdx::BatchArgs)";
+        case 50: return "void hdx::hash_window_kernel<256, 20480>(hdx::BatchArgs)";
+        case 51: return "void hdx::hash_window_kernel<512, 35840>(hdx::BatchArgs)";
+        case 36: return "void hdx::hash_regroup_kernel<4, true, true, true, false, true, false, 8>(hdx::BatchArgs)";
+        case 37: return "void hdx::hash_regroup_kernel<2, true, true, true, false, true, true, 8>(hdx::BatchArgs)";
+        case 38: return "void hdx::hash_regroup_kernel<3, true, true, true, false, true, false, 8>(hdx::BatchArgs)";
+        case 39: return "void hdx::hash_regroup_kernel<2, true, true, false, false, true, false, 8>(hdx::BatchArgs)";
+        case 18: return "void hdx::hash_regroup_kernel<4, true, true, true, false, false, false, 8>(hdx::BatchArgs)";
+        case 19: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, false, 8>(hdx::BatchArgs)";
+        case 20: return "void hdx::hash_regroup_kernel<8, true, false, true, false, false, false, 8>(hdx::BatchArgs)";
+        case 21: return "void hdx::hash_regroup_kernel<4, true, false, true, false, false, false, 8>(hdx::BatchArgs)";
+        case 22: return "void hdx::hash_regroup_kernel<16, true, false, true, false, false, false, 8>(hdx::BatchArgs)";
+        case 23: return "void hdx::hash_regroup_kernel<8, true, false, false, false, false, false, 8>(hdx::BatchArgs)";
+        case 24: return "void hdx::hash_regroup_kernel<4, true, false, false, false, false, false, 8>(hdx::BatchArgs)";
+        case 25: return "void hdx::hash_regroup_kernel<16, true, false, false, false, false, false, 8>(hdx::BatchArgs)";
+        case 26: return "void hdx::hash_regroup_kernel<2, true, true, true, false, false, false, 8>(hdx::BatchArgs)";
+        case 27: return "void hdx::hash_regroup_kernel<2, true, false, true, false, false, false, 8>(hdx::BatchArgs)";
+        case 28: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, false, 8>(hdx::BatchArgs)";
+        case 29: return "void hdx::hash_regroup_kernel<4, true, true, true, true, false, false, 8>(hdx::BatchArgs)";
         default: return "";
     }
 }

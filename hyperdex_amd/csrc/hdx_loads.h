@@ -96,28 +96,55 @@ __device__ __forceinline__ uint32_t gld4(const uint8_t* p) {
 }
 __device__ __forceinline__ const uint8_t* dw_floor(const uint8_t* p) { return p - ((uintptr_t)p & 3); }
 
-__device__ __forceinline__ Raw issue_block_a4(uint32_t code, const uint8_t* p, uint32_t n) {
-    const uint8_t* D = g_zero_pad;
+// Piece offsets of the A4 form, from the value's base (or from the zero pad
+// when the slot has no bytes to read: any = false), as 32-bit arithmetic;
+// pl = the base's low address bits.  Shared by the global-memory form
+// (issue_block_a4) and the LDS-window form (hdx_window.hip).
+struct A4Offsets {
+    int32_t o0, o1, o2, o3, e1, e3;  // dword-aligned piece starts and next dwords
+    uint32_t ra, rb;
+    bool any;
+};
+
+__device__ __forceinline__ A4Offsets a4_offsets(uint32_t code, uint32_t pl_, uint32_t n) {
     const bool str = code == CODE_STRING;
     const bool shortv = (str && n > 0 && n < 16) || (code >= CODE_INT64 && n == 8);
-    const uint8_t* lo = p - ((uintptr_t)p & 15);
-    const uint8_t* hi = (p + n - 1) - ((uintptr_t)(p + n - 1) & 15);
     const bool g64 = str && n > 64, g32 = str && n > 32 && n <= 64, g16 = str && n >= 16 && n <= 32;
-    const uint8_t* x0 = g64 ? p + n - 64 : g32 ? p : D;
-    const uint8_t* x1 = g64 ? p + n - 48 : g32 ? p + 16 : g16 ? p : shortv ? lo : D;
-    const uint8_t* x2 = g64 || g32 ? p + n - 32 : D;
-    const uint8_t* x3 = g64 ? p + n - 16 : g32 ? p + n - 16 : g16 ? p + n - 16 : shortv ? hi : D;
+    const bool big = g64 || g32;
+    A4Offsets o;
+    o.any = big || g16 || shortv;
+    const uint32_t pl = o.any ? pl_ : 0u;
+    const int32_t lo = -(int32_t)(pl & 15u);                          // 16-aligned chunk of byte 0
+    const int32_t hi = (int32_t)(((pl + n - 1u) & ~15u) - pl);       // ... of byte n-1
+    const int32_t x1 = g64 ? (int32_t)n - 48 : g32 ? 16 : g16 ? 0 : shortv ? lo : 0;
+    const int32_t x3 = big || g16 ? (int32_t)n - 16 : shortv ? hi : 0;
+    const int32_t x0 = big ? x1 - 16 : x1;  // g64: n-64, g32: 0; else a repeat of piece 1
+    const int32_t x2 = big ? x3 - 16 : x3;
+    o.ra = (pl + (uint32_t)x1) & 3u;  // piece 0 shares piece 1's alignment, piece 2 piece 3's
+    o.rb = (pl + (uint32_t)x3) & 3u;
+    // the dword after piece 1 (3) is the one holding its last byte when the
+    // piece is misaligned; else unused, and that dword is still a value byte's
+    o.e1 = x1 + 15 - (int32_t)((pl + (uint32_t)x1 + 15u) & 3u);
+    o.e3 = x3 + 15 - (int32_t)((pl + (uint32_t)x3 + 15u) & 3u);
+    o.o0 = x0 - (int32_t)o.ra;
+    o.o1 = x1 - (int32_t)o.ra;
+    o.o2 = x2 - (int32_t)o.rb;
+    o.o3 = x3 - (int32_t)o.rb;
+    return o;
+}
+
+__device__ __forceinline__ Raw issue_block_a4(uint32_t code, const uint8_t* p, uint32_t n) {
+    const A4Offsets o = a4_offsets(code, (uint32_t)(uintptr_t)p, n);
+    const uint8_t* base = o.any ? p : g_zero_pad;  // the zero pad is 64-byte aligned
     Raw r;
-    r.ra = (uint32_t)(uintptr_t)x1 & 3;
-    r.rb = (uint32_t)(uintptr_t)x3 & 3;
-    const uint8_t* a1 = dw_floor(x1);
-    const uint8_t* a3 = dw_floor(x3);
-    r.b.v0 = gld16(dw_floor(x0));
-    r.b.v1 = gld16(a1);
-    r.b.v2 = gld16(dw_floor(x2));
-    r.b.v3 = gld16(a3);
-    r.e1 = gld4(r.ra ? a1 + 16 : a1);  // only used when the piece is misaligned
-    r.e3 = gld4(r.rb ? a3 + 16 : a3);
+    r.ra = o.ra;
+    r.rb = o.rb;
+    r.b.v0 = gld16(base + o.o0);
+    r.b.v1 = gld16(base + o.o1);
+    r.b.v2 = gld16(base + o.o2);
+    r.b.v3 = gld16(base + o.o3);
+    r.e1 = gld4(base + o.e1);
+    r.e3 = gld4(base + o.e3);
     return r;
 }
 
@@ -125,8 +152,8 @@ __device__ __forceinline__ Raw issue_block_a4(uint32_t code, const uint8_t* p, u
 __device__ __forceinline__ u64x2 funnel16(const u64x2& v, uint32_t next, uint32_t r) {
     const uint32_t d0 = (uint32_t)v.x, d1 = (uint32_t)(v.x >> 32), d2 = (uint32_t)v.y, d3 = (uint32_t)(v.y >> 32);
     u64x2 w;
-    w.x = ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, r) << 32) | __builtin_amdgcn_alignbyte(d1, d0, r);
-    w.y = ((uint64_t)__builtin_amdgcn_alignbyte(next, d3, r) << 32) | __builtin_amdgcn_alignbyte(d3, d2, r);
+    w.x = pack64(__builtin_amdgcn_alignbyte(d1, d0, r), __builtin_amdgcn_alignbyte(d2, d1, r));
+    w.y = pack64(__builtin_amdgcn_alignbyte(d3, d2, r), __builtin_amdgcn_alignbyte(next, d3, r));
     return w;
 }
 
@@ -176,8 +203,8 @@ __device__ __forceinline__ u64x2 window16(const u64x2& c0, const u64x2& c1, uint
     const uint32_t o0 = __builtin_amdgcn_alignbyte(e1, e0, r), o1 = __builtin_amdgcn_alignbyte(e2, e1, r);
     const uint32_t o2 = __builtin_amdgcn_alignbyte(e3, e2, r), o3 = __builtin_amdgcn_alignbyte(e4, e3, r);
     u64x2 w;
-    w.x = ((uint64_t)o1 << 32) | o0;
-    w.y = ((uint64_t)o3 << 32) | o2;
+    w.x = pack64(o0, o1);
+    w.y = pack64(o2, o3);
     return w;
 }
 
@@ -188,32 +215,34 @@ __device__ __forceinline__ uint64_t window8(const u64x2& c0, const u64x2& c1, ui
     const uint32_t q = sh >> 2, r = sh & 3;
     const uint32_t e0 = pick4(q, d0, d1, d2, d3), e1 = pick4(q, d1, d2, d3, d4);
     const uint32_t e2 = pick4(q, d2, d3, d4, d5);
-    return ((uint64_t)__builtin_amdgcn_alignbyte(e2, e1, r) << 32) | __builtin_amdgcn_alignbyte(e1, e0, r);
+    return pack64(__builtin_amdgcn_alignbyte(e1, e0, r), __builtin_amdgcn_alignbyte(e2, e1, r));
 }
 
-// city.cc:278-301 with the (up to) 16 string bytes in registers.
+// city.cc:278-301 with the (up to) 16 string bytes in registers.  The
+// 8..16-byte and 4..7-byte cases both end in HashLen16(u, v, mul) (:283-296),
+// so their operands are chosen first and one HashLen16 serves both (a wave
+// holding both lengths runs one instead of two).
 __device__ __forceinline__ uint64_t city_le16_reg(const u64x2& w, uint32_t n) {
     const uint64_t mul = K2 + 2ull * n;
     const uint32_t d0 = (uint32_t)w.x, d1 = (uint32_t)(w.x >> 32);
     const uint32_t d2 = (uint32_t)w.y, d3 = (uint32_t)(w.y >> 32);
+    uint64_t u, v;
     if (n >= 8) {
         // b = bytes [n-8, n): shift by t = n-8 in 0..8
         const uint32_t t = n - 8, q = t >> 2, r = t & 3;
         const uint32_t e0 = q == 0 ? d0 : q == 1 ? d1 : d2;
         const uint32_t e1 = q == 0 ? d1 : q == 1 ? d2 : d3;
         const uint32_t e2 = q == 0 ? d2 : d3;
-        const uint64_t b = ((uint64_t)__builtin_amdgcn_alignbyte(e2, e1, r) << 32) |
-                           __builtin_amdgcn_alignbyte(e1, e0, r);
+        const uint64_t b = pack64(__builtin_amdgcn_alignbyte(e1, e0, r), __builtin_amdgcn_alignbyte(e2, e1, r));
         const uint64_t a = w.x + K2;
-        const uint64_t c = ror(b, 37) * mul + a;
-        const uint64_t d = (ror(a, 25) + b) * mul;
-        return mix16(c, d, mul);
+        u = ror(b, 37) * mul + a;
+        v = (ror(a, 25) + b) * mul;
+    } else {
+        u = n + ((uint64_t)d0 << 3);
+        v = __builtin_amdgcn_alignbyte(d1, d0, (n - 4) & 3);
     }
-    if (n >= 4) {
-        const uint64_t a = d0;
-        const uint32_t b = __builtin_amdgcn_alignbyte(d1, d0, n - 4);
-        return mix16(n + (a << 3), b, mul);
-    }
+    const uint64_t h = mix16(u, v, mul);
+    if (n >= 4) return h;
     if (n > 0) {
         const uint32_t y = (d0 & 0xff) + (((d0 >> (8 * (n >> 1))) & 0xff) << 8);
         const uint32_t z = n + (((d0 >> (8 * (n - 1))) & 0xff) << 2);
@@ -371,6 +400,39 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
     v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false); // row_bcast:15
     v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false); // row_bcast:31
     return v;
+}
+
+// Work classes for class-sorted passes: one per code path, so a pass holds as
+// few CityHash regimes as the slot mix allows (0: int64 / not hashable / past
+// the batch end, 1: float, 2: timestamp, 3: string <= 16 B, 4: 17..32,
+// 5: 33..64, 6..9: > 64 B with 1, 2, 3, >= 4 loop blocks).
+constexpr int kClasses10 = 10;
+__device__ __forceinline__ uint32_t work_class10(uint32_t code, uint32_t n) {
+    if (code == CODE_STRING) {
+        if (n <= 16) return 3;
+        if (n <= 32) return 4;
+        if (n <= 64) return 5;
+        const uint32_t b = (n - 1) >> 6;  // > 64-byte loop blocks
+        return b >= 4 ? 9u : 5u + b;
+    }
+    if (code == CODE_FLOAT) return 1;
+    if (code >= CODE_TS_SECOND) return 2;
+    return 0;
+}
+
+// Wave-uniform slot -> (object, attribute) split without a 64-bit integer
+// divide: q < 2^53, so the f64 quotient is off by at most one; fix it up.
+__device__ __forceinline__ void split_slot(uint64_t q, uint32_t A, uint64_t& i0, uint32_t& j0) {
+    uint64_t i = (uint64_t)((double)q * (1.0 / (double)A));
+    int64_t rem = (int64_t)(q - i * A);
+    if (rem < 0) { --i; rem += A; }
+    if (rem >= (int64_t)A) { ++i; rem -= A; }
+    i0 = i;
+    j0 = (uint32_t)rem;
+}
+
+__device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
+    return __builtin_amdgcn_readlane(wave_scan_dpp(v), 63);
 }
 
 }  // namespace hdx
