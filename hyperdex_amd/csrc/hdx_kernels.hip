@@ -346,6 +346,8 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 46: return launch_regroup<2, true, true, true, false, true, false, 3>(args, stream);
         case 50:
         case 51:
+        case 52:
+        case 53:
         case 59: return launch_hash_window(args, stream, variant);
         case 40: return launch_chunk<true, false, 1>(args, stream);
         case 41: return launch_chunk<true, false, 2>(args, stream);
@@ -355,8 +357,8 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
 
 static constexpr int kDefaultVariant = -1;  // automatic
 // 33 / 43 select the stored-object sweep's line-touch and byte-addressed forms,
-// 47-49 its class-sorted forms (hdx_encoded.hip).
-static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 49) || v == 50 || v == 51 || v == 59; }
+// 47-49 and 54-56 its class-sorted forms (hdx_encoded.hip).
+static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 49) || (v >= 50 && v <= 61); }
 
 static int g_variant = [] {
     const char* e = getenv("HDX_KERNEL_VARIANT");
@@ -429,8 +431,10 @@ const char* variant_kernel_name(int v) {
         case 32: return "void hdx::hash_regroup_kernel<4, true, false, true, false, true, false, 8>(hdx::BatchArgs)";
         case 34: return "void hdx::hash_regroup_kernel<8, true, true, true, false, true, false, 8>(hdx::BatchArgs)";
         case 35: return "void hdx::hash_regroup_kernel<2, true, true, true, false, true, false, 8>(hdx::BatchArgs)";
-        case 50: return "void hdx::hash_window_kernel<256, 20480>(hdx::BatchArgs)";
-        case 51: return "void hdx::hash_window_kernel<512, 35840>(hdx::BatchArgs)";
+        case 50: return "void hdx::hash_window_kernel<256, 20480, false>(hdx::BatchArgs)";
+        case 51: return "void hdx::hash_window_kernel<512, 35840, false>(hdx::BatchArgs)";
+        case 52: return "void hdx::hash_window_pipe_kernel<17920>(hdx::BatchArgs, unsigned long)";
+        case 53: return "void hdx::hash_window_pipe_kernel<24576>(hdx::BatchArgs, unsigned long)";
         case 36: return "void hdx::hash_regroup_kernel<4, true, true, true, false, true, false, 8>(hdx::BatchArgs)";
         case 37: return "void hdx::hash_regroup_kernel<2, true, true, true, false, true, true, 8>(hdx::BatchArgs)";
         case 38: return "void hdx::hash_regroup_kernel<3, true, true, true, false, true, false, 8>(hdx::BatchArgs)";

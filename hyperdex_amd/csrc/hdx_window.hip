@@ -327,6 +327,247 @@ hash_window_kernel(const BatchArgs args) {
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
+// ===========================================================================
+// Pipelined form (variants 52/53): a persistent workgroup walks windows of 256
+// slots (one chunk per wave) with two LDS buffers, so that window k+1's bytes
+// stream into LDS (LDS DMA) and window k+2's lengths / object bases load while
+// window k is hashed — one barrier per window, no exposed memory latency in
+// steady state.  Per iteration, with b = k's buffer:
+//   wait for every load in flight (window k's DMA, window k+1's metadata)
+//   A(k+1): addresses, classes, byte range -> meta[b^1]          [barrier]
+//   B(k+1): stage into win[b^1], descriptors, class sort -> perm[b^1]
+//   issue window k+2's metadata loads
+//   C(k):   hash window k from win[b] (or from global memory when it did not fit)
+// Buffer b^1 is free at the barrier: window k-1, its last user, was hashed
+// before it.
+// ===========================================================================
+template <int WIN>
+struct PipeLds {
+    uint32_t win[2][WIN / 4 + 8];
+    uint32_t desc[2][256];
+    uint16_t perm[2][256];
+    uint8_t code[2][256];
+    uint64_t lo[2][4], hi[2][4];
+    uint32_t ok[2][4];
+    uint32_t cnt[2][4][kWinClasses];
+    uint32_t cur[4][kWinClasses];
+};
+
+// One wave's 64 slots of a window: metadata loads in flight ...
+struct ChunkLoads {
+    uint32_t len;
+    uint64_t base;
+    uint32_t carry[4];  // lengths of the wave's first object's slots before the chunk
+    uint32_t j0;
+    uint64_t i0;
+};
+// ... and what they resolve to.
+struct ChunkSlots {
+    const uint8_t* p;
+    uint32_t n, code, cls;
+    bool need;
+};
+
+__device__ __forceinline__ ChunkLoads chunk_issue(const BatchArgs& args, uint64_t q0, uint64_t nslots, int lane) {
+    ChunkLoads c;
+    const uint32_t A = args.A;
+    split_slot(q0, A, c.i0, c.j0);
+    const uint64_t q = q0 + lane;
+    const bool valid = q < nslots;
+    const uint32_t t = c.j0 + (uint32_t)lane;
+    const uint32_t di = t / A;
+    c.len = valid ? args.attr_len[q] : 0u;
+    c.base = args.obj_base[valid ? c.i0 + di : c.i0];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {  // j0 < A <= 256
+        const uint32_t idx = (uint32_t)(r * 64 + lane);
+        c.carry[r] = (uint32_t)(r * 64) < c.j0 && idx < c.j0 ? args.attr_len[q0 - c.j0 + idx] : 0u;
+    }
+    return c;
+}
+
+__device__ __forceinline__ ChunkSlots chunk_resolve(const BatchArgs& args, const ChunkLoads& c, uint64_t q0,
+                                                    uint64_t nslots, int lane, uint32_t packed_codes) {
+    const uint32_t A = args.A;
+    uint32_t carry = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+        if ((uint32_t)(r * 64) < c.j0) carry += wave_sum_dpp(c.carry[r]);
+    const bool valid = q0 + lane < nslots;
+    const uint32_t t = c.j0 + (uint32_t)lane;
+    const uint32_t di = t / A;
+    const uint32_t j = t - di * A;
+    const uint32_t L = c.len;
+    const uint32_t Sx = wave_scan_dpp(L) - L;
+    const int head = lane - (int)j;
+    const uint32_t head_sx = __shfl(Sx, head < 0 ? 0 : head, 64);
+    const uint32_t off = head >= 0 ? Sx - head_sx : carry + Sx;
+    uint32_t code = args.uniform_code != 0xffu
+                        ? args.uniform_code
+                        : (__shfl(packed_codes, (int)(j >> 2), 64) >> (8 * (j & 3))) & 0xffu;
+    if (!valid) code = CODE_ZERO;
+    ChunkSlots s;
+    s.p = args.blob + c.base + off;
+    s.n = L;
+    s.code = code;
+    s.cls = valid ? work_class10(code, L) : 0u;
+    s.need = (code == CODE_STRING && L > 0) || (code >= CODE_INT64 && L == 8);
+    return s;
+}
+
+template <int WIN>
+__global__ void __launch_bounds__(256)
+hash_window_pipe_kernel(const BatchArgs args, uint64_t nwin) {
+    static_assert(WIN % 16 == 0 && WIN < 65536, "window shape");
+    __shared__ __attribute__((aligned(16))) PipeLds<WIN> L;
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const uint64_t nslots = args.n * args.A;
+    const uint64_t step = gridDim.x;
+    uint64_t k = blockIdx.x;
+    if (k >= nwin) return;  // whole workgroup
+    uint32_t packed_codes = 0;
+    if (args.uniform_code == 0xffu) packed_codes = reinterpret_cast<const uint32_t*>(args.codes)[lane];
+
+    // A: publish a window's byte range and class counts into meta[b]
+    auto publish = [&](const ChunkSlots& s, uint64_t q0, int b) {
+        const bool live = q0 < nslots;
+        if (lane < kWinClasses) L.cnt[b][w][lane] = 0;
+        __hip_atomic_fetch_add(&L.cnt[b][w][s.cls], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        const uint64_t first = readfirstlane64((uint64_t)(uintptr_t)s.p);
+        const int l_last = live ? (int)min<uint64_t>(63, nslots - 1 - q0) : 0;
+        const uint64_t e = (uint64_t)(uintptr_t)s.p + s.n;
+        const uint64_t last_end = pack64(__builtin_amdgcn_readlane((uint32_t)e, l_last),
+                                         __builtin_amdgcn_readlane((uint32_t)(e >> 32), l_last));
+        const uint64_t a = (uint64_t)(uintptr_t)s.p;
+        const bool inside = !s.need || (a >= first && a + s.n <= last_end);
+        const bool ok = __all(inside);
+        if (lane == 0) {
+            L.lo[b][w] = live ? first : ~0ull;
+            L.hi[b][w] = live ? last_end : 0ull;
+            L.ok[b][w] = ok;
+        }
+    };
+    // B: stage a window into buffer b, write its descriptors, sort it;
+    // returns whether it was staged (and whether it needs no permutation)
+    auto stage = [&](const ChunkSlots& s, int b, bool& uniform) -> bool {
+        uint64_t wlo = ~0ull, whi = 0;
+        bool ok = true;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            wlo = min(wlo, L.lo[b][v]);
+            whi = max(whi, L.hi[b][v]);
+            ok = ok && L.ok[b][v];
+        }
+        const uint64_t wbase = wlo & ~15ull;
+        const uint64_t t16 = whi > wlo ? ((whi + 15) & ~15ull) - wbase : 0;
+        uniform = false;
+        if (!(ok && t16 <= (uint64_t)WIN)) return false;
+        const uint32_t units = (uint32_t)(t16 >> 4);
+        for (uint32_t u0 = (uint32_t)w * 64; u0 < units; u0 += 256) {
+            const uint32_t u = u0 + (uint32_t)lane;
+            if (u < units)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(uintptr_t)(wbase + 16ull * u),
+                    (__attribute__((address_space(3))) void*)&L.win[b][u0 * 4], 16, 0, 0);
+        }
+        const uint32_t sl = (uint32_t)(w * 64 + lane);
+        const uint32_t off = s.need ? (uint32_t)((uint64_t)(uintptr_t)s.p - wbase) : 0u;
+        const uint32_t n = s.code == CODE_STRING ? s.n : min(s.n, 9u);
+        L.desc[b][sl] = off | (n << 16);
+        L.code[b][sl] = (uint8_t)s.code;
+        uint32_t tot = 0, before = 0;
+        if (lane < kWinClasses) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const uint32_t x = L.cnt[b][v][lane];
+                tot += x;
+                before += v < w ? x : 0u;
+            }
+        }
+        uniform = __any(tot == 256u);
+        if (!uniform) {
+            const uint32_t start = wave_scan_dpp(tot) - tot + before;
+            if (lane < kWinClasses) L.cur[w][lane] = start;
+            const uint32_t pos = __hip_atomic_fetch_add(&L.cur[w][s.cls], 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_WAVEFRONT);
+            L.perm[b][pos] = (uint16_t)sl;
+        }
+        return true;
+    };
+
+    // prologue: window k's metadata, publish, barrier, stage; window k+1's loads
+    uint64_t q0 = k * 256 + (uint64_t)w * 64;
+    ChunkSlots cur = chunk_resolve(args, chunk_issue(args, min(q0, nslots - 1), nslots, lane), q0, nslots, lane,
+                                   packed_codes);
+    publish(cur, q0, 0);
+    __syncthreads();
+    bool cur_uniform;
+    bool cur_staged = stage(cur, 0, cur_uniform);
+    uint64_t q0n = (k + step) * 256 + (uint64_t)w * 64;
+    ChunkLoads nl;
+    if (k + step < nwin) nl = chunk_issue(args, min(q0n, nslots - 1), nslots, lane);
+    bool bad = false;
+    for (int b = 0;; b ^= 1) {
+        const bool has_next = k + step < nwin;
+        __builtin_amdgcn_s_waitcnt(0);  // window k's DMA and window k+1's metadata
+        ChunkSlots nxt;
+        if (has_next) {
+            nxt = chunk_resolve(args, nl, q0n, nslots, lane, packed_codes);
+            publish(nxt, q0n, b ^ 1);
+        }
+        __syncthreads();
+        bool nxt_uniform = false, nxt_staged = false;
+        const uint64_t q0nn = (k + 2 * step) * 256 + (uint64_t)w * 64;
+        if (has_next) {
+            nxt_staged = stage(nxt, b ^ 1, nxt_uniform);
+            if (k + 2 * step < nwin) nl = chunk_issue(args, min(q0nn, nslots - 1), nslots, lane);
+        }
+        // C: hash window k
+        const uint64_t qwg = k * 256;
+        if (cur_staged) {
+            const uint32_t tpos = (uint32_t)(w * 64 + lane);
+            const uint32_t sl = cur_uniform ? tpos : L.perm[b][tpos];
+            const uint32_t d = L.desc[b][sl];
+            const uint32_t code = L.code[b][sl];
+            const uint32_t off = d & 0xffffu, n = d >> 16;
+            const Blk blk = lds_block_a4(L.win[b], code, off, n);
+            const uint64_t h = hash_blk_lds(L.win[b], code, off, n, blk, bad);
+            const uint64_t q = qwg + sl;
+            if (q < nslots) __builtin_nontemporal_store(h, args.coords + q);
+        } else if (q0 < nslots) {
+            const Raw r = issue_block_a4(cur.code, cur.p, cur.n);
+            const uint64_t h = hash_blk<false, false, true>(cur.code, cur.p, cur.n, funnel_raw(r), bad);
+            if (q0 + lane < nslots) __builtin_nontemporal_store(h, args.coords + q0 + lane);
+        }
+        if (!has_next) break;
+        k += step;
+        q0 = q0n;
+        q0n = q0nn;
+        cur = nxt;
+        cur_staged = nxt_staged;
+        cur_uniform = nxt_uniform;
+    }
+    if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
+}
+
+template <int WIN, int WG_PER_CU>
+static hipError_t launch_window_pipe(const BatchArgs& args, hipStream_t stream) {
+    static const int cus = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 256;
+        return n > 0 ? n : 256;
+    }();
+    const uint64_t nwin = (args.n * args.A + 255) / 256;
+    if (nwin == 0) return hipSuccess;
+    const uint64_t cap = (uint64_t)cus * WG_PER_CU;
+    const uint64_t grid = nwin < cap ? nwin : cap;
+    hipLaunchKernelGGL((hash_window_pipe_kernel<WIN>), dim3((uint32_t)grid), dim3(256), 0, stream, args, nwin);
+    return hipGetLastError();
+}
+
 template <int S, int WIN, bool NOHASH = false>
 static hipError_t launch_window(const BatchArgs& args, hipStream_t stream) {
     const uint64_t blocks = (args.n * args.A + S - 1) / S;
@@ -341,6 +582,8 @@ hipError_t launch_hash_window(const BatchArgs& args, hipStream_t stream, int var
         case 50: return launch_window<256, 20480>(args, stream);
         case 51: return launch_window<512, 35840>(args, stream);
         case 59: return launch_window<512, 35840, true>(args, stream);
+        case 52: return launch_window_pipe<17920, 4>(args, stream);
+        case 53: return launch_window_pipe<24576, 3>(args, stream);
         default: return hipErrorInvalidValue;
     }
 }
