@@ -50,52 +50,36 @@ struct alignas(8) EncDesc {
 };
 constexpr uint32_t kZeroSlot = 0xffffffffu;
 
-// Wave-private LDS: G object bases {value, key}, the code table, descriptors
-// and, when sorting, the class-sorted slot order and its counters.
-// Sort groups of a wave: at most ceil(G*A / (SPAN*64)) of 16 counters each.
-__host__ __device__ constexpr uint32_t encoded_sort_groups(uint32_t A, uint32_t G, uint32_t span) {
-    return span ? (G * A + span * 64 - 1) / (span * 64) : 1;
-}
-__host__ __device__ constexpr size_t encoded_lds_per_wave(uint32_t A, uint32_t G = 64, bool sort = false,
-                                                          uint32_t span = 0) {
-    return ((size_t)G * 16 + 256 + (size_t)G * A * sizeof(EncDesc) +
-            (sort ? (size_t)G * A * 2 + 2 * 16 * 4 * encoded_sort_groups(A, G, span) : 0) + 15) & ~(size_t)15;
+// Wave-private LDS: 64 object bases {value, key}, the code table, descriptors.
+__host__ __device__ constexpr size_t encoded_lds_per_wave(uint32_t A) {
+    return 64 * 16 + 256 + (size_t)64 * A * sizeof(EncDesc);
 }
 
-// G objects per wave (one lane each walks its value's length prefixes); SORT:
-// the wave's slots are hashed in passes sorted by work class (LDS fetch-add
-// counting sort), so a pass runs few CityHash regimes — within groups of
-// SPAN passes (SPAN = 0: all of the wave's slots), so that a group's passes
-// still read neighbouring bytes.
 // SHAPE (debug variants 57/58 only, wrong coordinates): 1 = the walk alone
 // (no phase 2), 2 = phase 2's loads without the hash arithmetic.
-template <bool TOUCH, bool A4 = false, int G = 64, bool SORT = false, int SPAN = 0, int SHAPE = 0>
+template <bool TOUCH, bool A4 = false, int SHAPE = 0>
 __global__ void __launch_bounds__(256)
 hash_encoded_kernel(const EncodedArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     const uint32_t A = a.A;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    uint8_t* wsmem = smem_raw + (size_t)w * encoded_lds_per_wave(A, G, SORT, SPAN);
-    uint64_t* bases = reinterpret_cast<uint64_t*>(wsmem);           // [G][2]
-    uint8_t* codes = wsmem + G * 16;                                 // [256]
-    EncDesc* desc = reinterpret_cast<EncDesc*>(wsmem + G * 16 + 256);
-    uint16_t* perm = reinterpret_cast<uint16_t*>(desc + G * A);      // [G*A] (SORT)
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(perm + G * A);       // [groups][16] (SORT); G*A*2 is even
-    uint32_t* cursor = cnt + 16 * encoded_sort_groups(A, G, SPAN);
-    const uint64_t o0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + w) * G;
+    // wave-private LDS: 64 object bases {value, key}, the code table, descriptors
+    uint8_t* wsmem = smem_raw + (size_t)w * encoded_lds_per_wave(A);
+    uint64_t* bases = reinterpret_cast<uint64_t*>(wsmem);           // [64][2]
+    uint8_t* codes = wsmem + 64 * 16;                                // [256]
+    EncDesc* desc = reinterpret_cast<EncDesc*>(wsmem + 64 * 16 + 256);
+    const uint64_t o0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + w) * 64;
     if (o0 >= a.n) return;  // no workgroup barrier: waves are independent
-    const uint32_t nobj = (uint32_t)min<uint64_t>(G, a.n - o0);
+    const uint32_t nobj = (uint32_t)min<uint64_t>(64, a.n - o0);
     const bool valid = (uint32_t)lane < nobj;
     const uint64_t i = o0 + (valid ? lane : 0);
 
     const uint64_t voff = valid ? a.val_off[i] : 0, koff = valid ? a.key_off[i] : 0;
     const uint32_t vlen = valid ? a.val_len[i] : 0u, klen = valid ? a.key_len[i] : 0u;
     const uint8_t* v = a.vals + voff;
-    if (lane < G) {
-        bases[2 * lane] = voff;
-        bases[2 * lane + 1] = koff;
-    }
+    bases[2 * lane] = voff;
+    bases[2 * lane + 1] = koff;
     for (uint32_t j = lane; j < A; j += 64) codes[j] = a.codes[j];
 
     // phase 0: pull the value's lines toward L2 (independent loads, consumed late)
@@ -136,53 +120,7 @@ hash_encoded_kernel(const EncodedArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
     const uint32_t nslots = nobj * A;
-    if constexpr (SORT) {
-        // counting sort of the slots by work class within each group of
-        // GS = SPAN * 64 slots: counts, exclusive scan into cursors, then one
-        // fetch-add per slot for its position
-        constexpr uint32_t GS = SPAN ? SPAN * 64 : G * 256;  // (no group boundary when SPAN = 0)
-        const uint32_t ngroups = (nslots + GS - 1) / GS;     // <= kMaxGroups
-        for (uint32_t x = lane; x < ngroups * 16; x += 64) cnt[x] = 0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        auto class_of = [&](uint32_t s) {
-            const uint32_t j = s - (s / A) * A;
-            const EncDesc d = desc[s];
-            return d.off == kZeroSlot ? 0u : work_class10(codes[j], d.len);
-        };
-        for (uint32_t s = lane; s < nslots; s += 64)
-            __hip_atomic_fetch_add(&cnt[(s / GS) * 16 + class_of(s)], 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WAVEFRONT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t g0 = 0; g0 < ngroups; g0 += 4) {  // 4 groups of 16 counters per wave op
-            const uint32_t g = g0 + (uint32_t)(lane >> 4);
-            const uint32_t c = g < ngroups ? cnt[g * 16 + (lane & 15)] : 0u;
-            // exclusive scan within each 16-lane row (row_shr DPP steps)
-            uint32_t v = c;
-            v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);
-            v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true);
-            v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true);
-            v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true);
-            if (g < ngroups) cursor[g * 16 + (lane & 15)] = g * GS + v - c;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        for (uint32_t s = lane; s < nslots; s += 64) {
-            const uint32_t p = __hip_atomic_fetch_add(&cursor[(s / GS) * 16 + class_of(s)], 1u, __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_WAVEFRONT);
-            perm[p] = (uint16_t)s;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-
-    // phase 2: passes of 64 slots (slot s = object * A + attribute; in class
-    // order when sorting).  The object's bases and the attribute's code are
+    // phase 2: passes of 64 slots (slot s = object * A + attribute).  The object's bases and the attribute's code are
     // read from LDS, not from other lanes: in a partial pass the lanes past the
     // batch end are inactive, and a ds_bpermute from an inactive lane returns 0.
     const uint32_t npass = SHAPE == 1 ? 0 : (nslots + 63) / 64;
@@ -198,7 +136,7 @@ hash_encoded_kernel(const EncodedArgs a) {
     };
     auto load_pass = [&](uint32_t t, Pass& P) {
         const uint32_t q = t * 64 + (uint32_t)lane;
-        const uint32_t s = SORT ? (q < nslots ? (uint32_t)perm[q] : nslots - 1) : min(q, nslots - 1);
+        const uint32_t s = min(q, nslots - 1);
         const uint32_t obj = s / A, j = s - obj * A;
         const EncDesc d = desc[s];
         const uint64_t base = bases[2 * obj + (j == 0)];
@@ -232,117 +170,16 @@ hash_encoded_kernel(const EncodedArgs a) {
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <bool TOUCH, bool A4, int G, bool SORT, int SPAN = 0, int SHAPE = 0>
+template <bool TOUCH, bool A4, int SHAPE = 0>
 static hipError_t launch_encoded(const EncodedArgs& a, hipStream_t stream) {
-    // 4 waves per workgroup while they fit in 64 KiB of LDS, else 1
-    const size_t per_wave = encoded_lds_per_wave(a.A, G, SORT, SPAN);
+    // 4 waves per workgroup while they fit in 64 KiB of LDS (A <= 28), else 1
+    const size_t per_wave = encoded_lds_per_wave(a.A);
     const uint32_t waves_per_block = 4 * per_wave <= 65536 ? 4 : 1;
-    const uint64_t waves = (a.n + G - 1) / G;
+    const uint64_t waves = (a.n + 63) / 64;
     const uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_encoded_kernel<TOUCH, A4, G, SORT, SPAN, SHAPE>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
+    hipLaunchKernelGGL((hash_encoded_kernel<TOUCH, A4, SHAPE>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
                        waves_per_block * per_wave, stream, a);
-    return hipGetLastError();
-}
-
-// ===========================================================================
-// Walk-and-hash form (variants 60/61): one lane per stored object decodes its
-// value prefix by prefix and hashes each attribute as soon as its length is
-// known, so the bytes the walk brings in are hashed while their lines are
-// still in cache — every value byte crosses HBM once (the two-phase kernel
-// above walks all 64 objects of a wave first, and its lines are evicted before
-// the hash passes re-read them: 2x the traffic, SHAPE probes 57/58).  All
-// loads are dword-aligned (A4).  A wave's lanes hash the same attribute of 64
-// objects, so numeric and fixed-size steps are uniform; the string steps run
-// the union of the regimes their lengths take.
-// COALESCE: coordinates are collected in LDS and stored coalesced per wave.
-// ===========================================================================
-// 4 bytes at p, any alignment, through the dwords holding its first and last byte.
-__device__ __forceinline__ uint32_t load4_a4(const uint8_t* p) {
-    const uint32_t r = (uint32_t)(uintptr_t)p & 3;
-    const uint32_t d0 = gld4(dw_floor(p)), d1 = gld4(dw_floor(p + 3));
-    return __builtin_amdgcn_alignbyte(d1, d0, r);
-}
-
-template <bool COALESCE>
-__global__ void __launch_bounds__(256)
-hash_encoded_lpo_kernel(const EncodedArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t coord_smem[];
-    const uint32_t A = a.A;
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t wave0 = i - (threadIdx.x & 63);  // first object of this wave
-    if (wave0 >= a.n) return;
-    const bool valid = i < a.n;
-    const int lane = threadIdx.x & 63;
-    uint64_t* wout = COALESCE ? coord_smem + (size_t)(threadIdx.x >> 6) * 64 * A : nullptr;
-    auto put = [&](uint32_t j, uint64_t h) {
-        if (COALESCE) wout[(size_t)lane * A + j] = h;
-        else if (valid) __builtin_nontemporal_store(h, a.coords + i * A + j);
-    };
-    const uint64_t voff = valid ? a.val_off[i] : 0, koff = valid ? a.key_off[i] : 0;
-    const uint32_t vlen = valid ? a.val_len[i] : 0u, klen = valid ? a.key_len[i] : 0u;
-    const uint8_t* v = a.vals + voff;
-    bool bad = false;
-    // header: [u64 BE version][u16 BE count] (datalayer_encodings.cc:168-180)
-    bool ok = valid && vlen >= 10;
-    uint64_t version = 0;
-    if (ok) {
-        const uint32_t hi = load4_a4(v), lo = load4_a4(v + 4);
-        version = ((uint64_t)__builtin_bswap32(hi) << 32) | __builtin_bswap32(lo);
-        const uint32_t c = load4_a4(v + 6);  // bytes 6..9: count in the top half
-        ok = (__builtin_bswap32(c) & 0xffffu) == A - 1;
-    }
-    // attribute 0: the key
-    {
-        const uint32_t code = ok ? (uint32_t)a.codes[0] : (uint32_t)CODE_ZERO;
-        const uint8_t* p = ok ? a.keys + koff : g_zero_pad;
-        const uint32_t n = ok ? klen : 0u;
-        const Raw r = issue_block_a4(code, p, n);
-        put(0, hash_blk<false, false, true>(code, p, n, funnel_raw(r), bad));
-    }
-    // attributes 1..A-1: prefix, then the attribute (decode_value :181-213)
-    uint32_t pos = 10;
-    for (uint32_t k = 1; k < A; ++k) {
-        uint32_t len = 0;
-        if (ok) {
-            if (vlen - pos < 4) {
-                ok = false;
-            } else {
-                len = __builtin_bswap32(load4_a4(v + pos));
-                pos += 4;
-                if (len > vlen - pos) ok = false;  // the reference does not check this (:201-213)
-            }
-        }
-        const uint32_t code = ok ? (uint32_t)a.codes[k] : (uint32_t)CODE_ZERO;
-        const uint8_t* p = ok ? v + pos : g_zero_pad;
-        const uint32_t n = ok ? len : 0u;
-        const Raw r = issue_block_a4(code, p, n);
-        put(k, hash_blk<false, false, true>(code, p, n, funnel_raw(r), bad));
-        if (ok) pos += len;
-    }
-    if (valid && !ok)  // undecodable: every coordinate of the object is 0
-        for (uint32_t j = 0; j < A; ++j) put(j, 0);
-    if (valid && a.versions) a.versions[i] = ok ? version : 0;
-    if (COALESCE) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t nobj = (uint32_t)min<uint64_t>(64, a.n - wave0);
-        uint64_t* out = a.coords + wave0 * A;
-        for (uint32_t s = lane; s < nobj * A; s += 64) __builtin_nontemporal_store(wout[s], out + s);
-    }
-    if (a.status && valid && !ok) atomicOr(a.status, 1u << 6 /* HDX_E_BADENC */);
-    if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
-}
-
-template <bool COALESCE>
-static hipError_t launch_encoded_lpo(const EncodedArgs& a, hipStream_t stream) {
-    const uint32_t waves_per_block = COALESCE && 4 * 64 * 8 * (size_t)a.A > 65536 ? 1 : 4;
-    const uint64_t blocks = (a.n + 64 * waves_per_block - 1) / (64 * waves_per_block);
-    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    const size_t lds = COALESCE ? (size_t)waves_per_block * 64 * 8 * a.A : 0;
-    hipLaunchKernelGGL((hash_encoded_lpo_kernel<COALESCE>), dim3((uint32_t)blocks), dim3(64 * waves_per_block), lds,
-                       stream, a);
     return hipGetLastError();
 }
 
@@ -350,22 +187,16 @@ hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
     // default: dword-aligned loads (5.49 vs 6.14 ms per 10 M config-3b objects,
     // profiles/r1/ab_a4_cfg5.jsonl); variant 43 = byte-addressed loads, variant
-    // 33 adds the phase-0 line touch to those (measured 11 % slower, r1u);
-    // 47-49: the class-sorted passes with 64 / 32 / 16 objects per wave
+    // 33 adds the phase-0 line touch to those (measured 11 % slower, r1u).
+    // Retired (profiles/r1/ab_cfg5_*.jsonl): class-sorted passes over the whole
+    // wave or over groups of 2 / 4 passes, 16 / 32 objects per wave, and a
+    // lane-per-object walk-and-hash kernel — all slower
     switch (hash_variant()) {
-        case 43: return launch_encoded<false, false, 64, false>(a, stream);
-        case 33: return launch_encoded<true, false, 64, false>(a, stream);
-        case 47: return launch_encoded<false, true, 64, true>(a, stream);
-        case 48: return launch_encoded<false, true, 32, true>(a, stream);
-        case 49: return launch_encoded<false, true, 16, true>(a, stream);
-        case 54: return launch_encoded<false, true, 64, true, 2>(a, stream);
-        case 55: return launch_encoded<false, true, 64, true, 4>(a, stream);
-        case 56: return launch_encoded<false, true, 32, true, 2>(a, stream);
-        case 57: return launch_encoded<false, true, 64, false, 0, 1>(a, stream);
-        case 58: return launch_encoded<false, true, 64, false, 0, 2>(a, stream);
-        case 60: return launch_encoded_lpo<false>(a, stream);
-        case 61: return launch_encoded_lpo<true>(a, stream);
-        default: return launch_encoded<false, true, 64, false>(a, stream);
+        case 43: return launch_encoded<false, false>(a, stream);
+        case 33: return launch_encoded<true, false>(a, stream);
+        case 57: return launch_encoded<false, true, 1>(a, stream);  // debug shape: the walk alone
+        case 58: return launch_encoded<false, true, 2>(a, stream);  // debug shape: phase 2 loads only
+        default: return launch_encoded<false, true>(a, stream);
     }
 }
 

@@ -36,12 +36,9 @@ struct BatchArgs {
 hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream);
 // Fills args.uniform_code from args.codes[0..A).
 void finalize_args(BatchArgs& args);
-// Kernel variants (hdx_kernels.hip): 0 plain, 1 +length prefetch, 2 +obj_base in
-// registers, 3 +string-block prefetch, 4 = 3 without length prefetch, 5/6 = 2/3 with
-// non-temporal coordinate stores.
+// Kernel variants (hdx_kernels.hip, variant_kernel_name): the automatic policy's
+// choices and the alternatives scripts/ab_variants.py times against them.
 hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, int variant);
-// The workgroup-window kernel (hdx_window.hip), variants 50 / 51.
-hipError_t launch_hash_window(const BatchArgs& args, hipStream_t stream, int variant);
 // The variant launch_hash_batch uses: HDX_KERNEL_VARIANT (tuning knob) or the default.
 int hash_variant();
 int set_hash_variant(int v);  // -2 if unknown, else the previous selection (-1 = auto)

@@ -10,16 +10,16 @@
 //                         LDS, optionally counting-sorted by work class so a
 //                         wave's lanes run the same CityHash regime.
 // launch_hash_batch picks one per schema and size (auto_variant).  Variant ids
-// are those of the round-1 A/B logs (profiles/r1/ab_variants_*.jsonl); the ids
-// of retired experiments (0-11, 13-17: a rounds-per-wave kernel with and
-// without software pipelining, non-temporal loads, a workgroup-barrier sort,
-// early touching of long strings) are no longer built; their results are in
-// DESIGN.md §4.
+// are those of the round-1 A/B logs (profiles/r1/ab_*.jsonl); the ids of
+// retired experiments (0-11, 13-17, 22-24, 27-29, 32-34, 36, 38, 39, 44-46,
+// 50-53, 59: rounds-per-wave kernels, non-temporal loads, workgroup-barrier
+// sorts, LDS-staged blocks, larger sort windows, occupancy caps, workgroup LDS
+// windows with and without pipelining) are no longer built; their results are
+// in DESIGN.md §4 and the logs.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
 
-#include <type_traits>
 
 #include "hdx_device_hash.h"
 #include "hdx_internal.h"
@@ -111,8 +111,8 @@ __device__ __forceinline__ uint32_t work_class(uint32_t code, uint32_t n, bool v
 
 
 // ===========================================================================
-// Regroup kernel (variants 18-22: 18/19 sorted with C = 4/8; 20/21/22 unsorted,
-// C = 8/4/16): a wave owns C consecutive chunks (C*64
+// Regroup kernel (variants 18/19/26/35/37 sorted with C = 4/8/2/2/2; 20/21/25
+// unsorted with C = 8/4/16): a wave owns C consecutive chunks (C*64
 // slots).  Phase 1 computes every slot's {pointer, length, code} as the chunk
 // kernel does (all C length loads issued at once; the carry chains from chunk
 // to chunk in registers) and writes a 16-byte descriptor per slot into the
@@ -129,22 +129,13 @@ struct RegroupLds {
     SlotDesc desc[4][C * 64];   // reused for the coordinates in phase 2
     uint16_t perm[4][C * 64];
 };
-// STAGE: each slot's four 16-byte pieces (Blk) are loaded in slot order in
-// phase 1 and parked in LDS, so the class-sorted passes read them from LDS
-// instead of gathering from global memory out of order.
-template <int C>
-struct RegroupStageLds {
-    SlotDesc desc[4][C * 64];
-    uint16_t perm[4][C * 64];
-    Blk blk[4][C * 64];
-};
 
-template <int C, bool NT_STORE, bool SORT = true, bool DIRECT = true, bool STAGE = false, bool A4 = false,
-          bool PIPE = false, int WPE = 8>
+// A4: dword-aligned loads (hdx_loads.h); PIPE: the > 64-byte loop keeps the
+// next block in flight.
+template <int C, bool NT_STORE, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false>
 __global__ void __launch_bounds__(256)
 hash_regroup_kernel(const BatchArgs args) {
-    typedef typename std::conditional<STAGE, RegroupStageLds<C>, RegroupLds<C>>::type Lds;
-    __shared__ Lds lds;
+    __shared__ RegroupLds<C> lds;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     SlotDesc* desc = lds.desc[w];
@@ -175,11 +166,6 @@ hash_regroup_kernel(const BatchArgs args) {
 
     // ---- phase 1: descriptors + classes -------------------------------------
     uint32_t cls[C];
-    Blk staged[STAGE ? C : 1];
-    auto lds_blk = [&](uint32_t s) -> Blk& {
-        if constexpr (STAGE) return lds.blk[w][s];
-        else return staged[0];
-    };
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const uint32_t t = j0 + (uint32_t)(c * 64 + lane);
@@ -204,11 +190,6 @@ hash_regroup_kernel(const BatchArgs args) {
         d.code_slot = code | ((uint32_t)(c * 64 + lane) << 8);
         desc[c * 64 + lane] = d;
         cls[c] = work_class(code, L, valid);
-        if constexpr (STAGE) staged[c] = issue_block(code, d.p, L);
-    }
-    if constexpr (STAGE) {
-#pragma unroll
-        for (int c = 0; c < C; ++c) lds_blk(c * 64 + lane) = staged[c];
     }
 
     // ---- counting sort by class (wave-local) ---------------------------------
@@ -247,8 +228,7 @@ hash_regroup_kernel(const BatchArgs args) {
     auto load_pass = [&](int t, Pass& P) {
         const uint32_t s = uniform ? (uint32_t)(t * 64 + lane) : perm[t * 64 + lane];
         P.d = desc[s];
-        if constexpr (STAGE) P.blk.b = lds_blk(s);
-        else P.blk = issue_any<A4>(P.d.code_slot & 0xffu, P.d.p, P.d.n);
+        P.blk = issue_any<A4>(P.d.code_slot & 0xffu, P.d.p, P.d.n);
     };
     bool bad = false;
     Pass P0, P1;
@@ -258,8 +238,8 @@ hash_regroup_kernel(const BatchArgs args) {
         Pass& cur = (t & 1) ? P1 : P0;
         Pass& nxt = (t & 1) ? P0 : P1;
         if (t + 1 < C) load_pass(t + 1, nxt);
-        const uint64_t h = hash_blk<PIPE, false, A4 && !STAGE>(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n,
-                                                                STAGE ? cur.blk.b : consume_any<A4>(cur.blk), bad);
+        const uint64_t h = hash_blk<PIPE, false, A4>(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n,
+                                                     consume_any<A4>(cur.blk), bad);
         if (DIRECT && uniform) {  // pass t is chunk t in slot order: store straight to HBM
             const uint64_t q = qw + t * 64 + lane;
             if (q < nslots) {
@@ -291,19 +271,14 @@ hash_regroup_kernel(const BatchArgs args) {
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <int C, bool NT, bool SORT = true, bool DIRECT = true, bool STAGE = false, bool A4 = false,
-          bool PIPE = false, int WPE = 8>
+template <int C, bool NT, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false>
 static hipError_t launch_regroup(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    // WPE < 8 (A/B only): pad the workgroup's LDS so that at most WPE
-    // workgroups (= waves per SIMD) fit on a CU
-    typedef typename std::conditional<STAGE, RegroupStageLds<C>, RegroupLds<C>>::type Lds;
-    const size_t pad = WPE < 8 ? 163840 / WPE - sizeof(Lds) - 1024 : 0;
-    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT, DIRECT, STAGE, A4, PIPE, WPE>), dim3((uint32_t)blocks), dim3(256),
-                       pad, stream, args);
+    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT, DIRECT, A4, PIPE>), dim3((uint32_t)blocks), dim3(256), 0,
+                       stream, args);
     return hipGetLastError();
 }
 
@@ -324,41 +299,31 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 19: return launch_regroup<8, true>(args, stream);
         case 20: return launch_regroup<8, true, false>(args, stream);
         case 21: return launch_regroup<4, true, false>(args, stream);
-        case 22: return launch_regroup<16, true, false>(args, stream);
-        case 23: return launch_regroup<8, true, false, false>(args, stream);
-        case 24: return launch_regroup<4, true, false, false>(args, stream);
         case 25: return launch_regroup<16, true, false, false>(args, stream);
         case 26: return launch_regroup<2, true>(args, stream);
-        case 27: return launch_regroup<2, true, false>(args, stream);
-        case 28: return launch_regroup<2, true, true, true, true>(args, stream);
-        case 29: return launch_regroup<4, true, true, true, true>(args, stream);
         case 30: return launch_chunk<true, true>(args, stream);
         case 31: return launch_chunk<true, false, 0, true>(args, stream);
-        case 32: return launch_regroup<4, true, false, true, false, true>(args, stream);
-        case 34: return launch_regroup<8, true, true, true, false, true>(args, stream);
-        case 35: return launch_regroup<2, true, true, true, false, true>(args, stream);
-        case 36: return launch_regroup<4, true, true, true, false, true>(args, stream);
-        case 37: return launch_regroup<2, true, true, true, false, true, true>(args, stream);
-        case 38: return launch_regroup<3, true, true, true, false, true>(args, stream);
-        case 39: return launch_regroup<2, true, true, false, false, true>(args, stream);
-        case 44: return launch_regroup<2, true, true, true, false, true, false, 5>(args, stream);
-        case 45: return launch_regroup<2, true, true, true, false, true, false, 4>(args, stream);
-        case 46: return launch_regroup<2, true, true, true, false, true, false, 3>(args, stream);
-        case 50:
-        case 51:
-        case 52:
-        case 53:
-        case 59: return launch_hash_window(args, stream, variant);
-        case 40: return launch_chunk<true, false, 1>(args, stream);
-        case 41: return launch_chunk<true, false, 2>(args, stream);
+        case 35: return launch_regroup<2, true, true, true, true>(args, stream);
+        case 37: return launch_regroup<2, true, true, true, true, true>(args, stream);
+        case 40: return launch_chunk<true, false, 1>(args, stream);  // debug shape: loads only
+        case 41: return launch_chunk<true, false, 2>(args, stream);  // debug shape: arithmetic only
         default: return hipErrorInvalidValue;
     }
 }
 
 static constexpr int kDefaultVariant = -1;  // automatic
 // 33 / 43 select the stored-object sweep's line-touch and byte-addressed forms,
-// 47-49 and 54-56 its class-sorted forms (hdx_encoded.hip).
-static bool known_variant(int v) { return v == -1 || v == 12 || (v >= 18 && v <= 49) || (v >= 50 && v <= 61); }
+// 57 / 58 its walk-only and loads-only shapes (hdx_encoded.hip).
+static bool known_variant(int v) {
+    switch (v) {
+        case -1: case 12: case 18: case 19: case 20: case 21: case 25: case 26: case 30: case 31: case 35: case 37:
+        case 40: case 41:
+        case 33: case 43: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
+            return true;
+        default:
+            return false;
+    }
+}
 
 static int g_variant = [] {
     const char* e = getenv("HDX_KERNEL_VARIANT");
@@ -428,29 +393,14 @@ const char* variant_kernel_name(int v) {
         case 12: return "void hdx::hash_chunk_kernel<true, false, 0, false>(hdx::BatchArgs)";
         case 30: return "void hdx::hash_chunk_kernel<true, true, 0, false>(hdx::BatchArgs)";
         case 31: return "void hdx::hash_chunk_kernel<true, false, 0, true>(hdx::BatchArgs)";
-        case 32: return "void hdx::hash_regroup_kernel<4, true, false, true, false, true, false, 8>(hdx::BatchArgs)";
-        case 34: return "void hdx::hash_regroup_kernel<8, true, true, true, false, true, false, 8>(hdx::BatchArgs)";
-        case 35: return "void hdx::hash_regroup_kernel<2, true, true, true, false, true, false, 8>(hdx::BatchArgs)";
-        case 50: return "void hdx::hash_window_kernel<256, 20480, false>(hdx::BatchArgs)";
-        case 51: return "void hdx::hash_window_kernel<512, 35840, false>(hdx::BatchArgs)";
-        case 52: return "void hdx::hash_window_pipe_kernel<17920>(hdx::BatchArgs, unsigned long)";
-        case 53: return "void hdx::hash_window_pipe_kernel<24576>(hdx::BatchArgs, unsigned long)";
-        case 36: return "void hdx::hash_regroup_kernel<4, true, true, true, false, true, false, 8>(hdx::BatchArgs)";
-        case 37: return "void hdx::hash_regroup_kernel<2, true, true, true, false, true, true, 8>(hdx::BatchArgs)";
-        case 38: return "void hdx::hash_regroup_kernel<3, true, true, true, false, true, false, 8>(hdx::BatchArgs)";
-        case 39: return "void hdx::hash_regroup_kernel<2, true, true, false, false, true, false, 8>(hdx::BatchArgs)";
-        case 18: return "void hdx::hash_regroup_kernel<4, true, true, true, false, false, false, 8>(hdx::BatchArgs)";
-        case 19: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, false, 8>(hdx::BatchArgs)";
-        case 20: return "void hdx::hash_regroup_kernel<8, true, false, true, false, false, false, 8>(hdx::BatchArgs)";
-        case 21: return "void hdx::hash_regroup_kernel<4, true, false, true, false, false, false, 8>(hdx::BatchArgs)";
-        case 22: return "void hdx::hash_regroup_kernel<16, true, false, true, false, false, false, 8>(hdx::BatchArgs)";
-        case 23: return "void hdx::hash_regroup_kernel<8, true, false, false, false, false, false, 8>(hdx::BatchArgs)";
-        case 24: return "void hdx::hash_regroup_kernel<4, true, false, false, false, false, false, 8>(hdx::BatchArgs)";
-        case 25: return "void hdx::hash_regroup_kernel<16, true, false, false, false, false, false, 8>(hdx::BatchArgs)";
-        case 26: return "void hdx::hash_regroup_kernel<2, true, true, true, false, false, false, 8>(hdx::BatchArgs)";
-        case 27: return "void hdx::hash_regroup_kernel<2, true, false, true, false, false, false, 8>(hdx::BatchArgs)";
-        case 28: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, false, 8>(hdx::BatchArgs)";
-        case 29: return "void hdx::hash_regroup_kernel<4, true, true, true, true, false, false, 8>(hdx::BatchArgs)";
+        case 18: return "void hdx::hash_regroup_kernel<4, true, true, true, false, false>(hdx::BatchArgs)";
+        case 19: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false>(hdx::BatchArgs)";
+        case 20: return "void hdx::hash_regroup_kernel<8, true, false, true, false, false>(hdx::BatchArgs)";
+        case 21: return "void hdx::hash_regroup_kernel<4, true, false, true, false, false>(hdx::BatchArgs)";
+        case 25: return "void hdx::hash_regroup_kernel<16, true, false, false, false, false>(hdx::BatchArgs)";
+        case 26: return "void hdx::hash_regroup_kernel<2, true, true, true, false, false>(hdx::BatchArgs)";
+        case 35: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false>(hdx::BatchArgs)";
+        case 37: return "void hdx::hash_regroup_kernel<2, true, true, true, true, true>(hdx::BatchArgs)";
         default: return "";
     }
 }

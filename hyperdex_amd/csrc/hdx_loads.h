@@ -402,24 +402,6 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
     return v;
 }
 
-// Work classes for class-sorted passes: one per code path, so a pass holds as
-// few CityHash regimes as the slot mix allows (0: int64 / not hashable / past
-// the batch end, 1: float, 2: timestamp, 3: string <= 16 B, 4: 17..32,
-// 5: 33..64, 6..9: > 64 B with 1, 2, 3, >= 4 loop blocks).
-constexpr int kClasses10 = 10;
-__device__ __forceinline__ uint32_t work_class10(uint32_t code, uint32_t n) {
-    if (code == CODE_STRING) {
-        if (n <= 16) return 3;
-        if (n <= 32) return 4;
-        if (n <= 64) return 5;
-        const uint32_t b = (n - 1) >> 6;  // > 64-byte loop blocks
-        return b >= 4 ? 9u : 5u + b;
-    }
-    if (code == CODE_FLOAT) return 1;
-    if (code >= CODE_TS_SECOND) return 2;
-    return 0;
-}
-
 // Wave-uniform slot -> (object, attribute) split without a 64-bit integer
 // divide: q < 2^53, so the f64 quotient is off by at most one; fix it up.
 __device__ __forceinline__ void split_slot(uint64_t q, uint32_t A, uint64_t& i0, uint32_t& j0) {
