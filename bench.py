@@ -166,7 +166,7 @@ def main():
     }
 
     if cfg == "cfg5":
-        result["roofline"]["kernel"] = "void hdx::hash_encoded_kernel<false, true, 0>(hdx::EncodedArgs)"
+        result["roofline"]["kernel"] = "void hdx::hash_encoded_kernel<false, true, 0, 32>(hdx::EncodedArgs)"
     if world > 1 and not args.no_allgather:
         result["allgather"] = time_allgather(coords, world, dev, backend, max_over_ranks)
     if not args.no_regions:

@@ -50,36 +50,39 @@ struct alignas(8) EncDesc {
 };
 constexpr uint32_t kZeroSlot = 0xffffffffu;
 
-// Wave-private LDS: 64 object bases {value, key}, the code table, descriptors.
-__host__ __device__ constexpr size_t encoded_lds_per_wave(uint32_t A) {
-    return 64 * 16 + 256 + (size_t)64 * A * sizeof(EncDesc);
+// Wave-private LDS: G object bases {value, key}, the code table, descriptors.
+__host__ __device__ constexpr size_t encoded_lds_per_wave(uint32_t A, uint32_t G = 64) {
+    return G * 16 + 256 + (size_t)G * A * sizeof(EncDesc);
 }
 
-// SHAPE (debug variants 57/58 only, wrong coordinates): 1 = the walk alone
-// (no phase 2), 2 = phase 2's loads without the hash arithmetic.
-template <bool TOUCH, bool A4 = false, int SHAPE = 0>
+// G objects per wave (lanes G..63 idle in phase 1).  SHAPE (debug variants
+// 57/58 only, wrong coordinates): 1 = the walk alone (no phase 2), 2 = phase
+// 2's loads without the hash arithmetic.
+template <bool TOUCH, bool A4 = false, int SHAPE = 0, int G = 64>
 __global__ void __launch_bounds__(256)
 hash_encoded_kernel(const EncodedArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     const uint32_t A = a.A;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    // wave-private LDS: 64 object bases {value, key}, the code table, descriptors
-    uint8_t* wsmem = smem_raw + (size_t)w * encoded_lds_per_wave(A);
-    uint64_t* bases = reinterpret_cast<uint64_t*>(wsmem);           // [64][2]
-    uint8_t* codes = wsmem + 64 * 16;                                // [256]
-    EncDesc* desc = reinterpret_cast<EncDesc*>(wsmem + 64 * 16 + 256);
-    const uint64_t o0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + w) * 64;
+    // wave-private LDS: G object bases {value, key}, the code table, descriptors
+    uint8_t* wsmem = smem_raw + (size_t)w * encoded_lds_per_wave(A, G);
+    uint64_t* bases = reinterpret_cast<uint64_t*>(wsmem);           // [G][2]
+    uint8_t* codes = wsmem + G * 16;                                 // [256]
+    EncDesc* desc = reinterpret_cast<EncDesc*>(wsmem + G * 16 + 256);
+    const uint64_t o0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + w) * G;
     if (o0 >= a.n) return;  // no workgroup barrier: waves are independent
-    const uint32_t nobj = (uint32_t)min<uint64_t>(64, a.n - o0);
+    const uint32_t nobj = (uint32_t)min<uint64_t>(G, a.n - o0);
     const bool valid = (uint32_t)lane < nobj;
     const uint64_t i = o0 + (valid ? lane : 0);
 
     const uint64_t voff = valid ? a.val_off[i] : 0, koff = valid ? a.key_off[i] : 0;
     const uint32_t vlen = valid ? a.val_len[i] : 0u, klen = valid ? a.key_len[i] : 0u;
     const uint8_t* v = a.vals + voff;
-    bases[2 * lane] = voff;
-    bases[2 * lane + 1] = koff;
+    if (lane < G) {
+        bases[2 * lane] = voff;
+        bases[2 * lane + 1] = koff;
+    }
     for (uint32_t j = lane; j < A; j += 64) codes[j] = a.codes[j];
 
     // phase 0: pull the value's lines toward L2 (independent loads, consumed late)
@@ -170,15 +173,15 @@ hash_encoded_kernel(const EncodedArgs a) {
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <bool TOUCH, bool A4, int SHAPE = 0>
+template <bool TOUCH, bool A4, int SHAPE = 0, int G = 64>
 static hipError_t launch_encoded(const EncodedArgs& a, hipStream_t stream) {
-    // 4 waves per workgroup while they fit in 64 KiB of LDS (A <= 28), else 1
-    const size_t per_wave = encoded_lds_per_wave(a.A);
+    // 4 waves per workgroup while they fit in 64 KiB of LDS (A <= 28 at G = 64), else 1
+    const size_t per_wave = encoded_lds_per_wave(a.A, G);
     const uint32_t waves_per_block = 4 * per_wave <= 65536 ? 4 : 1;
-    const uint64_t waves = (a.n + 63) / 64;
+    const uint64_t waves = (a.n + G - 1) / G;
     const uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_encoded_kernel<TOUCH, A4, SHAPE>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
+    hipLaunchKernelGGL((hash_encoded_kernel<TOUCH, A4, SHAPE, G>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
                        waves_per_block * per_wave, stream, a);
     return hipGetLastError();
 }
@@ -186,8 +189,10 @@ static hipError_t launch_encoded(const EncodedArgs& a, hipStream_t stream) {
 hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
     // default: dword-aligned loads (5.49 vs 6.14 ms per 10 M config-3b objects,
-    // profiles/r1/ab_a4_cfg5.jsonl); variant 43 = byte-addressed loads, variant
-    // 33 adds the phase-0 line touch to those (measured 11 % slower, r1u).
+    // profiles/r1/ab_a4_cfg5.jsonl), 32 objects per wave (5.05 vs 5.31 ms for
+    // 64 (variant 47) and 5.88 for 16 (48), ab_cfg5_objects_per_wave.jsonl);
+    // variant 43 = byte-addressed loads, 64 objects per wave, variant 33 adds
+    // the phase-0 line touch to those (measured 11 % slower, r1u).
     // Retired (profiles/r1/ab_cfg5_*.jsonl): class-sorted passes over the whole
     // wave or over groups of 2 / 4 passes, 16 / 32 objects per wave, and a
     // lane-per-object walk-and-hash kernel — all slower
@@ -196,7 +201,9 @@ hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream) {
         case 33: return launch_encoded<true, false>(a, stream);
         case 57: return launch_encoded<false, true, 1>(a, stream);  // debug shape: the walk alone
         case 58: return launch_encoded<false, true, 2>(a, stream);  // debug shape: phase 2 loads only
-        default: return launch_encoded<false, true>(a, stream);
+        case 47: return launch_encoded<false, true, 0, 64>(a, stream);
+        case 48: return launch_encoded<false, true, 0, 16>(a, stream);
+        default: return launch_encoded<false, true, 0, 32>(a, stream);
     }
 }
 

@@ -318,7 +318,7 @@ static bool known_variant(int v) {
     switch (v) {
         case -1: case 12: case 18: case 19: case 20: case 21: case 25: case 26: case 30: case 31: case 35: case 37:
         case 40: case 41:
-        case 33: case 43: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
+        case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;
         default:
             return false;

@@ -136,7 +136,7 @@ def test_gpu_encoded_partial_last_pass(oracle, A, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [-1, 33, 43])
+@pytest.mark.parametrize("variant", [-1, 33, 43, 47, 48])
 def test_gpu_encoded_every_variant(oracle, variant):
     """Every stored-object sweep kernel (hdx_encoded.hip; 33 adds the line
     touch) is bit-exact on every config, on corrupt values, on ragged object
