@@ -128,11 +128,14 @@ template <int C>
 struct RegroupLds {
     SlotDesc desc[4][C * 64];   // reused for the coordinates in phase 2
     uint16_t perm[4][C * 64];
+    uint32_t cnt[4][kClasses];  // ASORT: per-class counters / cursors
 };
 
 // A4: dword-aligned loads (hdx_loads.h); PIPE: the > 64-byte loop keeps the
-// next block in flight.
-template <int C, bool NT_STORE, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false>
+// next block in flight; ASORT: the class sort by LDS fetch-add instead of
+// ballot / mbcnt per (class, chunk).
+template <int C, bool NT_STORE, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false,
+          bool ASORT = false>
 __global__ void __launch_bounds__(256)
 hash_regroup_kernel(const BatchArgs args) {
     __shared__ RegroupLds<C> lds;
@@ -199,18 +202,37 @@ hash_regroup_kernel(const BatchArgs args) {
     for (int c = 0; c < C; ++c) uniform &= __all(cls[c] == c00);
     if (!SORT) uniform = true;
     if (!uniform) {
-        uint32_t before = 0;  // slots of lower classes, then of this class in lower chunks
+        if constexpr (ASORT) {
+            // LDS fetch-add counting sort: per-class counts, an exclusive scan
+            // into cursors (lane k holds class k), one fetch-add per slot
+            uint32_t* cnt = lds.cnt[w];
+            if (lane < kClasses) cnt[lane] = 0;
 #pragma unroll
-        for (int k = 0; k < kClasses; ++k) {
+            for (int c = 0; c < C; ++c)
+                __hip_atomic_fetch_add(&cnt[cls[c]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            const uint32_t k = lane < kClasses ? cnt[lane] : 0u;
+            const uint32_t start = wave_scan_dpp(k) - k;
+            if (lane < kClasses) cnt[lane] = start;
 #pragma unroll
             for (int c = 0; c < C; ++c) {
-                const uint64_t m = __ballot(cls[c] == (uint32_t)k);
-                if (cls[c] == (uint32_t)k) {
-                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    perm[before + rank] = (uint16_t)(c * 64 + lane);
+                const uint32_t pos = __hip_atomic_fetch_add(&cnt[cls[c]], 1u, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_WAVEFRONT);
+                perm[pos] = (uint16_t)(c * 64 + lane);
+            }
+        } else {
+            uint32_t before = 0;  // slots of lower classes, then of this class in lower chunks
+#pragma unroll
+            for (int k = 0; k < kClasses; ++k) {
+#pragma unroll
+                for (int c = 0; c < C; ++c) {
+                    const uint64_t m = __ballot(cls[c] == (uint32_t)k);
+                    if (cls[c] == (uint32_t)k) {
+                        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                  __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                        perm[before + rank] = (uint16_t)(c * 64 + lane);
+                    }
+                    before += (uint32_t)__popcll(m);
                 }
-                before += (uint32_t)__popcll(m);
             }
         }
     }
@@ -271,13 +293,14 @@ hash_regroup_kernel(const BatchArgs args) {
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <int C, bool NT, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false>
+template <int C, bool NT, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false,
+          bool ASORT = false>
 static hipError_t launch_regroup(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT, DIRECT, A4, PIPE>), dim3((uint32_t)blocks), dim3(256), 0,
+    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT, DIRECT, A4, PIPE, ASORT>), dim3((uint32_t)blocks), dim3(256), 0,
                        stream, args);
     return hipGetLastError();
 }
@@ -305,6 +328,8 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 31: return launch_chunk<true, false, 0, true>(args, stream);
         case 35: return launch_regroup<2, true, true, true, true>(args, stream);
         case 37: return launch_regroup<2, true, true, true, true, true>(args, stream);
+        case 38: return launch_regroup<2, true, true, true, true, false, true>(args, stream);
+        case 39: return launch_regroup<8, true, true, true, false, false, true>(args, stream);
         case 40: return launch_chunk<true, false, 1>(args, stream);  // debug shape: loads only
         case 41: return launch_chunk<true, false, 2>(args, stream);  // debug shape: arithmetic only
         default: return hipErrorInvalidValue;
@@ -317,6 +342,7 @@ static constexpr int kDefaultVariant = -1;  // automatic
 static bool known_variant(int v) {
     switch (v) {
         case -1: case 12: case 18: case 19: case 20: case 21: case 25: case 26: case 30: case 31: case 35: case 37:
+        case 38: case 39:
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;
@@ -342,9 +368,9 @@ static int g_variant = [] {
 //    32 M slots (config 3a: 2.24 vs 2.38 ms), else the one-chunk kernel (12)
 //    (config 1);
 //  * otherwise (strings + int64/float, config 3b): regroup with the class sort
-//    over 2 chunks and dword-aligned loads (35): 3.51 vs 4.22 ms for the chunk
-//    kernel — byte-misaligned 16-byte loads had made the texture-address unit
-//    the bound.
+//    over 2 chunks (LDS fetch-add counting sort) and dword-aligned loads (38):
+//    3.38 vs 4.22 ms for the chunk kernel — byte-misaligned 16-byte loads had
+//    made the texture-address unit the bound.
 static int auto_variant(const BatchArgs& args) {
     uint32_t numeric = 0;
     bool complex_types = false;
@@ -361,7 +387,7 @@ static int auto_variant(const BatchArgs& args) {
         if (slots >= (32ull << 20)) return 20;
         return 12;
     }
-    return 35;
+    return 38;
 }
 
 int hash_variant() { return __atomic_load_n(&g_variant, __ATOMIC_RELAXED); }
@@ -393,14 +419,16 @@ const char* variant_kernel_name(int v) {
         case 12: return "void hdx::hash_chunk_kernel<true, false, 0, false>(hdx::BatchArgs)";
         case 30: return "void hdx::hash_chunk_kernel<true, true, 0, false>(hdx::BatchArgs)";
         case 31: return "void hdx::hash_chunk_kernel<true, false, 0, true>(hdx::BatchArgs)";
-        case 18: return "void hdx::hash_regroup_kernel<4, true, true, true, false, false>(hdx::BatchArgs)";
-        case 19: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false>(hdx::BatchArgs)";
-        case 20: return "void hdx::hash_regroup_kernel<8, true, false, true, false, false>(hdx::BatchArgs)";
-        case 21: return "void hdx::hash_regroup_kernel<4, true, false, true, false, false>(hdx::BatchArgs)";
-        case 25: return "void hdx::hash_regroup_kernel<16, true, false, false, false, false>(hdx::BatchArgs)";
-        case 26: return "void hdx::hash_regroup_kernel<2, true, true, true, false, false>(hdx::BatchArgs)";
-        case 35: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false>(hdx::BatchArgs)";
-        case 37: return "void hdx::hash_regroup_kernel<2, true, true, true, true, true>(hdx::BatchArgs)";
+        case 18: return "void hdx::hash_regroup_kernel<4, true, true, true, false, false, false>(hdx::BatchArgs)";
+        case 19: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, false>(hdx::BatchArgs)";
+        case 20: return "void hdx::hash_regroup_kernel<8, true, false, true, false, false, false>(hdx::BatchArgs)";
+        case 21: return "void hdx::hash_regroup_kernel<4, true, false, true, false, false, false>(hdx::BatchArgs)";
+        case 25: return "void hdx::hash_regroup_kernel<16, true, false, false, false, false, false>(hdx::BatchArgs)";
+        case 26: return "void hdx::hash_regroup_kernel<2, true, true, true, false, false, false>(hdx::BatchArgs)";
+        case 35: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, false>(hdx::BatchArgs)";
+        case 37: return "void hdx::hash_regroup_kernel<2, true, true, true, true, true, false>(hdx::BatchArgs)";
+        case 38: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true>(hdx::BatchArgs)";
+        case 39: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, true>(hdx::BatchArgs)";
         default: return "";
     }
 }
