@@ -220,6 +220,9 @@ hipError_t ship(hdx_batcher_s* b, Slot& s) {
             r.t[t].lower = tb->d_lower;
             r.t[t].upper = tb->d_upper;
             r.t[t].ids = tb->d_ids;
+            r.t[t].index = tb->d_index;
+            r.t[t].W = tb->W;
+            r.t[t].index_words = tb->index_words;
             r.t[t].D = tb->D;
             r.t[t].R = tb->R;
             std::memcpy(r.t[t].attrs, tb->attrs, sizeof r.t[t].attrs);

@@ -499,6 +499,13 @@ HDX_EXPORT hdx_status hdx_synth_fill(const hdx_synth_rule* rules, uint32_t attrs
 
 // ---- region tables (hdx_regions.hip) ----------------------------------------
 
+// HDX_REGION_SCAN=1 (A/B only): tables created afterwards keep no interval
+// index, so lookups scan the boxes as the reference does.
+static bool region_index_disabled() {
+    const char* e = getenv("HDX_REGION_SCAN");
+    return e && *e == '1';
+}
+
 
 HDX_EXPORT hdx_status hdx_region_table_create(uint32_t dims, uint32_t regions, const uint16_t* attrs,
                                               const uint64_t* lower, const uint64_t* upper,
@@ -529,6 +536,18 @@ HDX_EXPORT hdx_status hdx_region_table_create(uint32_t dims, uint32_t regions, c
         hdx_region_table_destroy(t);
         return fail(HDX_E_DEVICE, "region table upload failed");
     }
+    // the interval index (hdx_regions.hip) for tables of up to 256 regions
+    std::vector<uint64_t> index;
+    region_index_build(dims, regions, lower, upper, index, t->W);
+    if (!index.empty() && !region_index_disabled()) {
+        t->index_words = (uint32_t)index.size();
+        if (hipMalloc((void**)&t->d_index, index.size() * 8) != hipSuccess ||
+            hipMemcpy(t->d_index, index.data(), index.size() * 8, hipMemcpyHostToDevice) != hipSuccess) {
+            (void)hipGetLastError();
+            hdx_region_table_destroy(t);
+            return fail(HDX_E_DEVICE, "region index upload failed");
+        }
+    }
     *out = t;
     return HDX_OK;
 }
@@ -538,6 +557,7 @@ HDX_EXPORT hdx_status hdx_region_table_destroy(hdx_region_table t) {
     (void)hipFree(t->d_lower);
     (void)hipFree(t->d_upper);
     (void)hipFree(t->d_ids);
+    (void)hipFree(t->d_index);
     delete t;
     return HDX_OK;
 }
@@ -557,6 +577,9 @@ HDX_EXPORT hdx_status hdx_lookup_region_device(hdx_region_table t, const uint64_
     a.lower = t->d_lower;
     a.upper = t->d_upper;
     a.ids = t->d_ids;
+    a.index = t->d_index;
+    a.W = t->W;
+    a.index_words = t->index_words;
     a.coords = coords;
     a.out = region_ids;
     a.n = n;

@@ -72,5 +72,7 @@ struct hdx_region_table_s {
     uint64_t* d_lower;
     uint64_t* d_upper;
     uint64_t* d_ids;
+    uint64_t* d_index;  // interval index (NULL: lookups scan the boxes)
+    uint32_t W, index_words;
 };
 

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../../include/hdxhash.h"
 
 namespace hdx {
@@ -48,10 +50,14 @@ const char* variant_kernel_name(int v);
 
 // Region lookup (hdx_regions.hip): table pointers are device memory owned by
 // an hdx_region_table handle; attrs[] holds the subspace's attribute indices.
+// index (may be NULL): the table's per-dimension interval index
+// (hdx_regions.hip, region_index_build) of index_words u64, W mask words.
 struct RegionArgs {
     const uint64_t* lower;   // [R*D]
     const uint64_t* upper;   // [R*D]
     const uint64_t* ids;     // [R]
+    const uint64_t* index;
+    uint32_t W, index_words;
     const uint64_t* coords;  // [n*A]
     uint64_t* out;           // [n]
     uint64_t n;
@@ -73,12 +79,19 @@ struct MultiRegionArgs {
         const uint64_t* lower;
         const uint64_t* upper;
         const uint64_t* ids;
+        const uint64_t* index;
+        uint32_t W, index_words;
         uint32_t D, R;
         uint16_t attrs[16];
     } t[kMaxMultiTables];
 };
 
 hipError_t launch_lookup_regions_multi(const MultiRegionArgs& a, hipStream_t stream);
+
+// Host: the interval index of a region table (empty when R > kIndexMaxRegions).
+constexpr uint32_t kIndexMaxRegions = 256;
+void region_index_build(uint32_t D, uint32_t R, const uint64_t* lower, const uint64_t* upper,
+                        std::vector<uint64_t>& index, uint32_t& W);
 
 // Stored-object sweep (hdx_encoded.hip): device arrays.
 struct EncodedArgs {

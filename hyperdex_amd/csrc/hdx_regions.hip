@@ -12,19 +12,107 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "hdx_internal.h"
 
 namespace hdx {
 
 constexpr uint32_t kMaxLookupDims = 16;
 
-template <bool IN_LDS>
+// ---------------------------------------------------------------------------
+// Interval index.  For every subspace dimension d the table's box edges
+// (lower[r][d] and upper[r][d] + 1) cut the u64 line into at most 2R+1
+// intervals, and every point of one interval lies in the same set of the
+// table's boxes on that dimension — a bit mask over the regions.  The first
+// region (in table order) whose box holds the coordinates is then the lowest
+// set bit of the AND of the D masks of the coordinates' intervals: exactly the
+// reference's first-match scan (configuration.cc:698-735), overlapping or
+// empty boxes included, at D binary searches instead of up to R*D compares.
+// Layout, u64 words: D headers (m | boundaries offset << 16 | masks offset
+// << 40), then per dimension its m sorted boundaries and (m + 1) * W mask words.
+// ---------------------------------------------------------------------------
+void region_index_build(uint32_t D, uint32_t R, const uint64_t* lower, const uint64_t* upper,
+                        std::vector<uint64_t>& index, uint32_t& W) {
+    index.clear();
+    W = 0;
+    if (R == 0 || R > kIndexMaxRegions || D == 0 || D > kMaxLookupDims) return;
+    W = (R + 63) / 64;
+    index.assign(D, 0);
+    std::vector<uint64_t> pts;
+    for (uint32_t d = 0; d < D; ++d) {
+        pts.clear();
+        for (uint32_t r = 0; r < R; ++r) {
+            pts.push_back(lower[(size_t)r * D + d]);
+            if (upper[(size_t)r * D + d] != UINT64_MAX) pts.push_back(upper[(size_t)r * D + d] + 1);
+        }
+        std::sort(pts.begin(), pts.end());
+        pts.erase(std::unique(pts.begin(), pts.end()), pts.end());
+        const uint64_t m = pts.size(), boff = index.size();
+        index.insert(index.end(), pts.begin(), pts.end());
+        const uint64_t moff = index.size();
+        for (uint64_t i = 0; i <= m; ++i) {
+            const uint64_t x = i == 0 ? 0 : pts[i - 1];  // a point of interval i (interval 0 may be empty)
+            uint64_t mask[kIndexMaxRegions / 64] = {0, 0, 0, 0};
+            for (uint32_t r = 0; r < R; ++r)
+                if (lower[(size_t)r * D + d] <= x && x <= upper[(size_t)r * D + d]) mask[r >> 6] |= 1ull << (r & 63);
+            index.insert(index.end(), mask, mask + W);
+        }
+        index[d] = m | (boff << 16) | (moff << 40);
+    }
+}
+
+// Region id of coordinates h[0..D) through the interval index idx.
+__device__ __forceinline__ uint64_t lookup_indexed(const uint64_t* idx, uint32_t W, uint32_t D, const uint64_t* h,
+                                                   const uint64_t* ids) {
+    uint64_t acc[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+#pragma unroll
+    for (uint32_t d = 0; d < kMaxLookupDims; ++d) {
+        if (d >= D) break;
+        const uint64_t hdr = idx[d];
+        const uint32_t m = (uint32_t)(hdr & 0xffff);
+        const uint64_t* B = idx + ((hdr >> 16) & 0xffffff);
+        // number of boundaries <= h[d]: fixed-step binary search (same steps on every lane)
+        uint32_t pos = 0;
+        for (uint32_t step = m ? 1u << (31 - __builtin_clz(m)) : 0u; step; step >>= 1)
+            if (pos + step <= m && B[pos + step - 1] <= h[d]) pos += step;
+        const uint64_t* mask = idx + (hdr >> 40) + (size_t)pos * W;
+#pragma unroll
+        for (uint32_t w = 0; w < 4; ++w)
+            if (w < W) acc[w] &= mask[w];
+    }
+#pragma unroll
+    for (uint32_t w = 0; w < 4; ++w)
+        if (w < W && acc[w]) return ids[64 * w + __builtin_ctzll(acc[w])];
+    return 0;  // region_id()
+}
+
+template <bool IN_LDS, bool INDEX = false>
 __global__ void __launch_bounds__(256)
 lookup_region_kernel(const RegionArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     const uint64_t* lower = a.lower;
     const uint64_t* upper = a.upper;
     const uint64_t* ids = a.ids;
+    const uint64_t* index = a.index;
+    if (INDEX) {
+        if (IN_LDS) {
+            for (uint32_t k = threadIdx.x; k < a.index_words; k += blockDim.x) smem[k] = a.index[k];
+            for (uint32_t k = threadIdx.x; k < a.R; k += blockDim.x) smem[a.index_words + k] = a.ids[k];
+            __syncthreads();
+            index = smem;
+            ids = smem + a.index_words;
+        }
+        const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        if (i >= a.n) return;
+        uint64_t h[kMaxLookupDims];
+        const uint64_t* row = a.coords + i * a.A;
+#pragma unroll
+        for (uint32_t d = 0; d < kMaxLookupDims; ++d)
+            if (d < a.D) h[d] = row[a.attrs[d]];
+        a.out[i] = lookup_indexed(index, a.W, a.D, h, ids);
+        return;
+    }
     if (IN_LDS) {
         const uint32_t box = a.R * a.D;
         for (uint32_t k = threadIdx.x; k < box; k += blockDim.x) {
@@ -62,6 +150,14 @@ hipError_t launch_lookup_region(const RegionArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
     const uint64_t blocks = (a.n + 255) / 256;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    if (a.index) {
+        const size_t lds = ((size_t)a.index_words + a.R) * 8;
+        if (lds <= 48 * 1024)
+            hipLaunchKernelGGL((lookup_region_kernel<true, true>), dim3((uint32_t)blocks), dim3(256), lds, stream, a);
+        else
+            hipLaunchKernelGGL((lookup_region_kernel<false, true>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+        return hipGetLastError();
+    }
     const size_t lds = (size_t)a.R * a.D * 16 + (size_t)a.R * 8;
     if (lds <= 48 * 1024) {
         hipLaunchKernelGGL(lookup_region_kernel<true>, dim3((uint32_t)blocks), dim3(256), lds, stream, a);
@@ -76,6 +172,8 @@ hipError_t launch_lookup_region(const RegionArgs& a, hipStream_t stream) {
 // and ids are staged in LDS per workgroup (the walk is then LDS broadcasts,
 // as in lookup_region_kernel); tables too large for that are walked in global
 // memory.
+// A table with an interval index stages the index (in the lower slot) and its
+// ids; one without stages its boxes and ids.
 struct MultiLayout {
     uint32_t lower[kMaxMultiTables], upper[kMaxMultiTables], ids[kMaxMultiTables];  // u64 offsets
     uint32_t words;
@@ -85,11 +183,11 @@ __host__ __device__ inline MultiLayout multi_layout(const MultiRegionArgs& a) {
     MultiLayout l{};
     uint32_t w = 0;
     for (uint32_t t = 0; t < a.T; ++t) {
-        const uint32_t box = a.t[t].R * a.t[t].D;
+        const uint32_t box = a.t[t].index ? a.t[t].index_words : a.t[t].R * a.t[t].D;
         l.lower[t] = w;
         l.upper[t] = w + box;
-        l.ids[t] = w + 2 * box;
-        w += 2 * box + a.t[t].R;
+        l.ids[t] = a.t[t].index ? w + box : w + 2 * box;
+        w = l.ids[t] + a.t[t].R;
     }
     l.words = w;
     return l;
@@ -101,10 +199,15 @@ __global__ void __launch_bounds__(256) lookup_regions_multi_kernel(const MultiRe
     const MultiLayout l = multi_layout(a);
     if (IN_LDS) {
         for (uint32_t t = 0; t < a.T; ++t) {
-            const uint32_t box = a.t[t].R * a.t[t].D;
-            for (uint32_t k = threadIdx.x; k < box; k += blockDim.x) {
-                smem[l.lower[t] + k] = a.t[t].lower[k];
-                smem[l.upper[t] + k] = a.t[t].upper[k];
+            if (a.t[t].index) {
+                for (uint32_t k = threadIdx.x; k < a.t[t].index_words; k += blockDim.x)
+                    smem[l.lower[t] + k] = a.t[t].index[k];
+            } else {
+                const uint32_t box = a.t[t].R * a.t[t].D;
+                for (uint32_t k = threadIdx.x; k < box; k += blockDim.x) {
+                    smem[l.lower[t] + k] = a.t[t].lower[k];
+                    smem[l.upper[t] + k] = a.t[t].upper[k];
+                }
             }
             for (uint32_t k = threadIdx.x; k < a.t[t].R; k += blockDim.x) smem[l.ids[t] + k] = a.t[t].ids[k];
         }
@@ -122,6 +225,10 @@ __global__ void __launch_bounds__(256) lookup_regions_multi_kernel(const MultiRe
 #pragma unroll
     for (uint32_t d = 0; d < kMaxLookupDims; ++d)
         if (d < tb.D) h[d] = row[tb.attrs[d]];
+    if (tb.index) {
+        a.out[t * a.out_stride + i] = lookup_indexed(IN_LDS ? smem + l.lower[t] : tb.index, tb.W, tb.D, h, ids);
+        return;
+    }
     uint64_t rid = 0;
     for (uint32_t r = 0; r < tb.R; ++r) {
         bool match = true;

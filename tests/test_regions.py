@@ -89,6 +89,38 @@ def test_gpu_lookup_overlapping_boxes(oracle, R):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("R", [2, 63, 64, 65, 200, 256])
+@pytest.mark.parametrize("scan", [False, True])
+def test_gpu_lookup_index_vs_scan(oracle, R, scan, monkeypatch):
+    """The interval index (tables of <= 256 regions) and the box scan
+    (HDX_REGION_SCAN=1) agree with the oracle's first-match scan on
+    overlapping boxes, empty boxes (lower > upper), boxes reaching 0 and
+    2^64-1, and duplicated boxes (first one wins)."""
+    import torch
+
+    from hyperdex_amd import regions
+    if scan:
+        monkeypatch.setenv("HDX_REGION_SCAN", "1")
+    rng = np.random.default_rng(R + 7)
+    A, attrs = 9, [8, 2]
+    a = rng.integers(0, 2**64, size=(R, 2), dtype=np.uint64)
+    b = rng.integers(0, 2**64, size=(R, 2), dtype=np.uint64)
+    lo, up = np.minimum(a, b), np.maximum(a, b)
+    lo[0, 0] = 0
+    up[R // 2, 1] = U64MAX
+    if R > 3:
+        lo[1], up[1] = up[1], lo[1]          # empty box on both dimensions
+        lo[R - 1], up[R - 1] = lo[2], up[2]  # duplicate of box 2: never the first match
+    ids = rng.integers(1, 2**63, R, dtype=np.uint64)
+    coords = _coords(rng, 20000, A, lo, up, attrs)
+    want = oracle.lookup_region(attrs, lo, up, ids, coords)
+    t = regions.RegionTable(attrs, lo, up, ids)
+    got = regions.lookup_region(t, torch.from_numpy(coords.view(np.int64)).to(torch.device("cuda", 0)))
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().view(np.uint64), want)
+
+
+@pytest.mark.gpu
 def test_gpu_hash_then_point_leader(oracle):
     """hash -> lookup on subspace 0 (point_leader's region step) end to end."""
     import torch
