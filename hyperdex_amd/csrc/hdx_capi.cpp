@@ -177,9 +177,10 @@ static hdx_status hash_host(const uint8_t* codes, uint32_t A, const uint8_t* blo
     if (st != HDX_OK) return st;
     ThreadState& ts = t_state;
 
-    // Host-side validation (the reference asserts here) + per-object extents.
-    std::vector<uint64_t> size(n);
-    for (uint64_t i = 0; i < n; ++i) {
+    // Host-side validation (the reference asserts here) and the object's byte
+    // extent, done chunk by chunk as the pipeline below reaches each object, so
+    // the first copies start after one chunk's validation, not the batch's.
+    auto extent = [&](uint64_t i, uint64_t* out) -> hdx_status {
         uint64_t s = 0;
         for (uint32_t j = 0; j < A; ++j) {
             const uint32_t L = attr_len[i * A + j];
@@ -195,8 +196,9 @@ static hdx_status hash_host(const uint8_t* codes, uint32_t A, const uint8_t* blo
             return fail(HDX_E_INVALID, "object %llu [%llu,+%llu) outside blob of %llu bytes",
                         (unsigned long long)i, (unsigned long long)obj_base[i],
                         (unsigned long long)s, (unsigned long long)blob_bytes);
-        size[i] = s;
-    }
+        *out = s;
+        return HDX_OK;
+    };
 
     const bool blob_pinned = is_pinned(blob);
     const bool len_pinned = is_pinned(attr_len);
@@ -220,14 +222,22 @@ static hdx_status hash_host(const uint8_t* codes, uint32_t A, const uint8_t* blo
         return HDX_OK;
     };
 
-    uint64_t i = 0;
+    uint64_t i = 0, next_size = 0;
     int k = 0;
+    if ((st = extent(0, &next_size)) != HDX_OK) return st;
+    auto drain = [&](hdx_status err) {  // an invalid object: let the copies in flight land
+        (void)finish(0);
+        (void)finish(1);
+        return err;
+    };
     while (i < n) {
-        // Grow the chunk while its byte extent stays under kChunkBytes.
-        uint64_t lo = obj_base[i], hi = obj_base[i] + size[i], e = i + 1;
+        // Grow the chunk while its byte extent stays under kChunkBytes; an
+        // object that does not fit starts the next chunk (its extent is kept).
+        uint64_t lo = obj_base[i], hi = obj_base[i] + next_size, e = i + 1;
         while (e < n) {
+            if ((st = extent(e, &next_size)) != HDX_OK) return drain(st);
             const uint64_t nlo = std::min(lo, obj_base[e]);
-            const uint64_t nhi = std::max(hi, obj_base[e] + size[e]);
+            const uint64_t nhi = std::max(hi, obj_base[e] + next_size);
             if (nhi - nlo > kChunkBytes) break;
             lo = nlo; hi = nhi; ++e;
         }

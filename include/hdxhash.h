@@ -108,10 +108,13 @@ hdx_status hdx_hash_batch_device(const uint32_t* types, uint32_t attrs_sz,
                                  hdx_stream stream);
 
 /* Same batch with every array in HOST memory (pageable or pinned).
- * Synchronous.  The library validates numeric sizes on the host, then
- * streams the batch through the device in chunks, overlapping H2D copies,
- * kernels and D2H copies on two streams.  blob_bytes is the size of the
- * blob allocation (every object must lie inside it). */
+ * Synchronous.  The library streams the batch through the device in chunks,
+ * overlapping H2D copies, kernels and D2H copies on two streams, and
+ * validates numeric sizes and object extents on the host chunk by chunk
+ * ahead of the copies.  blob_bytes is the size of the blob allocation (every
+ * object must lie inside it).  On HDX_E_BADSIZE / HDX_E_INVALID nothing is in
+ * flight when the call returns; coordinates of objects before the offending
+ * one may have been written, the rest are untouched. */
 hdx_status hdx_hash_batch_host(const uint32_t* types, uint32_t attrs_sz,
                                const uint8_t* blob, uint64_t blob_bytes,
                                const uint64_t* obj_base, const uint32_t* attr_len,

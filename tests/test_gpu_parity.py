@@ -227,6 +227,26 @@ def test_host_path_multichunk(oracle, torch_dev):
     assert np.array_equal(got[idx], want)
 
 
+def test_host_path_bad_size_in_a_late_chunk(oracle, torch_dev):
+    """Validation runs chunk by chunk inside the pipeline: a mis-sized numeric
+    in the third chunk fails the call with HDX_E_BADSIZE after the copies in
+    flight have landed; the objects of the first chunk are hashed, the last
+    objects untouched."""
+    torch, dev = torch_dev
+    types, blob, base, lens = synth.make_batch_host("cfg2", 3_000_000, seed=9)  # ~290 MB, 3 chunks
+    A = len(types)
+    lens = lens.copy()
+    bad = 2_900_000
+    lens[bad * A + 2] = 5  # an INT64 of 5 bytes
+    out = np.full((len(base), A), 0x5A5A5A5A5A5A5A5A, np.uint64)
+    with pytest.raises(hdx.HdxError) as e:
+        hdx.hash_batch_host(types, blob, base, lens, out=out)
+    assert e.value.status == _lib.HDX_E_BADSIZE
+    want, _ = oracle.hash_batch(types, blob, base[:1000], lens[:1000 * A])
+    assert np.array_equal(out[:1000], want.reshape(1000, A))
+    assert (out[-1000:] == 0x5A5A5A5A5A5A5A5A).all()
+
+
 def test_device_generator_matches_host_generator(torch_dev):
     torch, dev = torch_dev
     for cfg in ("cfg2", "cfg3b", "mixed"):
