@@ -99,7 +99,7 @@ __device__ __forceinline__ const uint8_t* dw_floor(const uint8_t* p) { return p 
 // Piece offsets of the A4 form, from the value's base (or from the zero pad
 // when the slot has no bytes to read: any = false), as 32-bit arithmetic;
 // pl = the base's low address bits.  Shared by the global-memory form
-// (issue_block_a4) and the LDS-window form (hdx_window.hip).
+// (issue_block_a4); the retired LDS-window kernels read the window with it.
 struct A4Offsets {
     int32_t o0, o1, o2, o3, e1, e3;  // dword-aligned piece starts and next dwords
     uint32_t ra, rb;
