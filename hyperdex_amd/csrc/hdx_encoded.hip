@@ -140,7 +140,7 @@ hash_encoded_kernel(const EncodedArgs a) {
     auto load_pass = [&](uint32_t t, Pass& P) {
         const uint32_t q = t * 64 + (uint32_t)lane;
         const uint32_t s = min(q, nslots - 1);
-        const uint32_t obj = s / A, j = s - obj * A;
+        const uint32_t obj = div_small(s, a.a_magic), j = s - obj * A;  // s < 64 * A
         const EncDesc d = desc[s];
         const uint64_t base = bases[2 * obj + (j == 0)];
         const bool zero = d.off == kZeroSlot || q >= nslots;
@@ -186,8 +186,10 @@ static hipError_t launch_encoded(const EncodedArgs& a, hipStream_t stream) {
     return hipGetLastError();
 }
 
-hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream) {
-    if (a.n == 0) return hipSuccess;
+hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
+    if (a_in.n == 0) return hipSuccess;
+    EncodedArgs a = a_in;
+    a.a_magic = (uint32_t)(((1ull << 31) + a.A - 1) / a.A);
     // default: dword-aligned loads (5.49 vs 6.14 ms per 10 M config-3b objects,
     // profiles/r1/ab_a4_cfg5.jsonl), 32 objects per wave (5.05 vs 5.31 ms for
     // 64 (variant 47) and 5.88 for 16 (48), ab_cfg5_objects_per_wave.jsonl);

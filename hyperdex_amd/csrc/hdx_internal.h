@@ -32,11 +32,14 @@ struct BatchArgs {
     uint64_t n;
     uint32_t A;
     uint32_t uniform_code;  // the code every attribute shares, or 0xff if mixed
+    double inv_A;           // 1.0 / A                       (finalize_args)
+    uint32_t a_magic;       // ceil(2^31 / A): t / A == (t * a_magic) >> 31 for t * A < 2^31
+    uint32_t pad_;
     uint8_t codes[HDX_MAX_ATTRS];
 };
 
 hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream);
-// Fills args.uniform_code from args.codes[0..A).
+// Fills args.uniform_code from args.codes[0..A), and inv_A / a_magic from A.
 void finalize_args(BatchArgs& args);
 // Kernel variants (hdx_kernels.hip, variant_kernel_name): the automatic policy's
 // choices and the alternatives scripts/ab_variants.py times against them.
@@ -106,7 +109,7 @@ struct EncodedArgs {
     uint32_t* status;    // may be NULL
     uint64_t n;
     uint32_t A;
-    uint32_t pad_;
+    uint32_t a_magic;  // ceil(2^31 / A) (launch_hash_encoded fills it)
     uint8_t codes[HDX_MAX_ATTRS];
 };
 

@@ -57,9 +57,9 @@ hash_chunk_kernel(const BatchArgs args) {
     // this lane's slot -> (object il, attribute j)
     uint64_t i0;
     uint32_t j0;
-    split_slot(q0, A, i0, j0);
+    split_slot(q0, A, args.inv_A, i0, j0);
     const uint32_t t = j0 + (uint32_t)lane;
-    const uint32_t di = t / A;  // small: t < A + 64
+    const uint32_t di = div_small(t, args.a_magic);  // t < A + 64
     const uint32_t j = t - di * A;
     const uint64_t il = i0 + di;
     const bool valid = q0 + lane < nslots;
@@ -153,7 +153,7 @@ hash_regroup_kernel(const BatchArgs args) {
 
     uint64_t i0;
     uint32_t j0;
-    split_slot(qw, A, i0, j0);
+    split_slot(qw, A, args.inv_A, i0, j0);
     uint32_t carry = 0;
     for (uint32_t k = 0; k < j0; k += 64) {
         const uint32_t idx = k + (uint32_t)lane;
@@ -172,7 +172,7 @@ hash_regroup_kernel(const BatchArgs args) {
 #pragma unroll
     for (int c = 0; c < C; ++c) {
         const uint32_t t = j0 + (uint32_t)(c * 64 + lane);
-        const uint32_t di = t / A;
+        const uint32_t di = div_small(t, args.a_magic);  // t < A + 64 * C
         const uint32_t j = t - di * A;
         const bool valid = qw + c * 64 + lane < nslots;
         const uint64_t il = valid ? i0 + di : i0;
@@ -398,6 +398,8 @@ int set_hash_variant(int v) {
 }
 
 void finalize_args(BatchArgs& args) {
+    args.inv_A = 1.0 / (double)args.A;
+    args.a_magic = (uint32_t)(((1ull << 31) + args.A - 1) / args.A);
     args.uniform_code = args.codes[0];
     for (uint32_t j = 1; j < args.A; ++j)
         if (args.codes[j] != args.codes[0]) args.uniform_code = 0xffu;

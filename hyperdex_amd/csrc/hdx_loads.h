@@ -402,10 +402,16 @@ __device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
     return v;
 }
 
+// t / A for small t (t * A < 2^31) by the host's ceil(2^31 / A).
+__device__ __forceinline__ uint32_t div_small(uint32_t t, uint32_t a_magic) {
+    return (uint32_t)(((uint64_t)t * a_magic) >> 31);
+}
+
 // Wave-uniform slot -> (object, attribute) split without a 64-bit integer
-// divide: q < 2^53, so the f64 quotient is off by at most one; fix it up.
-__device__ __forceinline__ void split_slot(uint64_t q, uint32_t A, uint64_t& i0, uint32_t& j0) {
-    uint64_t i = (uint64_t)((double)q * (1.0 / (double)A));
+// divide: q < 2^53, so the f64 quotient by the host's 1/A is off by at most
+// one; fix it up.
+__device__ __forceinline__ void split_slot(uint64_t q, uint32_t A, double inv_A, uint64_t& i0, uint32_t& j0) {
+    uint64_t i = (uint64_t)((double)q * inv_A);
     int64_t rem = (int64_t)(q - i * A);
     if (rem < 0) { --i; rem += A; }
     if (rem >= (int64_t)A) { ++i; rem -= A; }
