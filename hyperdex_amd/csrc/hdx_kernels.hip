@@ -102,11 +102,27 @@ hash_chunk_kernel(const BatchArgs args) {
 // Work classes (the regroup kernel's sort key) and the 16-byte slot descriptor.
 constexpr int kClasses = 8;
 
+// ORDER 0: {numerics, <= 16 B}, 17..64 B, then > 64 B by loop blocks.
+// ORDER 1: numerics, 33..64, <= 16, 17..32, then > 64 B by blocks (1, 2, 3, 4+):
+//          puts the cheap 33..64-byte regime beside the numerics in the first
+//          pass of a 2-chunk wave and the short-string regimes with the long ones.
+// ORDER 2: numerics, <= 16, 17..32, 33..64, then > 64 B by blocks.
+template <int ORDER = 0>
 __device__ __forceinline__ uint32_t work_class(uint32_t code, uint32_t n, bool valid) {
-    if (!valid || code != CODE_STRING || n <= 16) return 0;
-    if (n <= 64) return 1;
-    const uint32_t b = (n - 1) >> 6;
-    return b >= 6 ? 7u : 1u + b;
+    if constexpr (ORDER == 0) {
+        if (!valid || code != CODE_STRING || n <= 16) return 0;
+        if (n <= 64) return 1;
+        const uint32_t b = (n - 1) >> 6;
+        return b >= 6 ? 7u : 1u + b;
+    } else {
+        if (!valid || code != CODE_STRING) return 0;
+        if (n > 64) {
+            const uint32_t b = (n - 1) >> 6;
+            return b >= 4 ? 7u : 3u + b;
+        }
+        if (ORDER == 1) return n > 32 ? 1u : n <= 16 ? 2u : 3u;
+        return n <= 16 ? 1u : n <= 32 ? 2u : 3u;
+    }
 }
 
 
@@ -135,7 +151,7 @@ struct RegroupLds {
 // next block in flight; ASORT: the class sort by LDS fetch-add instead of
 // ballot / mbcnt per (class, chunk).
 template <int C, bool NT_STORE, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false,
-          bool ASORT = false>
+          bool ASORT = false, int ORDER = 0>
 __global__ void __launch_bounds__(256)
 hash_regroup_kernel(const BatchArgs args) {
     __shared__ RegroupLds<C> lds;
@@ -192,7 +208,7 @@ hash_regroup_kernel(const BatchArgs args) {
         d.n = L;
         d.code_slot = code | ((uint32_t)(c * 64 + lane) << 8);
         desc[c * 64 + lane] = d;
-        cls[c] = work_class(code, L, valid);
+        cls[c] = work_class<ORDER>(code, L, valid);
     }
 
     // ---- counting sort by class (wave-local) ---------------------------------
@@ -294,13 +310,13 @@ hash_regroup_kernel(const BatchArgs args) {
 }
 
 template <int C, bool NT, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false,
-          bool ASORT = false>
+          bool ASORT = false, int ORDER = 0>
 static hipError_t launch_regroup(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT, DIRECT, A4, PIPE, ASORT>), dim3((uint32_t)blocks), dim3(256), 0,
+    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT, DIRECT, A4, PIPE, ASORT, ORDER>), dim3((uint32_t)blocks), dim3(256), 0,
                        stream, args);
     return hipGetLastError();
 }
@@ -330,6 +346,9 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 37: return launch_regroup<2, true, true, true, true, true>(args, stream);
         case 38: return launch_regroup<2, true, true, true, true, false, true>(args, stream);
         case 39: return launch_regroup<8, true, true, true, false, false, true>(args, stream);
+        case 44: return launch_regroup<2, true, true, true, true, false, true, 1>(args, stream);
+        case 45: return launch_regroup<2, true, true, true, true, false, true, 2>(args, stream);
+        case 46: return launch_regroup<8, true, true, true, false, false, true, 1>(args, stream);
         case 40: return launch_chunk<true, false, 1>(args, stream);  // debug shape: loads only
         case 41: return launch_chunk<true, false, 2>(args, stream);  // debug shape: arithmetic only
         default: return hipErrorInvalidValue;
@@ -342,7 +361,7 @@ static constexpr int kDefaultVariant = -1;  // automatic
 static bool known_variant(int v) {
     switch (v) {
         case -1: case 12: case 18: case 19: case 20: case 21: case 25: case 26: case 30: case 31: case 35: case 37:
-        case 38: case 39:
+        case 38: case 39: case 44: case 45: case 46:
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;
@@ -359,8 +378,9 @@ static int g_variant = [] {
 // Automatic choice (interleaved A/B on one MI355X, profiles/r1/ab_variants_*.jsonl
 // and profiles/r1/ab_a4_*.jsonl):
 //  * schemas with timestamps or non-hashable attributes: regroup kernel with the
-//    class sort, 8 chunks per wave (19) — their diverse paths dominate (mixed:
-//    2.64 vs 3.58 ms for the chunk kernel, 3.56 for 35);
+//    class sort, 8 chunks per wave, classes in ORDER 1 (46) — their diverse
+//    paths dominate (mixed: 2.32 vs 2.49 ms in ORDER 0 (19), 3.48 for the
+//    chunk kernel);
 //  * mostly numerics: regroup unsorted, 4 chunks per wave, direct stores (21)
 //    (config 2: 0.31 vs 0.42 ms);
 //  * one code everywhere (all strings): regroup unsorted with 16 chunks per wave
@@ -368,9 +388,10 @@ static int g_variant = [] {
 //    32 M slots (config 3a: 2.24 vs 2.38 ms), else the one-chunk kernel (12)
 //    (config 1);
 //  * otherwise (strings + int64/float, config 3b): regroup with the class sort
-//    over 2 chunks (LDS fetch-add counting sort) and dword-aligned loads (38):
-//    3.38 vs 4.22 ms for the chunk kernel — byte-misaligned 16-byte loads had
-//    made the texture-address unit the bound.
+//    over 2 chunks (LDS fetch-add counting sort, classes in ORDER 1) and
+//    dword-aligned loads (44): 3.37 vs 3.43 ms in ORDER 0 (38) and 4.22 for
+//    the chunk kernel — byte-misaligned 16-byte loads had made the
+//    texture-address unit the bound.
 static int auto_variant(const BatchArgs& args) {
     uint32_t numeric = 0;
     bool complex_types = false;
@@ -380,14 +401,14 @@ static int auto_variant(const BatchArgs& args) {
         complex_types |= c == CODE_ZERO || c >= CODE_TS_SECOND;
     }
     const uint64_t slots = args.n * args.A;
-    if (complex_types) return 19;
+    if (complex_types) return 46;
     if (2 * numeric > args.A) return 21;
     if (args.uniform_code != 0xffu) {
         if (slots >= (64ull << 20)) return 25;
         if (slots >= (32ull << 20)) return 20;
         return 12;
     }
-    return 38;
+    return 44;
 }
 
 int hash_variant() { return __atomic_load_n(&g_variant, __ATOMIC_RELAXED); }
@@ -421,16 +442,19 @@ const char* variant_kernel_name(int v) {
         case 12: return "void hdx::hash_chunk_kernel<true, false, 0, false>(hdx::BatchArgs)";
         case 30: return "void hdx::hash_chunk_kernel<true, true, 0, false>(hdx::BatchArgs)";
         case 31: return "void hdx::hash_chunk_kernel<true, false, 0, true>(hdx::BatchArgs)";
-        case 18: return "void hdx::hash_regroup_kernel<4, true, true, true, false, false, false>(hdx::BatchArgs)";
-        case 19: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, false>(hdx::BatchArgs)";
-        case 20: return "void hdx::hash_regroup_kernel<8, true, false, true, false, false, false>(hdx::BatchArgs)";
-        case 21: return "void hdx::hash_regroup_kernel<4, true, false, true, false, false, false>(hdx::BatchArgs)";
-        case 25: return "void hdx::hash_regroup_kernel<16, true, false, false, false, false, false>(hdx::BatchArgs)";
-        case 26: return "void hdx::hash_regroup_kernel<2, true, true, true, false, false, false>(hdx::BatchArgs)";
-        case 35: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, false>(hdx::BatchArgs)";
-        case 37: return "void hdx::hash_regroup_kernel<2, true, true, true, true, true, false>(hdx::BatchArgs)";
-        case 38: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true>(hdx::BatchArgs)";
-        case 39: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, true>(hdx::BatchArgs)";
+        case 18: return "void hdx::hash_regroup_kernel<4, true, true, true, false, false, false, 0>(hdx::BatchArgs)";
+        case 19: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, false, 0>(hdx::BatchArgs)";
+        case 20: return "void hdx::hash_regroup_kernel<8, true, false, true, false, false, false, 0>(hdx::BatchArgs)";
+        case 21: return "void hdx::hash_regroup_kernel<4, true, false, true, false, false, false, 0>(hdx::BatchArgs)";
+        case 25: return "void hdx::hash_regroup_kernel<16, true, false, false, false, false, false, 0>(hdx::BatchArgs)";
+        case 26: return "void hdx::hash_regroup_kernel<2, true, true, true, false, false, false, 0>(hdx::BatchArgs)";
+        case 35: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, false, 0>(hdx::BatchArgs)";
+        case 37: return "void hdx::hash_regroup_kernel<2, true, true, true, true, true, false, 0>(hdx::BatchArgs)";
+        case 38: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true, 0>(hdx::BatchArgs)";
+        case 39: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, true, 0>(hdx::BatchArgs)";
+        case 44: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true, 1>(hdx::BatchArgs)";
+        case 45: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true, 2>(hdx::BatchArgs)";
+        case 46: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, true, 1>(hdx::BatchArgs)";
         default: return "";
     }
 }
