@@ -44,6 +44,8 @@ def main():
                     help="skip the coordinates -> region ids step (SURVEY §8f-1)")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip timing the host-resident (PCIe-inclusive) path")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip timing config 3b (16 mixed attrs) beside the config-3a line")
     ap.add_argument("--traffic", default=latest_traffic_file(),
                     help="HBM bytes/launch measured by scripts/gpu_profile.sh (rocprofv3 PMC)")
     args = ap.parse_args()
@@ -176,6 +178,11 @@ def main():
     if not args.no_host_path and rank == 0 and world == 1 and cfg != "cfg5":
         result["host_path"] = time_host_path(types, blob, base, lens, A)
 
+    if rank == 0 and world == 1 and cfg == "cfg3a" and not args.no_secondary:
+        # BASELINE's third config with its mixed attribute types, measured the
+        # same way in the same run (the headline line stays config 3a's)
+        result["secondary"] = {"cfg3b": time_config("cfg3b", n, dev, stream)}
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if cfg == "cfg5":
             result["cpu_baseline"] = cpu_baseline_encoded(
@@ -277,6 +284,37 @@ def time_regions(coords, world, dev, backend, max_over_ranks, stream, gather, re
         res["allgather_ids_bytes"] = out.numel() * 8
     for t in tables:
         t.close()
+    return res
+
+
+def time_config(cfg, n, dev, stream, steps=10, warmup=2):
+    """Device-resident throughput of another config at the same object count:
+    HIP events around each launch on the launch stream, as for the main line."""
+    import torch
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import synth
+    types, blob, base, lens = synth.make_batch_device(cfg, n, device=dev)
+    A = len(types)
+    coords = torch.empty((n, A), dtype=torch.int64, device=dev)
+    for _ in range(warmup):
+        hdx.hash_batch(types, blob, base, lens, coords=coords, stream=stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    for s, e in ev:
+        s.record(stream)
+        hdx.hash_batch(types, blob, base, lens, coords=coords, stream=stream)
+        e.record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    payload = int(blob.numel())
+    algo = payload + n * A * ALGO_EXTRA_PER_ATTR
+    res = {"workload": "%s: %dM objects, key + %d attrs" % (cfg, n // 1_000_000, A - 1),
+           "GiB_s": round(payload / (ms / 1e3) / 2**30, 3), "mobjects_per_s": round(n / (ms / 1e3) / 1e6, 2),
+           "kernel_ms": round(ms, 4), "roofline_frac": round(algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+           "kernel": hdx.hashing.kernel_for(types, n)[1]}
+    del blob, base, lens, coords
+    torch.cuda.empty_cache()
     return res
 
 
