@@ -4,7 +4,7 @@
 # kernel variants on config 3b / config 5.  Stops at the first failing step.
 #   bash scripts/gpu_check.sh TAG [VARIANTS_3B]
 TAG=${1:-check}
-V3B=${2:-12,18,26,27,28,29}
+V3B=${2:-44,38,35,12}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$ROOT/gpurun_out/check_$TAG
 mkdir -p $O
