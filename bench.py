@@ -174,6 +174,12 @@ def main():
     if not args.no_regions:
         result["regions"] = time_regions(coords, world, dev, backend, max_over_ranks, stream,
                                          gather=world > 1 and not args.no_allgather)
+        if cfg == "cfg5":
+            # the sweep's purpose: the new regions, decoded + hashed + looked up
+            # in one launch with no coordinate written (hdx_hash_encoded_regions_device)
+            result["fused_regions"] = time_fused_sweep(
+                types, (keys, key_off, key_len, vals, val_off, val_len), n, A, dev, stream, max_over_ranks,
+                result["roofline"]["kernel_ms"], result["regions"]["lookup_ms"])
 
     if not args.no_host_path and rank == 0 and world == 1 and cfg != "cfg5":
         result["host_path"] = time_host_path(types, blob, base, lens, A)
@@ -316,6 +322,30 @@ def time_config(cfg, n, dev, stream, steps=10, warmup=2):
     del blob, base, lens, coords
     torch.cuda.empty_cache()
     return res
+
+
+def time_fused_sweep(types, enc, n, A, dev, stream, max_over_ranks, sweep_ms, lookup_ms, reps=10):
+    """hdx_hash_encoded_regions_device over the same stored objects and the
+    same two tables as time_regions, coordinates not written; next to the
+    sweep + separate lookups it replaces."""
+    import torch
+
+    import hyperdex_amd as hdx
+    tables = key_subspace_tables(A)
+    hdx.hash_encoded_regions(types, *enc, tables, stream=stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    torch.cuda.synchronize()
+    for s, e in ev:
+        s.record(stream)
+        hdx.hash_encoded_regions(types, *enc, tables, stream=stream)
+        e.record(stream)
+    torch.cuda.synchronize()
+    (ms,) = max_over_ranks(float(np.mean([s.elapsed_time(e) for s, e in ev])))
+    for t in tables:
+        t.close()
+    return {"tables": len(tables), "fused_ms": round(ms, 4),
+            "separate_ms": round(sweep_ms + lookup_ms, 4),
+            "mobjects_per_s": round(n / (ms / 1e3) / 1e6, 2)}
 
 
 def latest_traffic_file():

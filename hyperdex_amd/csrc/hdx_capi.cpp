@@ -351,20 +351,43 @@ HDX_EXPORT hdx_status hdx_hash_batch_device(const uint32_t* types, uint32_t attr
     return HDX_OK;
 }
 
-HDX_EXPORT hdx_status hdx_hash_encoded_device(const uint32_t* types, uint32_t attrs_sz,
-                                              const uint8_t* keys, const uint64_t* key_off,
-                                              const uint32_t* key_len, const uint8_t* vals,
-                                              const uint64_t* val_off, const uint32_t* val_len,
-                                              uint64_t n, uint64_t* coords, uint64_t* versions,
-                                              uint32_t* status_dev, hdx_stream stream) {
+static hdx_status hash_encoded(const uint32_t* types, uint32_t attrs_sz, const uint8_t* keys,
+                               const uint64_t* key_off, const uint32_t* key_len, const uint8_t* vals,
+                               const uint64_t* val_off, const uint32_t* val_len, uint64_t n,
+                               const hdx_region_table* tables, uint32_t ntables, uint64_t* region_ids,
+                               uint64_t* coords, uint64_t* versions, uint32_t* status_dev, hdx_stream stream) {
     EncodedArgs a{};
     hdx_status st = check_schema(types, attrs_sz, a.codes);
     if (st != HDX_OK) return st;
     if (attrs_sz > 128) return fail(HDX_E_INVALID, "attrs_sz=%u > 128 for stored objects", attrs_sz);
+    if (ntables > kMaxSweepTables) return fail(HDX_E_INVALID, "%u region tables (at most %u)", ntables,
+                                               kMaxSweepTables);
+    if (ntables && (!tables || !region_ids)) return fail(HDX_E_INVALID, "NULL tables / region_ids");
+    for (uint32_t t = 0; t < ntables; ++t) {
+        if (!tables[t]) return fail(HDX_E_INVALID, "NULL table %u", t);
+        for (uint32_t d = 0; d < tables[t]->D; ++d)
+            if (tables[t]->attrs[d] >= attrs_sz)
+                return fail(HDX_E_INVALID, "table %u: subspace attribute %u >= attrs_sz %u", t,
+                            tables[t]->attrs[d], attrs_sz);
+    }
     if (n == 0) return HDX_OK;
-    if (!keys || !key_off || !key_len || !vals || !val_off || !val_len || !coords)
+    if (!keys || !key_off || !key_len || !vals || !val_off || !val_len || (!coords && !ntables))
         return fail(HDX_E_INVALID, "NULL device pointer");
     if ((st = bind_device(-1)) != HDX_OK) return st;
+    a.T = ntables;
+    for (uint32_t t = 0; t < ntables; ++t) {
+        const hdx_region_table tb = tables[t];
+        a.t[t].index = tb->d_index;
+        a.t[t].lower = tb->d_lower;
+        a.t[t].upper = tb->d_upper;
+        a.t[t].ids = tb->d_ids;
+        a.t[t].out = region_ids + (size_t)t * n;
+        a.t[t].W = tb->W;
+        a.t[t].D = tb->D;
+        a.t[t].R = tb->R;
+        a.t[t].index_words = tb->index_words;
+        std::memcpy(a.t[t].attrs, tb->attrs, sizeof a.t[t].attrs);
+    }
     a.keys = keys;
     a.key_off = key_off;
     a.key_len = key_len;
@@ -378,6 +401,29 @@ HDX_EXPORT hdx_status hdx_hash_encoded_device(const uint32_t* types, uint32_t at
     a.A = attrs_sz;
     HIP_TRY(launch_hash_encoded(a, (hipStream_t)stream));
     return HDX_OK;
+}
+
+HDX_EXPORT hdx_status hdx_hash_encoded_device(const uint32_t* types, uint32_t attrs_sz,
+                                              const uint8_t* keys, const uint64_t* key_off,
+                                              const uint32_t* key_len, const uint8_t* vals,
+                                              const uint64_t* val_off, const uint32_t* val_len,
+                                              uint64_t n, uint64_t* coords, uint64_t* versions,
+                                              uint32_t* status_dev, hdx_stream stream) {
+    return hash_encoded(types, attrs_sz, keys, key_off, key_len, vals, val_off, val_len, n, nullptr, 0, nullptr,
+                        coords, versions, status_dev, stream);
+}
+
+HDX_EXPORT hdx_status hdx_hash_encoded_regions_device(const uint32_t* types, uint32_t attrs_sz,
+                                                      const uint8_t* keys, const uint64_t* key_off,
+                                                      const uint32_t* key_len, const uint8_t* vals,
+                                                      const uint64_t* val_off, const uint32_t* val_len,
+                                                      uint64_t n, const hdx_region_table* tables,
+                                                      uint32_t ntables, uint64_t* region_ids, uint64_t* coords,
+                                                      uint64_t* versions, uint32_t* status_dev,
+                                                      hdx_stream stream) {
+    if (ntables == 0) return fail(HDX_E_INVALID, "no region tables");
+    return hash_encoded(types, attrs_sz, keys, key_off, key_len, vals, val_off, val_len, n, tables, ntables,
+                        region_ids, coords, versions, status_dev, stream);
 }
 
 HDX_EXPORT hdx_status hdx_hash_batch_host(const uint32_t* types, uint32_t attrs_sz,

@@ -20,10 +20,12 @@
 // inside its bytes yields zero coordinates and sets HDX_E_BADENC in status.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "hdx_device_hash.h"
 #include "hdx_internal.h"
 #include "hdx_loads.h"
+#include "hdx_region_lookup.h"
 
 namespace hdx {
 
@@ -50,6 +52,15 @@ struct alignas(8) EncDesc {
 };
 constexpr uint32_t kZeroSlot = 0xffffffffu;
 
+// HDX_SWEEP_REGION_LDS=0: the fused sweep reads the region tables from
+// global memory instead of staging them in LDS (A/B runs).
+static bool sweep_region_lds() {
+    static const bool v = [] {
+        const char* e = getenv("HDX_SWEEP_REGION_LDS");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
 // Wave-private LDS: G object bases {value, key}, the code table, descriptors.
 __host__ __device__ constexpr size_t encoded_lds_per_wave(uint32_t A, uint32_t G = 64) {
     return G * 16 + 256 + (size_t)G * A * sizeof(EncDesc);
@@ -57,21 +68,36 @@ __host__ __device__ constexpr size_t encoded_lds_per_wave(uint32_t A, uint32_t G
 
 // G objects per wave (lanes G..63 idle in phase 1).  SHAPE (debug variants
 // 57/58 only, wrong coordinates): 1 = the walk alone (no phase 2), 2 = phase
-// 2's loads without the hash arithmetic.
-template <bool TOUCH, bool A4 = false, int SHAPE = 0, int G = 64>
-__global__ void __launch_bounds__(256)
+// 2's loads without the hash arithmetic.  REGIONS: a wave holds all of its
+// objects' coordinates (G*A slots), so it also looks every object up in the
+// T region tables (hdx_region_lookup.h) — phase 2 parks each coordinate over
+// its consumed descriptor, phase 3 has one lane per object.
+template <bool TOUCH, bool A4 = false, int SHAPE = 0, int G = 64, bool REGIONS = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8)))
 hash_encoded_kernel(const EncodedArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
     const uint32_t A = a.A;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
+    // REGIONS: the tables' indexes and ids, one copy per workgroup, first
+    uint64_t* tbl = reinterpret_cast<uint64_t*>(smem_raw);
+    if constexpr (REGIONS) {
+        for (uint32_t t = 0; t < a.T; ++t) {
+            const SweepTable& tb = a.t[t];
+            if (tb.lds_index == 0xffffffffu) continue;
+            for (uint32_t k = threadIdx.x; k < tb.index_words; k += blockDim.x) tbl[tb.lds_index + k] = tb.index[k];
+            for (uint32_t k = threadIdx.x; k < tb.R; k += blockDim.x) tbl[tb.lds_ids + k] = tb.ids[k];
+        }
+        __syncthreads();  // the kernel's only workgroup barrier (before any wave may exit)
+    }
     // wave-private LDS: G object bases {value, key}, the code table, descriptors
-    uint8_t* wsmem = smem_raw + (size_t)w * encoded_lds_per_wave(A, G);
+    uint8_t* wsmem = smem_raw + (REGIONS ? (size_t)a.lds_tables * 8 : 0) + (size_t)w * encoded_lds_per_wave(A, G);
     uint64_t* bases = reinterpret_cast<uint64_t*>(wsmem);           // [G][2]
     uint8_t* codes = wsmem + G * 16;                                 // [256]
     EncDesc* desc = reinterpret_cast<EncDesc*>(wsmem + G * 16 + 256);
+    bool bad = false;
     const uint64_t o0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + w) * G;
-    if (o0 >= a.n) return;  // no workgroup barrier: waves are independent
+    if (o0 >= a.n) return;  // no barrier after this point: waves are independent
     const uint32_t nobj = (uint32_t)min<uint64_t>(G, a.n - o0);
     const bool valid = (uint32_t)lane < nobj;
     const uint64_t i = o0 + (valid ? lane : 0);
@@ -126,12 +152,13 @@ hash_encoded_kernel(const EncodedArgs a) {
     // phase 2: passes of 64 slots (slot s = object * A + attribute).  The object's bases and the attribute's code are
     // read from LDS, not from other lanes: in a partial pass the lanes past the
     // batch end are inactive, and a ds_bpermute from an inactive lane returns 0.
+    uint64_t* parked = reinterpret_cast<uint64_t*>(desc);  // REGIONS: coordinate of slot s over desc[s]
     const uint32_t npass = SHAPE == 1 ? 0 : (nslots + 63) / 64;
     if (SHAPE == 1) {
         for (uint32_t s = lane; s < nslots; s += 64) a.coords[o0 * A + s] = desc[s].off;
         return;
     }
-    uint64_t* out = a.coords + o0 * A;
+    uint64_t* out = a.coords ? a.coords + o0 * A : nullptr;
     struct Pass {
         const uint8_t* p;
         uint32_t n, code, s;
@@ -150,7 +177,6 @@ hash_encoded_kernel(const EncodedArgs a) {
         P.p = zero ? g_zero_pad : (j == 0 ? a.keys : a.vals) + base + d.off;
         P.blk = issue_any<A4>(P.code, P.p, P.n);
     };
-    bool bad = false;
     Pass P0, P1;
     load_pass(0, P0);
     for (uint32_t t = 0;; t += 2) {
@@ -158,31 +184,61 @@ hash_encoded_kernel(const EncodedArgs a) {
         {
             const uint64_t h = SHAPE == 2 ? touch_blk(P0.code, P0.p, P0.n, consume_any<A4>(P0.blk))
                                           : hash_blk<false, false, A4>(P0.code, P0.p, P0.n, consume_any<A4>(P0.blk), bad);
-            if (P0.s != 0xffffffffu) __builtin_nontemporal_store(h, out + P0.s);
+            if (P0.s != 0xffffffffu) {
+                if (!REGIONS || out) __builtin_nontemporal_store(h, out + P0.s);
+                if (REGIONS) parked[P0.s] = h;
+            }
         }
         if (t + 1 >= npass) break;
         if (t + 2 < npass) load_pass(t + 2, P0);
         {
             const uint64_t h = SHAPE == 2 ? touch_blk(P1.code, P1.p, P1.n, consume_any<A4>(P1.blk))
                                           : hash_blk<false, false, A4>(P1.code, P1.p, P1.n, consume_any<A4>(P1.blk), bad);
-            if (P1.s != 0xffffffffu) __builtin_nontemporal_store(h, out + P1.s);
+            if (P1.s != 0xffffffffu) {
+                if (!REGIONS || out) __builtin_nontemporal_store(h, out + P1.s);
+                if (REGIONS) parked[P1.s] = h;
+            }
         }
         if (t + 2 >= npass) break;
+    }
+    if constexpr (REGIONS) {
+        // phase 3: lane = object; configuration::lookup_region per table
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // one lane per (table, object) pair: G = 32 and T = 2 fill the wave
+        for (uint32_t k = lane; k < a.T * G; k += 64) {
+            const uint32_t t = k / G, o = k % G;
+            if (o >= nobj) continue;
+            const SweepTable& tb = a.t[t];
+            const uint64_t* po = parked + o * A;
+            if (tb.lds_index != 0xffffffffu) {
+                tb.out[o0 + o] = lookup_indexed_fn(tbl + tb.lds_index, tb.W, tb.D,
+                                                   [&](uint32_t d) { return po[tb.attrs[d]]; }, tbl + tb.lds_ids);
+                continue;
+            }
+            uint64_t h[kMaxLookupDims];
+#pragma unroll
+            for (uint32_t d = 0; d < kMaxLookupDims; ++d)
+                if (d < tb.D) h[d] = po[tb.attrs[d]];
+            tb.out[o0 + o] = tb.index ? lookup_indexed(tb.index, tb.W, tb.D, h, tb.ids)
+                                        : lookup_scan(tb.lower, tb.upper, tb.ids, tb.R, tb.D, h);
+        }
     }
     if (a.status && lane == 0 && any_bad) atomicOr(a.status, 1u << 6 /* HDX_E_BADENC */);
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <bool TOUCH, bool A4, int SHAPE = 0, int G = 64>
+template <bool TOUCH, bool A4, int SHAPE = 0, int G = 64, bool REGIONS = false>
 static hipError_t launch_encoded(const EncodedArgs& a, hipStream_t stream) {
     // 4 waves per workgroup while they fit in 64 KiB of LDS (A <= 28 at G = 64), else 1
     const size_t per_wave = encoded_lds_per_wave(a.A, G);
     const uint32_t waves_per_block = 4 * per_wave <= 65536 ? 4 : 1;
     const uint64_t waves = (a.n + G - 1) / G;
-    const uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
+    uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_encoded_kernel<TOUCH, A4, SHAPE, G>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
-                       waves_per_block * per_wave, stream, a);
+    hipLaunchKernelGGL((hash_encoded_kernel<TOUCH, A4, SHAPE, G, REGIONS>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
+                       waves_per_block * per_wave + (REGIONS ? (size_t)a.lds_tables * 8 : 0), stream, a);
     return hipGetLastError();
 }
 
@@ -198,6 +254,22 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
     // Retired (profiles/r1/ab_cfg5_*.jsonl): class-sorted passes over the whole
     // wave or over groups of 2 / 4 passes, 16 / 32 objects per wave, and a
     // lane-per-object walk-and-hash kernel — all slower
+    if (a.T) {
+        // stage each indexed table (index + ids) in LDS while they fit in 16 KiB together
+        uint32_t words = 0;
+        for (uint32_t t = 0; t < a.T; ++t) {
+            SweepTable& tb = a.t[t];
+            tb.lds_index = tb.lds_ids = 0xffffffffu;
+            const uint32_t need = tb.index_words + tb.R;
+            if (tb.index && sweep_region_lds() && (words + need) * 8 <= 16384) {
+                tb.lds_index = words;
+                tb.lds_ids = words + tb.index_words;
+                words += (need + 1) & ~1u;  // keep 16-byte alignment
+            }
+        }
+        a.lds_tables = words;
+        return launch_encoded<false, true, 0, 32, true>(a, stream);
+    }
     switch (hash_variant()) {
         case 43: return launch_encoded<false, false>(a, stream);
         case 33: return launch_encoded<true, false>(a, stream);

@@ -96,7 +96,20 @@ constexpr uint32_t kIndexMaxRegions = 256;
 void region_index_build(uint32_t D, uint32_t R, const uint64_t* lower, const uint64_t* upper,
                         std::vector<uint64_t>& index, uint32_t& W);
 
-// Stored-object sweep (hdx_encoded.hip): device arrays.
+// Stored-object sweep (hdx_encoded.hip): device arrays.  T region tables
+// (hdx_hash_encoded_regions_device): table t's region id of object i goes to
+// t[t].out[i]; coords may then be NULL.
+constexpr uint32_t kMaxSweepTables = 4;
+struct SweepTable {
+    const uint64_t* index;  // interval index (NULL: scan lower/upper)
+    const uint64_t* lower;
+    const uint64_t* upper;
+    const uint64_t* ids;
+    uint64_t* out;
+    uint32_t W, D, R, index_words;
+    uint32_t lds_index, lds_ids;  // u64 offsets of the LDS copies (launch_hash_encoded)
+    uint16_t attrs[16];
+};
 struct EncodedArgs {
     const uint8_t* keys;
     const uint64_t* key_off;
@@ -110,6 +123,8 @@ struct EncodedArgs {
     uint64_t n;
     uint32_t A;
     uint32_t a_magic;  // ceil(2^31 / A) (launch_hash_encoded fills it)
+    uint32_t T, lds_tables;  // lds_tables: u64 words of the workgroup's table copies
+    SweepTable t[kMaxSweepTables];
     uint8_t codes[HDX_MAX_ATTRS];
 };
 

@@ -15,10 +15,9 @@
 #include <algorithm>
 
 #include "hdx_internal.h"
+#include "hdx_region_lookup.h"
 
 namespace hdx {
-
-constexpr uint32_t kMaxLookupDims = 16;
 
 // ---------------------------------------------------------------------------
 // Interval index.  For every subspace dimension d the table's box edges
@@ -62,30 +61,6 @@ void region_index_build(uint32_t D, uint32_t R, const uint64_t* lower, const uin
     }
 }
 
-// Region id of coordinates h[0..D) through the interval index idx.
-__device__ __forceinline__ uint64_t lookup_indexed(const uint64_t* idx, uint32_t W, uint32_t D, const uint64_t* h,
-                                                   const uint64_t* ids) {
-    uint64_t acc[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-#pragma unroll
-    for (uint32_t d = 0; d < kMaxLookupDims; ++d) {
-        if (d >= D) break;
-        const uint64_t hdr = idx[d];
-        const uint32_t m = (uint32_t)(hdr & 0xffff);
-        const uint64_t* B = idx + ((hdr >> 16) & 0xffffff);
-        // number of boundaries <= h[d]: fixed-step binary search (same steps on every lane)
-        uint32_t pos = 0;
-        for (uint32_t step = m ? 1u << (31 - __builtin_clz(m)) : 0u; step; step >>= 1)
-            if (pos + step <= m && B[pos + step - 1] <= h[d]) pos += step;
-        const uint64_t* mask = idx + (hdr >> 40) + (size_t)pos * W;
-#pragma unroll
-        for (uint32_t w = 0; w < 4; ++w)
-            if (w < W) acc[w] &= mask[w];
-    }
-#pragma unroll
-    for (uint32_t w = 0; w < 4; ++w)
-        if (w < W && acc[w]) return ids[64 * w + __builtin_ctzll(acc[w])];
-    return 0;  // region_id()
-}
 
 template <bool IN_LDS, bool INDEX = false>
 __global__ void __launch_bounds__(256)

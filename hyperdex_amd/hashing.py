@@ -138,6 +138,36 @@ def hash_encoded(types, keys, key_off, key_len, vals, val_off, val_len, coords=N
     return coords
 
 
+def hash_encoded_regions(types, keys, key_off, key_len, vals, val_off, val_len, tables, coords=False,
+                         versions=None, status=None, stream=None):
+    """The sweep with the new regions in the same launch
+    (hdx_hash_encoded_regions_device): returns region ids (T, n) int64 for the
+    RegionTables `tables` (1..4), and the coordinates too when coords is True
+    (or a tensor to fill)."""
+    import torch
+
+    t = _u32_array(types)
+    A = len(t)
+    n = val_off.numel()
+    for x in (keys, key_off, key_len, vals, val_off, val_len):
+        assert x.is_cuda and x.is_contiguous()
+    dev = val_off.device
+    ids = torch.empty((len(tables), n), dtype=torch.int64, device=dev)
+    if coords is True:
+        coords = torch.empty((n, A), dtype=torch.int64, device=dev)
+    handles = (ctypes.c_void_p * max(len(tables), 1))(*[tb.handle.value for tb in tables])
+    if stream is None:
+        stream = torch.cuda.current_stream(dev)
+    handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+    check(lib().hdx_hash_encoded_regions_device(
+        t.ctypes.data, A, keys.data_ptr(), key_off.data_ptr(), key_len.data_ptr(), vals.data_ptr(),
+        val_off.data_ptr(), val_len.data_ptr(), n, handles, len(tables), ids.data_ptr(),
+        coords.data_ptr() if coords is not None and coords is not False else None,
+        versions.data_ptr() if versions is not None else None,
+        status.data_ptr() if status is not None else None, handle))
+    return (ids, coords) if coords is not None and coords is not False else ids
+
+
 def kernel_for(types, n: int):
     """(variant, kernel symbol) hash_batch would launch for this schema and n."""
     t = _u32_array(types)

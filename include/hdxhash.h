@@ -175,6 +175,22 @@ hdx_status hdx_lookup_region_device(hdx_region_table table, const uint64_t* coor
                                     uint32_t attrs_sz, uint64_t n, uint64_t* region_ids,
                                     hdx_stream stream);
 
+/* The sweep's purpose (daemon/datalayer_indexer_thread.cc): every stored
+ * object's region under a new subspace configuration.  One launch decodes,
+ * hashes and looks up: region_ids[t*n + i] = lookup_region(tables[t], the
+ * coordinates of object i) for t < ntables (1..4) — the values
+ * hdx_lookup_region_device would give on the coordinates hdx_hash_encoded_device
+ * computes (an undecodable object's are zero).  coords may be NULL: then no
+ * coordinate leaves the chip.  The tables' subspace attributes must be
+ * < attrs_sz.  Device pointers, asynchronous; attrs_sz <= 128. */
+hdx_status hdx_hash_encoded_regions_device(const uint32_t* types, uint32_t attrs_sz,
+                                           const uint8_t* keys, const uint64_t* key_off,
+                                           const uint32_t* key_len, const uint8_t* vals,
+                                           const uint64_t* val_off, const uint32_t* val_len,
+                                           uint64_t n, const hdx_region_table* tables,
+                                           uint32_t ntables, uint64_t* region_ids, uint64_t* coords,
+                                           uint64_t* versions, uint32_t* status_dev, hdx_stream stream);
+
 /* ---- secondary-index keys and search pruning ------------ */
 
 /* Bytes of one index key for `type`: 8 for INT64 and TIMESTAMP_*, 16 for

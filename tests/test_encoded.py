@@ -164,3 +164,37 @@ def test_gpu_encoded_every_variant(oracle, variant):
             assert np.array_equal(versions.cpu().numpy().view(np.uint64), wver), (cfg, n)
     finally:
         lib.hdxdbg_set_kernel_variant(prev)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_coords", [False, True])
+def test_gpu_encoded_regions_fused(oracle, with_coords):
+    """hdx_hash_encoded_regions_device = the sweep's coordinates looked up in
+    every table (an indexed 64-region key grid, an indexed 3-attribute grid,
+    and a 300-region table that is scanned), corrupt values included."""
+    import torch
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import RegionTable
+    dev = torch.device("cuda", 0)
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 3001, seed=31)
+    enc = synth.encode_values_host(types, blob, base, lens, first_version=9)
+    enc, _ = _corrupt(enc, np.random.default_rng(4))
+    want_coords, _, _ = oracle.hash_encoded(types, *enc)
+    rng = np.random.default_rng(5)
+    lo1, up1 = oracle.partition(1, 64)
+    lo3, up3 = oracle.partition(3, 64)
+    a = rng.integers(0, 2**64, size=(300, 2), dtype=np.uint64)
+    b = rng.integers(0, 2**64, size=(300, 2), dtype=np.uint64)
+    specs = [([0], lo1, up1), ([1, 2, 3], lo3, up3), ([16, 5], np.minimum(a, b), np.maximum(a, b))]
+    tables = [RegionTable(at, lo, up, np.arange(1, len(lo) + 1, dtype=np.uint64) * 7) for at, lo, up in specs]
+    out = hdx.hash_encoded_regions(types, *_to_dev(torch, dev, enc), tables, coords=with_coords)
+    torch.cuda.synchronize()
+    ids, coords = out if with_coords else (out, None)
+    for k, (at, lo, up) in enumerate(specs):
+        want = oracle.lookup_region(at, lo, up, np.arange(1, len(lo) + 1, dtype=np.uint64) * 7, want_coords)
+        assert np.array_equal(ids[k].cpu().numpy().view(np.uint64), want), k
+    if with_coords:
+        assert np.array_equal(coords.cpu().numpy().view(np.uint64), want_coords)
+    for t in tables:
+        t.close()
