@@ -135,8 +135,66 @@ def test_gpu_encoded_partial_last_pass(oracle, A, n):
     assert np.array_equal(got.cpu().numpy().view(np.uint64), want)
 
 
+def _scatter(enc, rng):
+    """The same objects with their keys and values moved to a shuffled order
+    with gaps between them (no group of objects is a contiguous run)."""
+    keys, key_off, key_len, vals, val_off, val_len = [np.array(x) for x in enc]
+
+    def move(buf, off, ln):
+        n = len(off)
+        order = rng.permutation(n)
+        out = np.zeros(int(ln.astype(np.int64).sum()) + 41 * n + 16, np.uint8)
+        new_off = np.zeros(n, np.uint64)
+        cur = int(rng.integers(0, 16))
+        for i in order:
+            L = int(ln[i])
+            out[cur:cur + L] = buf[int(off[i]):int(off[i]) + L]
+            new_off[i] = cur
+            cur += L + int(rng.integers(0, 41))
+        return out[:max(cur, 1)], new_off
+
+    keys2, key_off2 = move(keys, key_off, key_len)
+    vals2, val_off2 = move(vals, val_off, val_len)
+    return keys2, key_off2, key_len, vals2, val_off2, val_len
+
+
+def test_oracle_scattered_layout(oracle):
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 120, seed=4)
+    enc = synth.encode_values_host(types, blob, base, lens)
+    want = oracle.hash_encoded(types, *enc)
+    got = oracle.hash_encoded(types, *_scatter(enc, np.random.default_rng(3)))
+    assert all(np.array_equal(x, y) for x, y in zip(got, want))
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [-1, 33, 43, 47, 48])
+@pytest.mark.parametrize("variant", [-1, 64, 65, 66])
+def test_gpu_encoded_scattered_layout(oracle, variant):
+    """Objects whose keys and values are not contiguous runs (the LDS-staged
+    sweep's global fallback) hash exactly as the packed layout does."""
+    import torch
+
+    import hyperdex_amd as hdx
+    dev = torch.device("cuda", 0)
+    lib = hdx.lib()
+    prev = lib.hdxdbg_set_kernel_variant(variant)
+    assert prev != -2
+    try:
+        for cfg, n in (("cfg3b", 700), ("mixed", 300), ("cfg2", 129)):
+            types, blob, base, lens = synth.make_batch_host(cfg, n, seed=n + 11)
+            enc = synth.encode_values_host(types, blob, base, lens, first_version=9)
+            want, wver, _ = oracle.hash_encoded(types, *enc)
+            enc2 = _scatter(enc, np.random.default_rng(n))
+            versions = torch.zeros(n, dtype=torch.int64, device=dev)
+            got = hdx.hash_encoded(types, *_to_dev(torch, dev, enc2), versions=versions)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy().view(np.uint64), want), (cfg, n)
+            assert np.array_equal(versions.cpu().numpy().view(np.uint64), wver), (cfg, n)
+    finally:
+        lib.hdxdbg_set_kernel_variant(prev)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [-1, 33, 43, 47, 48, 64, 65, 66])
 def test_gpu_encoded_every_variant(oracle, variant):
     """Every stored-object sweep kernel (hdx_encoded.hip; 33 adds the line
     touch) is bit-exact on every config, on corrupt values, on ragged object
