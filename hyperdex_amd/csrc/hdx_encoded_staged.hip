@@ -181,6 +181,17 @@ __device__ __forceinline__ uint64_t readfirstlane64(uint64_t v) {
     return pack64(__builtin_amdgcn_readfirstlane((uint32_t)v), __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)));
 }
 
+// the regroup kernel's work classes in ORDER 1 (hdx_kernels.hip work_class):
+// numerics, 33..64, <= 16, 17..32, then > 64 B by loop blocks
+__device__ __forceinline__ uint32_t work_class1(uint32_t code, uint32_t n) {
+    if (code != CODE_STRING) return 0;
+    if (n > 64) {
+        const uint32_t b = (n - 1) >> 6;
+        return b >= 4 ? 7u : 3u + b;
+    }
+    return n > 32 ? 1u : n <= 16 ? 2u : 3u;
+}
+
 struct alignas(8) SDesc {
     uint32_t off;  // staged: byte offset in the window; global: offset in the value (key)
     uint32_t len;
@@ -446,6 +457,201 @@ hash_encoded_pipe_kernel(const EncodedArgs a, uint64_t ngroups) {
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
+// Ping-pong form (variants 74/75): the metadata of group g+1 is loaded one
+// whole iteration ahead into one of two register sets used alternately (no
+// copy of an in-flight load), and SORT hashes each staged group's slots in
+// work-class order (the regroup kernel's LDS fetch-add counting sort) with
+// the coordinates parked over their descriptors and stored in slot order.
+template <int G, int WB, bool SORT>
+__global__ void __launch_bounds__(64) hash_encoded_pp_kernel(const EncodedArgs a, uint64_t ngroups) {
+    static_assert(G <= 64 && WB % 1024 == 0 && WB < 65536, "group shape");
+    constexpr int U = WB / 1024;
+    constexpr int kCls = 8;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
+    const uint32_t A = a.A;
+    const int lane = threadIdx.x;
+    uint32_t* win = reinterpret_cast<uint32_t*>(smem_raw);
+    SDesc* desc = reinterpret_cast<SDesc*>(smem_raw + WB + 16);
+    uint64_t* bases = reinterpret_cast<uint64_t*>(smem_raw + WB + 16 + (size_t)G * A * sizeof(SDesc));
+    uint8_t* codes = reinterpret_cast<uint8_t*>(bases + 2 * G);
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(codes + 256);
+    uint16_t* perm = reinterpret_cast<uint16_t*>(cnt + 16);
+    uint64_t g = blockIdx.x;
+    if (g >= ngroups) return;  // every wave below runs its loop to ngroups: no barriers
+    reinterpret_cast<uint32_t*>(codes)[lane] = reinterpret_cast<const uint32_t*>(a.codes)[lane];
+
+    uint32_t bad = 0, any_bad = 0;
+    GroupMeta mA = load_meta<G>(a, g, lane);
+    GroupSpan s = make_span<G, WB>(a, mA, g, lane);
+    u64x2 r[U];
+    issue_window<U>(s, r, lane);
+    GroupMeta mB = load_meta<G>(a, g + gridDim.x < ngroups ? g + gridDim.x : g, lane);
+
+    // X = group g's metadata (loaded), Y = group g+1's (in flight)
+    auto body = [&](GroupMeta& X, const GroupMeta& Y) -> bool {
+        if (s.staged) store_window<U>(s, r, win, lane);
+        const uint64_t gn = g + gridDim.x;
+        const bool more = gn < ngroups;
+        GroupSpan sn = make_span<G, WB>(a, Y, more ? gn : g, lane);
+        if (!more) sn.units = 0;
+        issue_window<U>(sn, r, lane);
+        wave_lds_sync();
+
+        const uint64_t o0 = g * G;
+        const bool valid = (uint32_t)lane < s.nobj;
+        bool ok = valid && X.vlen >= 10;
+        uint64_t version = 0;
+        if (s.staged) {
+            const uint32_t vs = s.vsh + (uint32_t)(X.voff - s.vfirst);
+            const uint32_t ks = s.vunits * 16 + s.ksh + (uint32_t)(X.koff - s.kfirst);
+            if (ok) version = ((uint64_t)lds_be32(win, vs) << 32) | lds_be32(win, vs + 4);
+            ok = ok && (lds_be32(win, vs + 6) & 0xffffu) == A - 1;
+            if (valid) desc[lane * A] = SDesc{ks, X.klen};
+            uint32_t pos = 10;
+            for (uint32_t k = 0; k + 1 < A; ++k) {
+                uint32_t len = 0;
+                if (ok) {
+                    if (X.vlen - pos < 4) {
+                        ok = false;
+                    } else {
+                        len = lds_be32(win, vs + pos);
+                        pos += 4;
+                        if (len > X.vlen - pos) ok = false;  // the reference does not check this (:201-213)
+                    }
+                }
+                if (valid) desc[lane * A + 1 + k] = SDesc{ok ? vs + pos : kZero, ok ? len : 0u};
+                if (ok) pos += len;
+            }
+        } else {
+            const uint8_t* v = a.vals + X.voff;
+            if (valid) {
+                bases[2 * lane] = X.voff;
+                bases[2 * lane + 1] = X.koff;
+            }
+            if (ok) version = gload_be64(v);
+            ok = ok && gload_be16(v + 8) == A - 1;
+            if (valid) desc[lane * A] = SDesc{0u, X.klen};
+            uint32_t pos = 10;
+            for (uint32_t k = 0; k + 1 < A; ++k) {
+                uint32_t len = 0;
+                if (ok) {
+                    if (X.vlen - pos < 4) {
+                        ok = false;
+                    } else {
+                        len = gload_be32(v + pos);
+                        pos += 4;
+                        if (len > X.vlen - pos) ok = false;
+                    }
+                }
+                if (valid) desc[lane * A + 1 + k] = SDesc{ok ? pos : kZero, ok ? len : 0u};
+                if (ok) pos += len;
+            }
+        }
+        if (valid && !ok)
+            for (uint32_t j = 0; j < A; ++j) desc[lane * A + j] = SDesc{kZero, 0u};
+        if (valid && a.versions) a.versions[o0 + lane] = ok ? version : 0;
+        any_bad |= __any(valid && !ok) ? 1u : 0u;
+        // group g+2's metadata into X (dead now), a whole iteration ahead
+        const uint64_t g2 = gn + gridDim.x;
+        X = load_meta<G>(a, g2 < ngroups ? g2 : g, lane);
+        wave_lds_sync();
+
+        const uint32_t nslots = s.nobj * A;
+        const uint32_t npass = (nslots + 63) / 64;
+        uint64_t* out = a.coords + o0 * A;
+        const bool sorted = SORT && s.staged;
+        if (sorted) {
+            // counting sort of the group's slots by work class
+            if (lane < kCls) cnt[lane] = 0;
+            wave_lds_sync();
+            for (uint32_t t = 0; t < npass; ++t) {
+                const uint32_t sl = t * 64 + (uint32_t)lane;
+                if (sl < nslots) {
+                    const SDesc d = desc[sl];
+                    const uint32_t j = sl - div_small(sl, a.a_magic) * A;
+                    const uint32_t c = d.off == kZero ? 0u : work_class1(codes[j], d.len);
+                    __hip_atomic_fetch_add(&cnt[c], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                }
+            }
+            wave_lds_sync();
+            const uint32_t k = lane < kCls ? cnt[lane] : 0u;
+            const uint32_t start = wave_scan_dpp(k) - k;
+            if (lane < kCls) cnt[lane] = start;
+            wave_lds_sync();
+            for (uint32_t t = 0; t < npass; ++t) {
+                const uint32_t sl = t * 64 + (uint32_t)lane;
+                if (sl < nslots) {
+                    const SDesc d = desc[sl];
+                    const uint32_t j = sl - div_small(sl, a.a_magic) * A;
+                    const uint32_t c = d.off == kZero ? 0u : work_class1(codes[j], d.len);
+                    const uint32_t p = __hip_atomic_fetch_add(&cnt[c], 1u, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    perm[p] = (uint16_t)sl;
+                }
+            }
+            wave_lds_sync();
+        }
+        uint64_t* parked = reinterpret_cast<uint64_t*>(desc);
+        for (uint32_t t = 0; t < npass; ++t) {
+            const uint32_t q = t * 64 + (uint32_t)lane;
+            const bool live = q < nslots;
+            const uint32_t sl = !live ? nslots - 1 : sorted ? (uint32_t)perm[q] : q;
+            const uint32_t obj = div_small(sl, a.a_magic), j = sl - obj * A;
+            const SDesc d = desc[sl];
+            const bool zero = d.off == kZero || !live;
+            const uint32_t code = zero ? (uint32_t)CODE_ZERO : (uint32_t)codes[j];
+            const uint32_t n = zero ? 0u : d.len;
+            uint64_t h;
+            bool pbad = false;
+            if (s.staged) {
+                const uint32_t off = zero ? 0u : d.off;
+                h = hash_blk_lds(win, code, off, n, lds_block_a4(win, code, off, n), pbad);
+            } else {
+                const uint8_t* p = zero ? g_zero_pad
+                                        : (j == 0 ? a.keys : a.vals) + bases[2 * obj + (j == 0)] + d.off;
+                h = hash_blk<false, false, true>(code, p, n, funnel_raw(issue_block_a4(code, p, n)), pbad);
+            }
+            bad |= pbad ? 1u : 0u;
+            if (live) {
+                if (sorted) parked[sl] = h;  // over its own (consumed) descriptor
+                else __builtin_nontemporal_store(h, out + q);
+            }
+        }
+        if (sorted) {
+            wave_lds_sync();
+            for (uint32_t t = 0; t < npass; ++t) {
+                const uint32_t q = t * 64 + (uint32_t)lane;
+                if (q < nslots) __builtin_nontemporal_store(parked[q], out + q);
+            }
+        }
+        wave_lds_sync();  // this group's LDS reads precede the next group's writes
+        s = sn;
+        g = gn;
+        return more;
+    };
+    while (body(mA, mB) && body(mB, mA)) {
+    }
+    if (a.status && lane == 0 && any_bad) atomicOr(a.status, 1u << 6 /* HDX_E_BADENC */);
+    if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
+}
+
+template <int G, int WB, bool SORT>
+static hipError_t launch_pp(const EncodedArgs& a, hipStream_t stream) {
+    const uint64_t ngroups = (a.n + G - 1) / G;
+    const size_t lds = staged_lds_bytes(a.A, G, WB) + 64 + (size_t)G * a.A * 2;
+    int dev = 0, cus = 0, per_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, hash_encoded_pp_kernel<G, WB, SORT>, 64, lds);
+    if (e != hipSuccess) return e;
+    const uint64_t resident = (uint64_t)max(cus, 1) * (uint64_t)max(per_cu, 1);
+    const uint64_t blocks = ngroups < resident ? ngroups : resident;
+    hipLaunchKernelGGL((hash_encoded_pp_kernel<G, WB, SORT>), dim3((uint32_t)blocks), dim3(64), lds, stream, a,
+                       ngroups);
+    return hipGetLastError();
+}
+
 template <int G, int WB, int MODE = 0, int WPE = 1>
 static hipError_t launch_pipe(const EncodedArgs& a, hipStream_t stream) {
     const uint64_t ngroups = (a.n + G - 1) / G;
@@ -475,6 +681,8 @@ hipError_t launch_hash_encoded_staged(const EncodedArgs& a, hipStream_t stream, 
         case 68: return launch_pipe<7, 10240, 2>(a, stream);
         case 69: return launch_pipe<7, 10240, 3>(a, stream);
         case 70: return launch_pipe<7, 10240, 4>(a, stream);
+        case 74: return launch_pp<7, 10240, true>(a, stream);
+        case 75: return launch_pp<7, 10240, false>(a, stream);
         case 72: return launch_pipe<7, 10240, 0, 4>(a, stream);
         case 73: return launch_pipe<7, 10240, 0, 5>(a, stream);
         case 71: return launch_pipe<7, 10240, 5>(a, stream);  // versions must hold n + 4 * blocks entries
