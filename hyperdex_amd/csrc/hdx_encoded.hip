@@ -271,7 +271,6 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
         return launch_encoded<false, true, 0, 32, true>(a, stream);
     }
     switch (hash_variant()) {
-        case 64: case 65: case 66: case 67: case 68: case 69: case 70: case 71: case 72: case 73: case 74: case 75: return launch_hash_encoded_staged(a, stream, hash_variant());
         case 43: return launch_encoded<false, false>(a, stream);
         case 33: return launch_encoded<true, false>(a, stream);
         case 57: return launch_encoded<false, true, 1>(a, stream);  // debug shape: the walk alone

@@ -129,8 +129,6 @@ struct EncodedArgs {
 };
 
 hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream);
-// the LDS-staged form (hdx_encoded_staged.hip), variants 64-66
-hipError_t launch_hash_encoded_staged(const EncodedArgs& a, hipStream_t stream, int variant);
 
 // Index-key encoding (hdx_index.hip): n values of one INT64 / FLOAT /
 // TIMESTAMP_* attribute at blob + off[i], len[i] bytes; out holds n entries

@@ -34,7 +34,7 @@ def main():
     lib = hdx.lib()
     dev = torch.device("cuda", 0)
     variants = [int(v) for v in args.variants.split(",")]
-    checked = set(int(v) for v in args.check.split(",")) if args.check else set(variants) - {40, 41, 57, 58, 67, 68, 69, 70}
+    checked = set(int(v) for v in args.check.split(",")) if args.check else set(variants) - {40, 41, 57, 58}
     for cfg in args.configs.split(","):
         if cfg == "cfg5":  # stored-object sweep (variants 30-32)
             types, *enc = synth.make_encoded_device("cfg3b", args.objects, device=dev)

@@ -167,10 +167,10 @@ def test_oracle_scattered_layout(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [-1, 64, 74, 75])
+@pytest.mark.parametrize("variant", [-1, 43, 47])
 def test_gpu_encoded_scattered_layout(oracle, variant):
-    """Objects whose keys and values are not contiguous runs (the LDS-staged
-    sweep's global fallback) hash exactly as the packed layout does."""
+    """Objects whose keys and values lie in shuffled order with gaps hash
+    exactly as the packed layout does."""
     import torch
 
     import hyperdex_amd as hdx
@@ -194,7 +194,7 @@ def test_gpu_encoded_scattered_layout(oracle, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [-1, 33, 43, 47, 48, 64, 65, 66, 74, 75])
+@pytest.mark.parametrize("variant", [-1, 33, 43, 47, 48])
 def test_gpu_encoded_every_variant(oracle, variant):
     """Every stored-object sweep kernel (hdx_encoded.hip; 33 adds the line
     touch) is bit-exact on every config, on corrupt values, on ragged object
