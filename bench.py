@@ -44,6 +44,8 @@ def main():
                     help="skip the coordinates -> region ids step (SURVEY §8f-1)")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip timing the host-resident (PCIe-inclusive) path")
+    ap.add_argument("--no-stream-probe", action="store_true",
+                    help="skip the plain streaming-read probe (practical HBM ceiling)")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip timing config 3b (16 mixed attrs) beside the config-3a line")
     ap.add_argument("--traffic", default=latest_traffic_file(),
@@ -107,6 +109,9 @@ def main():
     torch.cuda.synchronize()
     log("rank %d: %s n=%d A=%d payload %.2f GB" % (rank, cfg, n, A, payload / 1e9))
 
+    # measured ceiling of this access shape beside the spec peak (uses coords
+    # as its store target, so it runs before the hash fills them)
+    sp = stream_probe(blob, coords, stream) if cfg != "cfg5" and not args.no_stream_probe else None
     for _ in range(args.warmup):
         launch()
     torch.cuda.synchronize()
@@ -167,6 +172,9 @@ def main():
                      "kernel": hdx.hashing.kernel_for(types, n)[1]},
     }
 
+    if sp is not None:
+        result["roofline"]["stream_probe"] = sp
+        result["roofline"]["frac_of_probe"] = round(achieved / sp["read_write_1to8_GBps"], 4)
     if cfg == "cfg5":
         result["roofline"]["kernel"] = "void hdx::hash_encoded_kernel<false, true, 0, 32>(hdx::EncodedArgs)"
     if world > 1 and not args.no_allgather:
@@ -290,6 +298,35 @@ def time_regions(coords, world, dev, backend, max_over_ranks, stream, gather, re
         res["allgather_ids_bytes"] = out.numel() * 8
     for t in tables:
         t.close()
+    return res
+
+
+def stream_probe(blob, sink, stream, reps=10):
+    """Practical HBM ceiling measured in the same run: a plain
+    streaming read of the batch's bytes in the hash kernels' access shape
+    (hdxdbg_stream_probe), alone and with one 8-byte store per 64 bytes read
+    (the hash's 1:8 write mix on 64-byte attributes)."""
+    import torch
+
+    import hyperdex_amd as hdx
+    lib = hdx.lib()
+    nbytes = (blob.numel() // 4096) * 4096
+    nbytes = min(nbytes, sink.numel() * 64 // 4096 * 4096)  # one sink word per 64 bytes read
+    res = {"bytes": nbytes}
+    for key, write in (("read_GBps", 0), ("read_write_1to8_GBps", 1)):
+        def go():
+            rc = lib.hdxdbg_stream_probe(blob.data_ptr(), nbytes, sink.data_ptr(), write, stream.cuda_stream)
+            assert rc == 0, rc
+        go()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        s.record(stream)
+        for _ in range(reps):
+            go()
+        e.record(stream)
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / reps
+        res[key] = round(nbytes * (1 + write / 8) / (ms / 1e3) / 1e9, 1)
     return res
 
 

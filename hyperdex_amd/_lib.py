@@ -70,6 +70,7 @@ SIGNATURES = [
     ("hdxdbg_set_kernel_variant", _i32, [_i32]),
     ("hdxdbg_kernel_variant", _i32, []),
     ("hdxdbg_kernel_for", _i32, [_vp, _u32, _u64, ctypes.POINTER(ctypes.c_char_p)]),
+    ("hdxdbg_stream_probe", _i32, [_vp, _u64, _vp, _i32, _vp]),
     ("hdx_synth_fill", _i32, [ctypes.POINTER(SynthRule), _u32, _u64, _u64, _u64, _vp, _vp, _vp,
                               _u64, _vp]),
 ]

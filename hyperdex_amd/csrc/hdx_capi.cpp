@@ -652,6 +652,12 @@ HDX_EXPORT hdx_status hdx_lookup_region_device(hdx_region_table t, const uint64_
 HDX_EXPORT int hdxdbg_set_kernel_variant(int variant) { return set_hash_variant(variant); }
 HDX_EXPORT int hdxdbg_kernel_variant(void) { return hash_variant(); }
 
+HDX_EXPORT int hdxdbg_stream_probe(const void* src, uint64_t bytes, uint64_t* sink, int write, void* stream) {
+    if (!src || (write && !sink) || bytes % 4096) return HDX_E_INVALID;
+    HIP_TRY(launch_stream_probe((const uint8_t*)src, bytes, sink, write, (hipStream_t)stream));
+    return HDX_OK;
+}
+
 HDX_EXPORT int hdxdbg_kernel_for(const uint32_t* types, uint32_t attrs_sz, uint64_t n, const char** name) {
     BatchArgs a{};
     if (check_schema(types, attrs_sz, a.codes) != HDX_OK) return -2;

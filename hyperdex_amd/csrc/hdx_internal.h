@@ -129,6 +129,9 @@ struct EncodedArgs {
 };
 
 hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream);
+// HBM streaming probe (hdx_synth.hip): read `bytes` (write = 1: plus one
+// 8-byte store per 64 bytes read into sink[bytes / 64]).
+hipError_t launch_stream_probe(const uint8_t* src, uint64_t bytes, uint64_t* sink, int write, hipStream_t s);
 
 // Index-key encoding (hdx_index.hip): n values of one INT64 / FLOAT /
 // TIMESTAMP_* attribute at blob + off[i], len[i] bytes; out holds n entries

@@ -21,6 +21,12 @@ int hdxdbg_kernel_variant(void);
  * count (under the current selection), and the kernel's symbol as rocprofv3
  * reports it (*name; static string).  Returns -2 on a bad schema. */
 int hdxdbg_kernel_for(const uint32_t* types, uint32_t attrs_sz, uint64_t n, const char** name);
+/* HBM streaming probe: read `bytes` (a multiple of 4096) of device memory at
+ * src in the hash kernels' access shape; write != 0 also stores one 8-byte
+ * word per 64 bytes read into sink[bytes / 64] (the 1:8 write mix of the
+ * 64-byte-attribute configs).  Asynchronous on `stream`.  bench.py reports the
+ * rate as the practical ceiling beside the HBM3E spec. */
+int hdxdbg_stream_probe(const void* src, uint64_t bytes, uint64_t* sink, int write, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,32 @@
+"""The committed evidence bench.py reads (profiles/r*/traffic.json) parses for
+every config it can be run on, and each rocprof kernel summary under
+profiles/ names kernels that exist in the built library."""
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_traffic_file_covers_every_bench_config():
+    sys.path.insert(0, ROOT)
+    import bench
+    path = bench.latest_traffic_file()
+    assert path, "no profiles/r*/traffic.json"
+    for cfg in ("cfg3a", "cfg3b", "cfg2", "cfg1", "cfg5"):
+        t = bench.measured_traffic(path, cfg, 10_000_000)
+        assert isinstance(t, int) and t > 0, (cfg, t)
+
+
+def test_default_profile_matches_default_kernel():
+    """profiles/<latest round>/default_bench_kernel_stats.csv holds the kernel
+    the default bench line names (roofline.kernel)."""
+    from hyperdex_amd import synth
+    from hyperdex_amd.hashing import kernel_for
+    rnd = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")))[-1]
+    stats = open(os.path.join(rnd, "default_bench_kernel_stats.csv")).read()
+    _, name = kernel_for([r.type for r in synth.CONFIGS["cfg3a"]], 10_000_000)
+    assert '"%s"' % name in stats, name
+    line = json.load(open(os.path.join(rnd, "default_bench_under_rocprof.json")))
+    assert line["roofline"]["kernel"] == name

@@ -1,5 +1,6 @@
 """libhdxhash.so loads on any host and exports exactly what include/hdxhash.h
 declares.  Host-only checks here; no compute call needs (or may fake) a GPU."""
+import ctypes
 import os
 import re
 import subprocess
@@ -137,3 +138,31 @@ def test_kernel_names_match_the_built_symbols():
         for n in (1000, 10_000_000):
             _, name = kernel_for(types, n)
             assert name in demangled, (name, sorted(demangled)[:5])
+
+
+def test_stream_probe_rejects_bad_sizes():
+    lib = hdx.lib()
+    from hyperdex_amd import _lib
+    assert lib.hdxdbg_stream_probe(None, 4096, None, 0, None) == _lib.HDX_E_INVALID
+    buf = ctypes.create_string_buffer(8192)
+    assert lib.hdxdbg_stream_probe(ctypes.addressof(buf), 1000, None, 0, None) == _lib.HDX_E_INVALID
+    assert lib.hdxdbg_stream_probe(ctypes.addressof(buf), 4096, None, 1, None) == _lib.HDX_E_INVALID
+
+
+@pytest.mark.gpu
+def test_stream_probe_writes_one_word_per_64_bytes():
+    """bench.py's streaming probe: with write = 1 word k of the sink is the XOR
+    of the four 16-byte pieces lane (k % 64) read from chunk k // 64, folded
+    to 64 bits."""
+    import numpy as np
+    import torch
+    lib = hdx.lib()
+    dev = torch.device("cuda", 0)
+    src = torch.randint(0, 256, (64 * 4096,), dtype=torch.uint8, device=dev)
+    sink = torch.zeros(src.numel() // 64, dtype=torch.int64, device=dev)
+    assert lib.hdxdbg_stream_probe(src.data_ptr(), src.numel(), sink.data_ptr(), 1, None) == 0
+    assert lib.hdxdbg_stream_probe(src.data_ptr(), src.numel(), sink.data_ptr(), 0, None) == 0
+    torch.cuda.synchronize()
+    w = src.cpu().numpy().view(np.uint64).reshape(-1, 8)  # 64 bytes per lane span
+    want = np.bitwise_xor.reduce(w, axis=1)
+    assert np.array_equal(sink.cpu().numpy().view(np.uint64), want)
