@@ -179,6 +179,8 @@ def main():
         result["roofline"]["kernel"] = "void hdx::hash_encoded_kernel<false, true, 0, 32>(hdx::EncodedArgs)"
     if world > 1 and not args.no_allgather:
         result["allgather"] = time_allgather(coords, world, dev, backend, max_over_ranks)
+        # hash phase then the coordinate exchange, back to back
+        result["allgather"]["end_to_end_ms"] = round(kernel_ms + result["allgather"]["ms"], 3)
     if not args.no_regions:
         result["regions"] = time_regions(coords, world, dev, backend, max_over_ranks, stream,
                                          gather=world > 1 and not args.no_allgather)
@@ -229,8 +231,23 @@ def time_allgather(coords, world, dev, backend, max_over_ranks, reps=3):
     torch.cuda.synchronize()
     (dt,) = max_over_ranks((time.perf_counter() - t0) / reps)
     nbytes = out.numel() * 8
-    return {"ms": round(dt * 1e3, 3), "bytes": nbytes, "backend": backend,
-            "busbw_GBps": round(nbytes * (world - 1) / world / dt / 1e9, 2)}
+    del out
+    res = {"ms": round(dt * 1e3, 3), "bytes": nbytes, "backend": backend,
+           "busbw_GBps": round(nbytes * (world - 1) / world / dt / 1e9, 2)}
+    # the cheaper "gather to host" alternative: every rank
+    # copies its own shard to pinned host memory at once
+    host = torch.empty(coords.shape, dtype=coords.dtype, pin_memory=True)
+    host.copy_(coords, non_blocking=True)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    host.copy_(coords, non_blocking=True)
+    torch.cuda.synchronize()
+    (d2h,) = max_over_ranks(time.perf_counter() - t0)
+    res["d2h_local_shard_ms"] = round(d2h * 1e3, 3)
+    res["d2h_GBps_per_gpu"] = round(coords.numel() * 8 / d2h / 1e9, 2)
+    del host
+    return res
 
 
 def key_subspace_tables(A):
