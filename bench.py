@@ -184,6 +184,11 @@ def main():
     if not args.no_regions:
         result["regions"] = time_regions(coords, world, dev, backend, max_over_ranks, stream,
                                          gather=world > 1 and not args.no_allgather)
+        if cfg != "cfg5" and A <= 128:
+            # ingest's purpose: regions, hashed + looked up in one launch
+            result["fused_regions"] = time_fused_batch(
+                types, blob, base, lens, n, A, dev, stream, max_over_ranks,
+                result["roofline"]["kernel_ms"], result["regions"]["lookup_ms"])
         if cfg == "cfg5":
             # the sweep's purpose: the new regions, decoded + hashed + looked up
             # in one launch with no coordinate written (hdx_hash_encoded_regions_device)
@@ -399,6 +404,30 @@ def time_fused_sweep(types, enc, n, A, dev, stream, max_over_ranks, sweep_ms, lo
         t.close()
     return {"tables": len(tables), "fused_ms": round(ms, 4),
             "separate_ms": round(sweep_ms + lookup_ms, 4),
+            "mobjects_per_s": round(n / (ms / 1e3) / 1e6, 2)}
+
+
+def time_fused_batch(types, blob, base, lens, n, A, dev, stream, max_over_ranks, hash_ms, lookup_ms, reps=10):
+    """hdx_hash_batch_regions_device over the same batch and the same two
+    tables as time_regions, coordinates not written (the ingest path needs
+    only the regions); next to the hash + separate lookups it replaces."""
+    import torch
+
+    import hyperdex_amd as hdx
+    tables = key_subspace_tables(A)
+    hdx.hash_batch_regions(types, blob, base, lens, tables, stream=stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    torch.cuda.synchronize()
+    for s, e in ev:
+        s.record(stream)
+        hdx.hash_batch_regions(types, blob, base, lens, tables, stream=stream)
+        e.record(stream)
+    torch.cuda.synchronize()
+    (ms,) = max_over_ranks(float(np.mean([s.elapsed_time(e) for s, e in ev])))
+    for t in tables:
+        t.close()
+    return {"tables": len(tables), "fused_ms": round(ms, 4),
+            "separate_ms": round(hash_ms + lookup_ms, 4),
             "mobjects_per_s": round(n / (ms / 1e3) / 1e6, 2)}
 
 

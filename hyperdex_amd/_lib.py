@@ -57,6 +57,7 @@ SIGNATURES = [
     ("hdx_lookup_region_device", _i32, [_vp, _vp, _u32, _u64, _vp, _vp]),
     ("hdx_hash_encoded_regions_device", _i32, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _u32,
                                                _vp, _vp, _vp, _vp, _vp]),
+    ("hdx_hash_batch_regions_device", _i32, [_vp, _u32, _vp, _vp, _vp, _u64, _vp, _u32, _vp, _vp, _vp, _vp]),
     ("hdx_index_key_size", ctypes.c_size_t, [_u32]),
     ("hdx_index_encode_device", _i32, [_u32, _vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     ("hdx_search_regions", _i32, [_vp, _vp, _u32, _vp, _vp]),

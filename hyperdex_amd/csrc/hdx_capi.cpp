@@ -426,6 +426,56 @@ HDX_EXPORT hdx_status hdx_hash_encoded_regions_device(const uint32_t* types, uin
                         region_ids, coords, versions, status_dev, stream);
 }
 
+HDX_EXPORT hdx_status hdx_hash_batch_regions_device(const uint32_t* types, uint32_t attrs_sz, const uint8_t* blob,
+                                                    const uint64_t* obj_base, const uint32_t* attr_len, uint64_t n,
+                                                    const hdx_region_table* tables, uint32_t ntables,
+                                                    uint64_t* region_ids, uint64_t* coords, uint32_t* status_dev,
+                                                    hdx_stream stream) {
+    if (ntables == 0) return fail(HDX_E_INVALID, "no region tables");
+    if (n && !attr_len) return fail(HDX_E_INVALID, "NULL device pointer");
+    BatchArgs args{};
+    hdx_status st = check_schema(types, attrs_sz, args.codes);
+    if (st != HDX_OK) return st;
+    if (attrs_sz > 128) return fail(HDX_E_INVALID, "attrs_sz=%u > 128 for the fused lookup", attrs_sz);
+    if (ntables > kMaxSweepTables)
+        return fail(HDX_E_INVALID, "%u region tables (at most %u)", ntables, kMaxSweepTables);
+    if (!tables || !region_ids) return fail(HDX_E_INVALID, "NULL tables / region_ids");
+    for (uint32_t t = 0; t < ntables; ++t) {
+        if (!tables[t]) return fail(HDX_E_INVALID, "NULL table %u", t);
+        for (uint32_t d = 0; d < tables[t]->D; ++d)
+            if (tables[t]->attrs[d] >= attrs_sz)
+                return fail(HDX_E_INVALID, "table %u: subspace attribute %u >= attrs_sz %u", t, tables[t]->attrs[d],
+                            attrs_sz);
+    }
+    if (n == 0) return HDX_OK;
+    if (!blob || !obj_base) return fail(HDX_E_INVALID, "NULL device pointer");
+    if ((st = bind_device(-1)) != HDX_OK) return st;
+    args.blob = blob;
+    args.obj_base = obj_base;
+    args.attr_len = attr_len;
+    args.coords = coords;
+    args.status = status_dev;
+    args.n = n;
+    args.A = attrs_sz;
+    finalize_args(args);
+    args.T = ntables;
+    for (uint32_t t = 0; t < ntables; ++t) {
+        const hdx_region_table tb = tables[t];
+        args.t[t].index = tb->d_index;
+        args.t[t].lower = tb->d_lower;
+        args.t[t].upper = tb->d_upper;
+        args.t[t].ids = tb->d_ids;
+        args.t[t].out = region_ids + (size_t)t * n;
+        args.t[t].W = tb->W;
+        args.t[t].D = tb->D;
+        args.t[t].R = tb->R;
+        args.t[t].index_words = tb->index_words;
+        std::memcpy(args.t[t].attrs, tb->attrs, sizeof args.t[t].attrs);
+    }
+    HIP_TRY(launch_hash_batch_regions(args, (hipStream_t)stream));
+    return HDX_OK;
+}
+
 HDX_EXPORT hdx_status hdx_hash_batch_host(const uint32_t* types, uint32_t attrs_sz,
                                           const uint8_t* blob, uint64_t blob_bytes,
                                           const uint64_t* obj_base, const uint32_t* attr_len,

@@ -23,6 +23,18 @@ enum : uint32_t {
 
 // Kernel arguments, passed by value (kernarg segment).  codes[] holds the
 // per-attribute dispatch class (hdx_device_hash.h CODE_*).
+constexpr uint32_t kMaxSweepTables = 4;
+struct SweepTable {
+    const uint64_t* index;  // interval index (NULL: scan lower/upper)
+    const uint64_t* lower;
+    const uint64_t* upper;
+    const uint64_t* ids;
+    uint64_t* out;
+    uint32_t W, D, R, index_words;
+    uint32_t lds_index, lds_ids;  // u64 offsets of the LDS copies (launch_hash_encoded)
+    uint16_t attrs[16];
+};
+
 struct BatchArgs {
     const uint8_t* blob;
     const uint64_t* obj_base;
@@ -36,9 +48,15 @@ struct BatchArgs {
     uint32_t a_magic;       // ceil(2^31 / A): t / A == (t * a_magic) >> 31 for t * A < 2^31
     uint32_t pad_;
     uint8_t codes[HDX_MAX_ATTRS];
+    // fused region lookup (hash_regroup_regions_kernel): T tables, K whole
+    // objects per wave, lds_tables u64 words of LDS table copies per workgroup
+    uint32_t T, K, lds_tables, pad2_;
+    SweepTable t[kMaxSweepTables];
 };
 
 hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream);
+// hash + lookup_region in one launch (args.T tables in args.t, A <= 128)
+hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream);
 // Fills args.uniform_code from args.codes[0..A), and inv_A / a_magic from A.
 void finalize_args(BatchArgs& args);
 // Kernel variants (hdx_kernels.hip, variant_kernel_name): the automatic policy's
@@ -99,17 +117,6 @@ void region_index_build(uint32_t D, uint32_t R, const uint64_t* lower, const uin
 // Stored-object sweep (hdx_encoded.hip): device arrays.  T region tables
 // (hdx_hash_encoded_regions_device): table t's region id of object i goes to
 // t[t].out[i]; coords may then be NULL.
-constexpr uint32_t kMaxSweepTables = 4;
-struct SweepTable {
-    const uint64_t* index;  // interval index (NULL: scan lower/upper)
-    const uint64_t* lower;
-    const uint64_t* upper;
-    const uint64_t* ids;
-    uint64_t* out;
-    uint32_t W, D, R, index_words;
-    uint32_t lds_index, lds_ids;  // u64 offsets of the LDS copies (launch_hash_encoded)
-    uint16_t attrs[16];
-};
 struct EncodedArgs {
     const uint8_t* keys;
     const uint64_t* key_off;

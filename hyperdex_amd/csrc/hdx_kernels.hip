@@ -24,6 +24,7 @@
 #include "hdx_device_hash.h"
 #include "hdx_internal.h"
 #include "hdx_loads.h"
+#include "hdx_region_lookup.h"
 
 namespace hdx {
 
@@ -150,11 +151,13 @@ struct RegroupLds {
 // A4: dword-aligned loads (hdx_loads.h); PIPE: the > 64-byte loop keeps the
 // next block in flight; ASORT: the class sort by LDS fetch-add instead of
 // ballot / mbcnt per (class, chunk).
-template <int C, bool NT_STORE, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false,
-          bool ASORT = false, int ORDER = 0>
-__global__ void __launch_bounds__(256)
-hash_regroup_kernel(const BatchArgs args) {
-    __shared__ RegroupLds<C> lds;
+// REG (hash_regroup_regions_kernel): a wave owns K = args.K whole objects
+// (K * A <= C * 64 slots) instead of C * 64 slots, parks every coordinate,
+// looks its objects up in the args.T region tables (configuration::
+// lookup_region, hdx_region_lookup.h; tbl = the workgroup's LDS copies) and
+// stores coordinates only when args.coords is set.
+template <int C, bool NT_STORE, bool SORT, bool DIRECT, bool A4, bool PIPE, bool ASORT, int ORDER, bool REG>
+__device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C>& lds, const uint64_t* tbl) {
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     SlotDesc* desc = lds.desc[w];
@@ -163,9 +166,18 @@ hash_regroup_kernel(const BatchArgs args) {
 
     const uint64_t wave = (uint64_t)blockIdx.x * 4 + w;
     const uint32_t A = args.A;
-    const uint64_t nslots = args.n * A;
-    const uint64_t qw = wave * (uint64_t)(C * 64);
-    if (qw >= nslots) return;  // no workgroup barrier anywhere: waves are independent
+    uint64_t qw, nslots, o_begin = 0, o_end = 0;  // nslots: end of this wave's slots
+    if constexpr (REG) {
+        o_begin = wave * args.K;
+        if (o_begin >= args.n) return;
+        o_end = min<uint64_t>(args.n, o_begin + args.K);
+        qw = o_begin * A;
+        nslots = o_end * A;
+    } else {
+        nslots = args.n * A;
+        qw = wave * (uint64_t)(C * 64);
+        if (qw >= nslots) return;  // no workgroup barrier anywhere: waves are independent
+    }
 
     uint64_t i0;
     uint32_t j0;
@@ -278,7 +290,7 @@ hash_regroup_kernel(const BatchArgs args) {
         if (t + 1 < C) load_pass(t + 1, nxt);
         const uint64_t h = hash_blk<PIPE, false, A4>(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n,
                                                      consume_any<A4>(cur.blk), bad);
-        if (DIRECT && uniform) {  // pass t is chunk t in slot order: store straight to HBM
+        if (DIRECT && uniform && !REG) {  // pass t is chunk t in slot order: store straight to HBM
             const uint64_t q = qw + t * 64 + lane;
             if (q < nslots) {
                 if (NT_STORE) __builtin_nontemporal_store(h, args.coords + q);
@@ -288,13 +300,42 @@ hash_regroup_kernel(const BatchArgs args) {
             res[2 * (cur.d.code_slot >> 8)] = h;
         }
     }
-    if (DIRECT && uniform) {
+    if (DIRECT && uniform && !REG) {
         if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
         return;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    if constexpr (REG) {
+        // ---- phase 2b: lookup_region, one lane per (table, object) ----------
+        const uint32_t K = args.K, nobj = (uint32_t)(o_end - o_begin);
+        for (uint32_t k = lane; k < args.T * K; k += 64) {
+            const uint32_t t = k / K, o = k - t * K;
+            if (o >= nobj) continue;
+            const SweepTable& tb = args.t[t];
+            const uint64_t* po = res + 2ull * o * A;
+            const auto coord = [&](uint32_t d) { return po[2 * tb.attrs[d]]; };
+            uint64_t id;
+            if (tb.lds_index != 0xffffffffu) {
+                id = lookup_indexed_fn(tbl + tb.lds_index, tb.W, tb.D, coord, tbl + tb.lds_ids);
+            } else if (tb.index) {
+                id = lookup_indexed_fn(tb.index, tb.W, tb.D, coord, tb.ids);
+            } else {
+                uint64_t h[kMaxLookupDims];
+#pragma unroll
+                for (uint32_t d = 0; d < kMaxLookupDims; ++d)
+                    if (d < tb.D) h[d] = coord(d);
+                id = lookup_scan(tb.lower, tb.upper, tb.ids, tb.R, tb.D, h);
+            }
+            tb.out[o_begin + o] = id;
+        }
+        if (!args.coords) {
+            if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
+            return;
+        }
+    }
 
     // ---- phase 3: coalesced stores in slot order -----------------------------
 #pragma unroll
@@ -307,6 +348,34 @@ hash_regroup_kernel(const BatchArgs args) {
         }
     }
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
+}
+
+template <int C, bool NT_STORE, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false,
+          bool ASORT = false, int ORDER = 0>
+__global__ void __launch_bounds__(256)
+hash_regroup_kernel(const BatchArgs args) {
+    __shared__ RegroupLds<C> lds;
+    regroup_body<C, NT_STORE, SORT, DIRECT, A4, PIPE, ASORT, ORDER, false>(args, lds, nullptr);
+}
+
+// hash + lookup_region in one launch (hdx_hash_batch_regions_device).  The
+// workgroup first copies the indexed tables that fit into LDS (its only
+// barrier, before any wave may leave).
+template <int C, bool SORT, bool A4, bool ASORT, int ORDER>
+__global__ void __launch_bounds__(256)
+hash_regroup_regions_kernel(const BatchArgs args) {
+    __shared__ RegroupLds<C> lds;
+    extern __shared__ __attribute__((aligned(16))) uint64_t tbl[];
+    if (args.lds_tables) {
+        for (uint32_t t = 0; t < args.T; ++t) {
+            const SweepTable& tb = args.t[t];
+            if (tb.lds_index == 0xffffffffu) continue;
+            for (uint32_t k = threadIdx.x; k < tb.index_words; k += blockDim.x) tbl[tb.lds_index + k] = tb.index[k];
+            for (uint32_t k = threadIdx.x; k < tb.R; k += blockDim.x) tbl[tb.lds_ids + k] = tb.ids[k];
+        }
+        __syncthreads();
+    }
+    regroup_body<C, true, SORT, true, A4, false, ASORT, ORDER, true>(args, lds, tbl);
 }
 
 template <int C, bool NT, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false,
@@ -352,6 +421,53 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 40: return launch_chunk<true, false, 1>(args, stream);  // debug shape: loads only
         case 41: return launch_chunk<true, false, 2>(args, stream);  // debug shape: arithmetic only
         default: return hipErrorInvalidValue;
+    }
+}
+
+template <int C, bool SORT, bool A4, bool ASORT, int ORDER>
+static hipError_t launch_regroup_regions(BatchArgs args, hipStream_t stream) {
+    // stage indexed tables in LDS while they fit in 16 KiB together and the
+    // workgroup's LDS stays within 80 KiB (two workgroups per CU)
+    uint32_t words = 0;
+    const bool room = sizeof(RegroupLds<C>) + 16384 <= 81920;
+    for (uint32_t t = 0; t < args.T; ++t) {
+        SweepTable& tb = args.t[t];
+        tb.lds_index = tb.lds_ids = 0xffffffffu;
+        const uint32_t need = tb.index_words + tb.R;
+        if (room && tb.index && (words + need) * 8 <= 16384) {
+            tb.lds_index = words;
+            tb.lds_ids = words + tb.index_words;
+            words += (need + 1) & ~1u;
+        }
+    }
+    args.lds_tables = words;
+    args.K = (C * 64) / args.A;
+    if (args.K == 0) return hipErrorInvalidValue;
+    const uint64_t waves = (args.n + args.K - 1) / args.K;
+    const uint64_t blocks = (waves + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((hash_regroup_regions_kernel<C, SORT, A4, ASORT, ORDER>), dim3((uint32_t)blocks), dim3(256),
+                       (size_t)words * 8, stream, args);
+    return hipGetLastError();
+}
+
+static int auto_variant(const BatchArgs& args);
+
+// The fused form follows the automatic policy's kind of pass shape with whole
+// objects per wave: uniform strings 8 unsorted chunks (the tables then fit in
+// LDS beside the descriptors: 1.97 vs 2.66 ms with 16 chunks and the tables in
+// global memory, config 3a); numeric-heavy 4 unsorted; complex types 8 sorted;
+// mixed strings 3 sorted with A4 loads (3.84 ms vs 4.32 / 3.89 / 4.15 with
+// 2 / 4 / 8, config 3b; profiles/r1/fused_batch_regions.jsonl).
+// A <= 128 (checked by the caller).
+hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream) {
+    if (args.n == 0) return hipSuccess;
+    switch (auto_variant(args)) {
+        case 25: case 20: case 12: return launch_regroup_regions<8, false, false, false, 0>(args, stream);
+        case 21: return launch_regroup_regions<4, false, false, false, 0>(args, stream);
+        case 46: return launch_regroup_regions<8, true, false, true, 1>(args, stream);
+        default: return launch_regroup_regions<3, true, true, true, 1>(args, stream);
     }
 }
 

@@ -168,6 +168,34 @@ def hash_encoded_regions(types, keys, key_off, key_len, vals, val_off, val_len, 
     return (ids, coords) if coords is not None and coords is not False else ids
 
 
+def hash_batch_regions(types, blob, obj_base, attr_len, tables, coords=False, status=None, stream=None):
+    """hash_batch fused with the region lookup (hdx_hash_batch_regions_device):
+    returns region ids (T, n) int64 for the RegionTables `tables` (1..4) of
+    the packed batch, and the coordinates too when coords is True (or a
+    tensor to fill)."""
+    import torch
+
+    t = _u32_array(types)
+    A = len(t)
+    n = obj_base.numel()
+    for x in (blob, obj_base, attr_len):
+        assert x.is_cuda and x.is_contiguous()
+    assert attr_len.numel() == n * A
+    dev = obj_base.device
+    ids = torch.empty((len(tables), n), dtype=torch.int64, device=dev)
+    if coords is True:
+        coords = torch.empty((n, A), dtype=torch.int64, device=dev)
+    handles = (ctypes.c_void_p * max(len(tables), 1))(*[tb.handle.value for tb in tables])
+    if stream is None:
+        stream = torch.cuda.current_stream(dev)
+    handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+    check(lib().hdx_hash_batch_regions_device(
+        t.ctypes.data, A, blob.data_ptr(), obj_base.data_ptr(), attr_len.data_ptr(), n, handles, len(tables),
+        ids.data_ptr(), coords.data_ptr() if coords is not None and coords is not False else None,
+        status.data_ptr() if status is not None else None, handle))
+    return (ids, coords) if coords is not None and coords is not False else ids
+
+
 def kernel_for(types, n: int):
     """(variant, kernel symbol) hash_batch would launch for this schema and n."""
     t = _u32_array(types)

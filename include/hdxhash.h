@@ -191,6 +191,21 @@ hdx_status hdx_hash_encoded_regions_device(const uint32_t* types, uint32_t attrs
                                            uint32_t ntables, uint64_t* region_ids, uint64_t* coords,
                                            uint64_t* versions, uint32_t* status_dev, hdx_stream stream);
 
+/* The batch form of the same fusion, for objects in the packed layout of
+ * hdx_hash_batch_device (blob / obj_base / attr_len): one launch hashes every
+ * object and looks it up in ntables (1..4) region tables — region_ids[t*n + i]
+ * = lookup_region(tables[t], hash(schema, key, value) of object i), what
+ * hdx_lookup_region_device gives on hdx_hash_batch_device's coordinates.
+ * coords may be NULL (then no coordinate leaves the chip: the ingest path
+ * key_state::hash_objects -> point_leader / lookup_region needs only the
+ * region).  Device pointers, asynchronous; attrs_sz <= 128; status_dev (may be
+ * NULL) gets HDX_E_BADSIZE's bit for a numeric value not 0 or 8 bytes long. */
+hdx_status hdx_hash_batch_regions_device(const uint32_t* types, uint32_t attrs_sz, const uint8_t* blob,
+                                         const uint64_t* obj_base, const uint32_t* attr_len, uint64_t n,
+                                         const hdx_region_table* tables, uint32_t ntables,
+                                         uint64_t* region_ids, uint64_t* coords, uint32_t* status_dev,
+                                         hdx_stream stream);
+
 /* ---- secondary-index keys and search pruning ------------ */
 
 /* Bytes of one index key for `type`: 8 for INT64 and TIMESTAMP_*, 16 for

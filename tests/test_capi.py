@@ -166,3 +166,15 @@ def test_stream_probe_writes_one_word_per_64_bytes():
     w = src.cpu().numpy().view(np.uint64).reshape(-1, 8)  # 64 bytes per lane span
     want = np.bitwise_xor.reduce(w, axis=1)
     assert np.array_equal(sink.cpu().numpy().view(np.uint64), want)
+
+
+def test_batch_regions_argument_checks():
+    """hdx_hash_batch_regions_device rejects a call without tables or
+    lengths before touching a device."""
+    lib = hdx.lib()
+    t = np.array([9217, 9218], dtype=np.uint32)
+    assert lib.hdx_hash_batch_regions_device(t.ctypes.data, 2, None, None, None, 5, None, 0, None, None,
+                                             None, None) == _lib.HDX_E_INVALID
+    one = (ctypes.c_void_p * 1)(1)
+    assert lib.hdx_hash_batch_regions_device(t.ctypes.data, 2, 1, 1, None, 5, one, 1, 1, None,
+                                             None, None) == _lib.HDX_E_INVALID

@@ -137,3 +137,44 @@ def test_gpu_hash_then_point_leader(oracle):
     want = oracle.lookup_region([0], lo, up, ids, coords.cpu().numpy().view(np.uint64))
     assert np.array_equal(got.cpu().numpy().view(np.uint64), want)
     assert (want != 0).all()  # the key grid covers the whole space
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cfg,n,with_coords", [("cfg3a", 3001, False), ("cfg3b", 2999, True), ("cfg2", 4097, False),
+                                               ("mixed", 1000, True), ("cfg1", 65, True), ("cfg3b", 1, False)])
+def test_gpu_batch_regions_fused(oracle, cfg, n, with_coords):
+    """hdx_hash_batch_regions_device = hash_batch's coordinates looked up in
+    every table (indexed key grid, indexed 3-attribute grid, a scanned
+    300-region table), with and without the coordinates written."""
+    import numpy as np
+    import torch
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import RegionTable, synth
+    dev = torch.device("cuda", 0)
+    types, blob, base, lens = synth.make_batch_host(cfg, n, seed=n + 17)
+    want_coords, _ = oracle.hash_batch(types, blob, base, lens)
+    A = len(types)
+    rng = np.random.default_rng(n)
+    lo1, up1 = oracle.partition(1, 64)
+    specs = [([0], lo1, up1)]
+    if A >= 4:
+        lo3, up3 = oracle.partition(3, 64)
+        specs.append(([1, 2, 3], lo3, up3))
+    a = rng.integers(0, 2**64, size=(300, 2), dtype=np.uint64)
+    b = rng.integers(0, 2**64, size=(300, 2), dtype=np.uint64)
+    specs.append(([A - 1, 0], np.minimum(a, b), np.maximum(a, b)))
+    tables = [RegionTable(at, lo, up, np.arange(1, len(lo) + 1, dtype=np.uint64) * 3) for at, lo, up in specs]
+    d_blob = torch.from_numpy(np.ascontiguousarray(blob) if len(blob) else np.zeros(1, np.uint8)).to(dev)
+    d_base = torch.from_numpy(base.view(np.int64)).to(dev)
+    d_lens = torch.from_numpy(lens.view(np.int32)).to(dev)
+    out = hdx.hash_batch_regions(types, d_blob, d_base, d_lens, tables, coords=with_coords)
+    torch.cuda.synchronize()
+    ids, coords = out if with_coords else (out, None)
+    for k, (at, lo, up) in enumerate(specs):
+        want = oracle.lookup_region(at, lo, up, np.arange(1, len(lo) + 1, dtype=np.uint64) * 3, want_coords)
+        assert np.array_equal(ids[k].cpu().numpy().view(np.uint64), want), k
+    if with_coords:
+        assert np.array_equal(coords.cpu().numpy().view(np.uint64), want_coords)
+    for t in tables:
+        t.close()
