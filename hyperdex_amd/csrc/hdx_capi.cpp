@@ -1,9 +1,9 @@
 // hdx_capi.cpp — C-ABI of libhdxhash.so (include/hdxhash.h).
 //
 // Host side of the engine: argument validation, the hyperdatatype -> dispatch
-// code table, per-thread streams, the pipelined host-resident batch path and
-// the per-object entry points that mirror common/hash.h.  Every compute entry
-// point runs the gfx950 kernels; there is no CPU hashing code in this library.
+// code table, per-thread streams and the pipelined host-resident batch path.
+// Every batch entry point runs the gfx950 kernels, with no CPU substitute; the
+// per-object entry points that mirror common/hash.h are hdx_cpu.cpp's.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -17,6 +17,10 @@
 
 #include "hdx_host.h"
 #include "../../include/hdxhash_debug.h"
+
+#ifndef HDX_DEBUG_BUILD
+#define HDX_DEBUG_BUILD 0
+#endif
 
 
 namespace hdx {
@@ -96,8 +100,24 @@ static void probe() {
     }
 }
 
-struct ThreadState {
+// Per-thread device scratch (streams, host-path staging) and the search
+// staging of hdx_capi_index.cpp register here, so hdx_shutdown can free every
+// thread's scratch, not only the caller's.
+static std::mutex g_scratch_mu;
+static std::vector<Scratch*> g_scratch;
+
+void track_scratch(Scratch* s) {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    g_scratch.push_back(s);
+}
+void untrack_scratch(Scratch* s) {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    g_scratch.erase(std::remove(g_scratch.begin(), g_scratch.end(), s), g_scratch.end());
+}
+
+struct ThreadState : Scratch {
     int device = -1;
+    bool tracked = false;
     hipStream_t stream = nullptr;
     // host-path pipeline: two slots, each with device + pinned staging
     struct Slot {
@@ -110,8 +130,8 @@ struct ThreadState {
         uint64_t* h_coords = nullptr; size_t cap_hcoords = 0;
         uint32_t* h_len = nullptr; size_t cap_hlen = 0;
     } slot[2];
-    uint32_t* d_status = nullptr;
-    ~ThreadState() {
+    // Frees everything and unbinds the thread (it rebinds lazily on its next call).
+    void release() override {
         if (device < 0) return;
         (void)hipSetDevice(device);
         for (auto& s : slot) {
@@ -121,9 +141,18 @@ struct ThreadState {
             (void)hipHostFree(s.h_base); (void)hipHostFree(s.h_blob);
             (void)hipHostFree(s.h_coords); (void)hipHostFree(s.h_len);
             if (s.s) (void)hipStreamDestroy(s.s);
+            s = Slot{};
         }
-        (void)hipFree(d_status);
-        if (stream) (void)hipStreamDestroy(stream);
+        if (stream) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipStreamDestroy(stream);
+        }
+        stream = nullptr;
+        device = -1;
+    }
+    ~ThreadState() {
+        if (tracked) untrack_scratch(this);
+        release();
     }
 };
 static thread_local ThreadState t_state;
@@ -143,6 +172,10 @@ hdx_status bind_device(int want /* -1: current */) {
         if (t_state.device >= 0)
             return fail(HDX_E_INVALID, "thread already bound to device %d", t_state.device);
         t_state.device = dev;
+        if (!t_state.tracked) {
+            track_scratch(&t_state);
+            t_state.tracked = true;
+        }
     }
     return HDX_OK;
 }
@@ -312,6 +345,29 @@ HDX_EXPORT hdx_status hdx_init(int device) {
     return bind_device(device);
 }
 
+HDX_EXPORT hdx_status hdx_init_mask(uint64_t device_mask) {
+    std::call_once(g_probe_once, probe);
+    if (device_mask == 0) return fail(HDX_E_INVALID, "empty device mask");
+    if (g_ndev <= 0) return fail(HDX_E_DEVICE, "no HIP device visible");
+    int first = -1;
+    for (int d = 0; d < 64; ++d) {
+        if (!(device_mask >> d & 1)) continue;
+        if (d >= g_ndev) return fail(HDX_E_INVALID, "device %d in the mask >= device count %d", d, g_ndev);
+        if (!g_is_gfx950[d]) return fail(HDX_E_DEVICE, "device %d is not gfx950 (MI355X)", d);
+        if (first < 0) first = d;
+    }
+    hdx_status st = bind_device(first);
+    if (st != HDX_OK) return st;
+    hipStream_t s;
+    return thread_stream(&s);
+}
+
+HDX_EXPORT hdx_status hdx_shutdown(void) {
+    std::lock_guard<std::mutex> lk(g_scratch_mu);
+    for (Scratch* s : g_scratch) s->release();
+    return HDX_OK;
+}
+
 HDX_EXPORT hdx_status hdx_sync(hdx_stream stream) {
     hdx_status st = bind_device(-1);
     if (st != HDX_OK) return st;
@@ -351,6 +407,16 @@ HDX_EXPORT hdx_status hdx_hash_batch_device(const uint32_t* types, uint32_t attr
     return HDX_OK;
 }
 
+// Region tables live on the device they were created on; a fused launch on
+// another device would read that device's memory (the batcher checks the same).
+static hdx_status check_table_devices(const hdx_region_table* tables, uint32_t ntables) {
+    for (uint32_t t = 0; t < ntables; ++t)
+        if (tables[t]->device != t_state.device)
+            return fail(HDX_E_INVALID, "region table %u was created on device %d, the call runs on device %d", t,
+                        tables[t]->device, t_state.device);
+    return HDX_OK;
+}
+
 static hdx_status hash_encoded(const uint32_t* types, uint32_t attrs_sz, const uint8_t* keys,
                                const uint64_t* key_off, const uint32_t* key_len, const uint8_t* vals,
                                const uint64_t* val_off, const uint32_t* val_len, uint64_t n,
@@ -374,6 +440,7 @@ static hdx_status hash_encoded(const uint32_t* types, uint32_t attrs_sz, const u
     if (!keys || !key_off || !key_len || !vals || !val_off || !val_len || (!coords && !ntables))
         return fail(HDX_E_INVALID, "NULL device pointer");
     if ((st = bind_device(-1)) != HDX_OK) return st;
+    if ((st = check_table_devices(tables, ntables)) != HDX_OK) return st;
     a.T = ntables;
     for (uint32_t t = 0; t < ntables; ++t) {
         const hdx_region_table tb = tables[t];
@@ -450,6 +517,7 @@ HDX_EXPORT hdx_status hdx_hash_batch_regions_device(const uint32_t* types, uint3
     if (n == 0) return HDX_OK;
     if (!blob || !obj_base) return fail(HDX_E_INVALID, "NULL device pointer");
     if ((st = bind_device(-1)) != HDX_OK) return st;
+    if ((st = check_table_devices(tables, ntables)) != HDX_OK) return st;
     args.blob = blob;
     args.obj_base = obj_base;
     args.attr_len = attr_len;
@@ -490,48 +558,8 @@ HDX_EXPORT hdx_status hdx_hash_batch_host(const uint32_t* types, uint32_t attrs_
     return hash_host(codes, attrs_sz, blob ? blob : &one, blob_bytes, obj_base, attr_len, n, coords);
 }
 
-HDX_EXPORT hdx_status hdx_hash_object(const uint32_t* types, uint32_t attrs_sz,
-                                      const uint8_t* key, size_t key_len,
-                                      const uint8_t* const* values, const size_t* value_lens,
-                                      uint64_t* hs) {
-    uint8_t codes[HDX_MAX_ATTRS];
-    hdx_status st = check_schema(types, attrs_sz, codes);
-    if (st != HDX_OK) return st;
-    if (!hs || (!key && key_len) || (attrs_sz > 1 && (!values || !value_lens)))
-        return fail(HDX_E_INVALID, "NULL pointer");
-    // Pack {key, value[0..A-2]} contiguously: one object, one launch.
-    uint64_t total = key_len;
-    uint32_t lens[HDX_MAX_ATTRS];
-    lens[0] = (uint32_t)key_len;
-    if (key_len >= (1ull << 32)) return fail(HDX_E_INVALID, "key of %zu bytes", key_len);
-    for (uint32_t j = 1; j < attrs_sz; ++j) {
-        if (value_lens[j - 1] >= (1ull << 32))
-            return fail(HDX_E_INVALID, "value of %zu bytes", value_lens[j - 1]);
-        lens[j] = (uint32_t)value_lens[j - 1];
-        total += lens[j];
-    }
-    std::vector<uint8_t> packed(std::max<uint64_t>(total, 1));
-    uint64_t off = 0;
-    if (key_len) std::memcpy(packed.data(), key, key_len);
-    off = key_len;
-    for (uint32_t j = 1; j < attrs_sz; ++j) {
-        if (lens[j]) std::memcpy(packed.data() + off, values[j - 1], lens[j]);
-        off += lens[j];
-    }
-    const uint64_t base = 0;
-    return hash_host(codes, attrs_sz, packed.data(), total, &base, lens, 1, hs);
-}
-
-HDX_EXPORT hdx_status hdx_hash_key(const uint32_t* types, uint32_t attrs_sz, const uint8_t* key,
-                                   size_t key_len, uint64_t* h) {
-    if (!types || attrs_sz == 0) return fail(HDX_E_INVALID, "empty schema");
-    (void)attrs_sz;
-    return hdx_hash_object(types, 1, key, key_len, nullptr, nullptr, h);
-}
-
-HDX_EXPORT hdx_status hdx_hash_value(uint32_t type, const uint8_t* data, size_t len, uint64_t* out) {
-    return hdx_hash_object(&type, 1, data, len, nullptr, nullptr, out);
-}
+// hdx_hash_value / hdx_hash_key / hdx_hash_object: the per-object entry points
+// run on the host CPU (hdx_cpu.cpp).
 
 HDX_EXPORT hdx_status hdx_alloc_pinned(size_t bytes, void** out) {
     if (!out) return fail(HDX_E_INVALID, "out is NULL");
@@ -605,11 +633,15 @@ HDX_EXPORT hdx_status hdx_synth_fill(const hdx_synth_rule* rules, uint32_t attrs
 
 // ---- region tables (hdx_regions.hip) ----------------------------------------
 
-// HDX_REGION_SCAN=1 (A/B only): tables created afterwards keep no interval
-// index, so lookups scan the boxes as the reference does.
+// Debug library only: HDX_REGION_SCAN=1 (A/B runs) — tables created afterwards
+// keep no interval index, so lookups scan the boxes as the reference does.
 static bool region_index_disabled() {
+#if HDX_DEBUG_BUILD
     const char* e = getenv("HDX_REGION_SCAN");
     return e && *e == '1';
+#else
+    return false;
+#endif
 }
 
 
@@ -679,6 +711,7 @@ HDX_EXPORT hdx_status hdx_lookup_region_device(hdx_region_table t, const uint64_
             return fail(HDX_E_INVALID, "subspace attribute %u >= attrs_sz %u", t->attrs[d], attrs_sz);
     hdx_status st = bind_device(-1);
     if (st != HDX_OK) return st;
+    if ((st = check_table_devices(&t, 1)) != HDX_OK) return st;
     RegionArgs a{};
     a.lower = t->d_lower;
     a.upper = t->d_upper;
@@ -699,8 +732,10 @@ HDX_EXPORT hdx_status hdx_lookup_region_device(hdx_region_table t, const uint64_
 
 // ---- tuning hooks (include/hdxhash_debug.h) --------------------------------
 
+#if HDX_DEBUG_BUILD
 HDX_EXPORT int hdxdbg_set_kernel_variant(int variant) { return set_hash_variant(variant); }
 HDX_EXPORT int hdxdbg_kernel_variant(void) { return hash_variant(); }
+#endif
 
 HDX_EXPORT int hdxdbg_stream_probe(const void* src, uint64_t bytes, uint64_t* sink, int write, void* stream) {
     if (!src || (write && !sink) || bytes % 4096) return HDX_E_INVALID;

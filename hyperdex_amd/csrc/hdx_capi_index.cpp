@@ -24,16 +24,24 @@ int index_code(uint32_t type) {
 // Per-thread staging for hdx_search_regions: one pinned block
 // [endpoints | obj_base | attr_len | hashes | include | cleared/status] and
 // its device twin, so a search is one H2D, two launches and one D2H.
-struct SearchStage {
+struct SearchStage : Scratch {
     int device = -1;
+    bool tracked = false;
     uint8_t* host = nullptr;
     uint8_t* dev = nullptr;
     size_t cap = 0;
-    ~SearchStage() {
+    void release() override {
         if (device < 0) return;
         (void)hipSetDevice(device);
         (void)hipHostFree(host);
         (void)hipFree(dev);
+        host = dev = nullptr;
+        cap = 0;
+        device = -1;
+    }
+    ~SearchStage() {
+        if (tracked) untrack_scratch(this);
+        release();
     }
 };
 thread_local SearchStage t_search;
@@ -72,7 +80,7 @@ HDX_EXPORT hdx_status hdx_index_encode_device(uint32_t type, const uint8_t* blob
 }
 
 HDX_EXPORT hdx_status hdx_search_regions(hdx_region_table t, const hdx_range* ranges, uint32_t nranges,
-                                         uint8_t* include, int* cleared) {
+                                         const uint8_t* has_replicas, uint8_t* include, int* cleared) {
     if (!t || !cleared || (nranges && !ranges) || (t->R && !include))
         return fail(HDX_E_INVALID, "NULL pointer");
     *cleared = 0;
@@ -120,8 +128,8 @@ HDX_EXPORT hdx_status hdx_search_regions(hdx_region_table t, const hdx_range* ra
         ++a.m;
     }
     if (t->R == 0) return HDX_OK;
-    if (a.m == 0) {
-        std::memset(include, 1, t->R);
+    if (a.m == 0) {  // no range names this subspace: every region with replicas
+        for (uint32_t r = 0; r < t->R; ++r) include[r] = has_replicas ? (has_replicas[r] != 0) : 1;
         return HDX_OK;
     }
     hdx_status st = bind_device(t->device);
@@ -134,7 +142,8 @@ HDX_EXPORT hdx_status hdx_search_regions(hdx_region_table t, const hdx_range* ra
     const size_t o_base = align_up(ep_bytes + 16, 16);
     const size_t o_len = o_base + 8;
     const size_t o_hash = align_up(o_len + 4 * A, 16);
-    const size_t o_incl = o_hash + 8 * A;
+    const size_t o_rep = o_hash + 8 * A;
+    const size_t o_incl = align_up(o_rep + (has_replicas ? t->R : 0), 16);
     const size_t o_flag = align_up(o_incl + t->R, 16);
     const size_t need = o_flag + 16;
     SearchStage& g = t_search;
@@ -151,6 +160,10 @@ HDX_EXPORT hdx_status hdx_search_regions(hdx_region_table t, const hdx_range* ra
         }
         g.cap = cap;
         g.device = t->device;
+        if (!g.tracked) {
+            track_scratch(&g);
+            g.tracked = true;
+        }
     }
     BatchArgs b{};
     uint64_t pos = 0;
@@ -176,6 +189,7 @@ HDX_EXPORT hdx_status hdx_search_regions(hdx_region_table t, const hdx_range* ra
         b.codes[2 * k + 1] = ce;
     }
     *reinterpret_cast<uint64_t*>(g.host + o_base) = 0;
+    if (has_replicas) std::memcpy(g.host + o_rep, has_replicas, t->R);
     std::memset(g.host + o_flag, 0, 16);
     HIP_TRY(hipMemcpyAsync(g.dev, g.host, need, hipMemcpyHostToDevice, s));
     b.blob = g.dev;
@@ -191,6 +205,7 @@ HDX_EXPORT hdx_status hdx_search_regions(hdx_region_table t, const hdx_range* ra
     a.upper = t->d_upper;
     a.hashes = b.coords;
     a.include = g.dev + o_incl;
+    a.replicas = has_replicas ? g.dev + o_rep : nullptr;
     a.cleared = reinterpret_cast<uint32_t*>(g.dev + o_flag);
     a.R = t->R;
     a.D = t->D;

@@ -52,14 +52,22 @@ struct alignas(8) EncDesc {
 };
 constexpr uint32_t kZeroSlot = 0xffffffffu;
 
-// HDX_SWEEP_REGION_LDS=0: the fused sweep reads the region tables from
-// global memory instead of staging them in LDS (A/B runs).
+#ifndef HDX_DEBUG_BUILD
+#define HDX_DEBUG_BUILD 0
+#endif
+
+// Debug library only: HDX_SWEEP_REGION_LDS=0 makes the fused sweep read the
+// region tables from global memory instead of staging them in LDS (A/B runs).
 static bool sweep_region_lds() {
+#if HDX_DEBUG_BUILD
     static const bool v = [] {
         const char* e = getenv("HDX_SWEEP_REGION_LDS");
         return !(e && e[0] == '0');
     }();
     return v;
+#else
+    return true;
+#endif
 }
 // Wave-private LDS: G object bases {value, key}, the code table, descriptors.
 __host__ __device__ constexpr size_t encoded_lds_per_wave(uint32_t A, uint32_t G = 64) {
@@ -270,15 +278,18 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
         a.lds_tables = words;
         return launch_encoded<false, true, 0, 32, true>(a, stream);
     }
+#if HDX_DEBUG_BUILD
     switch (hash_variant()) {
         case 43: return launch_encoded<false, false>(a, stream);
         case 33: return launch_encoded<true, false>(a, stream);
-        case 57: return launch_encoded<false, true, 1>(a, stream);  // debug shape: the walk alone
-        case 58: return launch_encoded<false, true, 2>(a, stream);  // debug shape: phase 2 loads only
+        case 57: return launch_encoded<false, true, 1>(a, stream);  // debug shape: the walk alone (WRONG coords)
+        case 58: return launch_encoded<false, true, 2>(a, stream);  // debug shape: phase 2 loads only (WRONG coords)
         case 47: return launch_encoded<false, true, 0, 64>(a, stream);
         case 48: return launch_encoded<false, true, 0, 16>(a, stream);
-        default: return launch_encoded<false, true, 0, 32>(a, stream);
+        default: break;
     }
+#endif
+    return launch_encoded<false, true, 0, 32>(a, stream);
 }
 
 }  // namespace hdx

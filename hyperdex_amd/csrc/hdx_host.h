@@ -9,12 +9,8 @@
 
 #include "hdx_internal.h"
 
-#define HDX_EXPORT extern "C" __attribute__((visibility("default")))
-
 namespace hdx {
 
-// Sets the calling thread's hdx_last_error() text and returns s.
-hdx_status fail(hdx_status s, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 hdx_status hip_fail(hipError_t e, const char* what);
 
 #define HIP_TRY(expr)                                     \
@@ -23,10 +19,17 @@ hdx_status hip_fail(hipError_t e, const char* what);
         if (e_ != hipSuccess) return hip_fail(e_, #expr); \
     } while (0)
 
-// hyperdatatype -> CODE_* (-1: the reference's lookup() returns NULL).
-int type_code(uint32_t t);
 // Validates a schema and fills codes_out[A] (may be NULL).
 hdx_status check_schema(const uint32_t* types, uint32_t A, uint8_t* codes_out);
+// Device scratch owned by the library (per-thread staging and streams),
+// registered so hdx_shutdown can free every thread's (track_scratch /
+// untrack_scratch; release() must leave the object reusable).
+struct Scratch {
+    virtual void release() = 0;
+    virtual ~Scratch() = default;
+};
+void track_scratch(Scratch* s);
+void untrack_scratch(Scratch* s);
 // Binds the calling thread to `want` (-1: its current device) after checking it is gfx950.
 hdx_status bind_device(int want);
 // The calling thread's library stream (created on first use).

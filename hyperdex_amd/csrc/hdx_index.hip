@@ -64,6 +64,10 @@ hipError_t launch_index_encode(const IndexArgs& a, hipStream_t stream) {
 __global__ void __launch_bounds__(256) search_regions_kernel(const SearchArgs a) {
     const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= a.R) return;
+    if (a.replicas && !a.replicas[r]) {  // configuration.cc:782-785, before any range test
+        a.include[r] = 0;
+        return;
+    }
     bool exclude = false, cleared = false;
     for (uint32_t k = 0; k < a.m && !exclude; ++k) {
         const uint32_t l = a.dim[k];

@@ -7,18 +7,9 @@
 #include <vector>
 
 #include "../../include/hdxhash.h"
+#include "hdx_host_common.h"
 
 namespace hdx {
-
-// Attribute classes the kernel dispatches on (host maps hyperdatatype -> code).
-enum : uint32_t {
-    CODE_ZERO = 0,     // not hashable: document/list/set/map/macaroon -> 0
-    CODE_STRING = 1,
-    CODE_INT64 = 2,
-    CODE_FLOAT = 3,
-    CODE_TS_SECOND = 4,  // .. CODE_TS_MONTH = 9, in hyperdatatype order
-    CODE_TS_MONTH = 9,
-};
 
 
 // Kernel arguments, passed by value (kernarg segment).  codes[] holds the
@@ -62,9 +53,10 @@ void finalize_args(BatchArgs& args);
 // Kernel variants (hdx_kernels.hip, variant_kernel_name): the automatic policy's
 // choices and the alternatives scripts/ab_variants.py times against them.
 hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, int variant);
-// The variant launch_hash_batch uses: HDX_KERNEL_VARIANT (tuning knob) or the default.
+// The variant launch_hash_batch uses: -1 (the automatic policy) in the product
+// library; libhdxhash_dbg.so (HDX_DEBUG_BUILD) adds a process-wide selection.
 int hash_variant();
-int set_hash_variant(int v);  // -2 if unknown, else the previous selection (-1 = auto)
+int set_hash_variant(int v);  // debug build only: -2 if unknown, else the previous selection
 // The variant launch_hash_batch would run for args, and its kernel's symbol.
 int chosen_variant(const BatchArgs& args);
 const char* variant_kernel_name(int v);
@@ -163,6 +155,7 @@ struct SearchArgs {
     const uint64_t* lower;   // [R*D]
     const uint64_t* upper;   // [R*D]
     const uint64_t* hashes;  // [2*m]: hash of start, hash of end
+    const uint8_t* replicas; // [R] 0 = region without replicas (skipped), or NULL = all have
     uint8_t* include;        // [R]
     uint32_t* cleared;       // set when the reference would clear the server list
     uint32_t R, D, m;
@@ -189,8 +182,5 @@ hipError_t launch_synth_fill(const SynthArgs& a, const uint64_t* obj_base, const
 hipError_t launch_synth_encode(const uint8_t* blob, const uint64_t* obj_base, const uint32_t* attr_len,
                                uint32_t A, uint64_t n, uint64_t first_version, const uint64_t* val_off,
                                uint8_t* vals, hipStream_t s);
-
-// hyperdatatype -> dispatch code; -1 for an id datatype_info::lookup rejects.
-int type_code(uint32_t type);
 
 }  // namespace hdx

@@ -26,6 +26,10 @@
 #include "hdx_loads.h"
 #include "hdx_region_lookup.h"
 
+#ifndef HDX_DEBUG_BUILD
+#define HDX_DEBUG_BUILD 0
+#endif
+
 namespace hdx {
 
 // ===========================================================================
@@ -402,12 +406,17 @@ static hipError_t launch_chunk(const BatchArgs& args, hipStream_t stream) {
 
 hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, int variant) {
     switch (variant) {
+        // the automatic policy's kernels (auto_variant)
         case 12: return launch_chunk<true>(args, stream);
-        case 18: return launch_regroup<4, true>(args, stream);
-        case 19: return launch_regroup<8, true>(args, stream);
         case 20: return launch_regroup<8, true, false>(args, stream);
         case 21: return launch_regroup<4, true, false>(args, stream);
         case 25: return launch_regroup<16, true, false, false>(args, stream);
+        case 44: return launch_regroup<2, true, true, true, true, false, true, 1>(args, stream);
+        case 46: return launch_regroup<8, true, true, true, false, false, true, 1>(args, stream);
+#if HDX_DEBUG_BUILD
+        // alternatives for interleaved A/B (scripts/ab_variants.py), bit-exact
+        case 18: return launch_regroup<4, true>(args, stream);
+        case 19: return launch_regroup<8, true>(args, stream);
         case 26: return launch_regroup<2, true>(args, stream);
         case 30: return launch_chunk<true, true>(args, stream);
         case 31: return launch_chunk<true, false, 0, true>(args, stream);
@@ -415,11 +424,11 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 37: return launch_regroup<2, true, true, true, true, true>(args, stream);
         case 38: return launch_regroup<2, true, true, true, true, false, true>(args, stream);
         case 39: return launch_regroup<8, true, true, true, false, false, true>(args, stream);
-        case 44: return launch_regroup<2, true, true, true, true, false, true, 1>(args, stream);
         case 45: return launch_regroup<2, true, true, true, true, false, true, 2>(args, stream);
-        case 46: return launch_regroup<8, true, true, true, false, false, true, 1>(args, stream);
-        case 40: return launch_chunk<true, false, 1>(args, stream);  // debug shape: loads only
-        case 41: return launch_chunk<true, false, 2>(args, stream);  // debug shape: arithmetic only
+        // debug shapes: WRONG coordinates, debug library only
+        case 40: return launch_chunk<true, false, 1>(args, stream);  // loads only
+        case 41: return launch_chunk<true, false, 2>(args, stream);  // arithmetic only
+#endif
         default: return hipErrorInvalidValue;
     }
 }
@@ -471,9 +480,11 @@ hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream) 
     }
 }
 
-static constexpr int kDefaultVariant = -1;  // automatic
-// 33 / 43 select the stored-object sweep's line-touch and byte-addressed forms,
-// 57 / 58 its walk-only and loads-only shapes (hdx_encoded.hip).
+#if HDX_DEBUG_BUILD
+// Debug library only (libhdxhash_dbg.so): a process-wide kernel selection for
+// interleaved A/B runs, from hdxdbg_set_kernel_variant or HDX_KERNEL_VARIANT.
+// 33 / 43 / 47 / 48 select the stored-object sweep's alternative forms, 57 / 58
+// its walk-only and loads-only debug shapes (hdx_encoded.hip).
 static bool known_variant(int v) {
     switch (v) {
         case -1: case 12: case 18: case 19: case 20: case 21: case 25: case 26: case 30: case 31: case 35: case 37:
@@ -488,8 +499,9 @@ static bool known_variant(int v) {
 
 static int g_variant = [] {
     const char* e = getenv("HDX_KERNEL_VARIANT");
-    return e && *e ? atoi(e) : kDefaultVariant;
+    return e && *e && known_variant(atoi(e)) ? atoi(e) : -1;
 }();
+#endif
 
 // Automatic choice (interleaved A/B on one MI355X, profiles/r1/ab_variants_*.jsonl
 // and profiles/r1/ab_a4_*.jsonl):
@@ -527,12 +539,17 @@ static int auto_variant(const BatchArgs& args) {
     return 44;
 }
 
+#if HDX_DEBUG_BUILD
 int hash_variant() { return __atomic_load_n(&g_variant, __ATOMIC_RELAXED); }
 
 int set_hash_variant(int v) {
     if (!known_variant(v)) return -2;
     return __atomic_exchange_n(&g_variant, v, __ATOMIC_RELAXED);
 }
+#else
+// The product library has no kernel selection: the automatic policy only.
+int hash_variant() { return -1; }
+#endif
 
 void finalize_args(BatchArgs& args) {
     args.inv_A = 1.0 / (double)args.A;

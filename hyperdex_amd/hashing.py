@@ -79,13 +79,11 @@ def hash_batch(types, blob, obj_base, attr_len, coords=None, status=None, stream
     t = _u32_array(types)
     A = len(t)
     n = obj_base.numel()
-    assert attr_len.numel() == n * A, "attr_len must hold n*A lengths"
-    assert blob.element_size() == 1 and obj_base.element_size() == 8 and attr_len.element_size() == 4
-    for x in (blob, obj_base, attr_len):
-        assert x.is_cuda and x.is_contiguous()
+    _check_packed(blob, obj_base, attr_len, A)
     if coords is None:
         coords = torch.empty((n, A), dtype=torch.int64, device=obj_base.device)
-    assert coords.is_cuda and coords.is_contiguous() and coords.element_size() == 8
+    _check_out(coords, n * A, obj_base.device, "coords")
+    _check_status(status, obj_base.device)
     if stream is None:
         stream = torch.cuda.current_stream(obj_base.device)
     handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
@@ -93,6 +91,39 @@ def hash_batch(types, blob, obj_base, attr_len, coords=None, status=None, stream
         t.ctypes.data, A, blob.data_ptr(), obj_base.data_ptr(), attr_len.data_ptr(), n,
         coords.data_ptr(), status.data_ptr() if status is not None else None, handle))
     return coords
+
+
+def _check_packed(blob, obj_base, attr_len, A):
+    """The packed layout's device tensors: u8 blob, u64 bases, u32 lengths (n*A)."""
+    n = obj_base.numel()
+    assert attr_len.numel() == n * A, "attr_len must hold n*A lengths"
+    assert blob.element_size() == 1 and obj_base.element_size() == 8 and attr_len.element_size() == 4, \
+        "blob / obj_base / attr_len must have 1 / 8 / 4-byte elements"
+    for x in (blob, obj_base, attr_len):
+        assert x.is_cuda and x.is_contiguous() and x.device == obj_base.device, "contiguous tensors on one device"
+
+
+def _check_stored(keys, key_off, key_len, vals, val_off, val_len):
+    """Stored objects: u8 keys / values, u64 offsets, u32 lengths, n of each."""
+    n = val_off.numel()
+    assert key_off.numel() == n and key_len.numel() == n and val_len.numel() == n
+    assert keys.element_size() == 1 and vals.element_size() == 1
+    assert key_off.element_size() == 8 and val_off.element_size() == 8
+    assert key_len.element_size() == 4 and val_len.element_size() == 4
+    for x in (keys, key_off, key_len, vals, val_off, val_len):
+        assert x.is_cuda and x.is_contiguous() and x.device == val_off.device
+
+
+def _check_out(x, numel, device, what):
+    assert x.is_cuda and x.is_contiguous() and x.element_size() == 8 and x.device == device, \
+        "%s must be a contiguous 8-byte tensor on %s" % (what, device)
+    assert x.numel() == numel, "%s must hold %d elements, has %d" % (what, numel, x.numel())
+
+
+def _check_status(status, device):
+    if status is not None:
+        assert status.is_cuda and status.device == device and status.numel() * status.element_size() >= 4, \
+            "status must be a device tensor of at least 4 bytes"
 
 
 def hash_batch_host(types, blob, obj_base, attr_len, out: Optional[np.ndarray] = None):
@@ -122,11 +153,13 @@ def hash_encoded(types, keys, key_off, key_len, vals, val_off, val_len, coords=N
     t = _u32_array(types)
     A = len(t)
     n = val_off.numel()
-    assert key_off.numel() == n and key_len.numel() == n and val_len.numel() == n
-    for x in (keys, key_off, key_len, vals, val_off, val_len):
-        assert x.is_cuda and x.is_contiguous()
+    _check_stored(keys, key_off, key_len, vals, val_off, val_len)
     if coords is None:
         coords = torch.empty((n, A), dtype=torch.int64, device=val_off.device)
+    _check_out(coords, n * A, val_off.device, "coords")
+    if versions is not None:
+        _check_out(versions, n, val_off.device, "versions")
+    _check_status(status, val_off.device)
     if stream is None:
         stream = torch.cuda.current_stream(val_off.device)
     handle = stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
@@ -149,12 +182,16 @@ def hash_encoded_regions(types, keys, key_off, key_len, vals, val_off, val_len, 
     t = _u32_array(types)
     A = len(t)
     n = val_off.numel()
-    for x in (keys, key_off, key_len, vals, val_off, val_len):
-        assert x.is_cuda and x.is_contiguous()
+    _check_stored(keys, key_off, key_len, vals, val_off, val_len)
     dev = val_off.device
     ids = torch.empty((len(tables), n), dtype=torch.int64, device=dev)
     if coords is True:
         coords = torch.empty((n, A), dtype=torch.int64, device=dev)
+    if coords is not None and coords is not False:
+        _check_out(coords, n * A, dev, "coords")
+    if versions is not None:
+        _check_out(versions, n, dev, "versions")
+    _check_status(status, dev)
     handles = (ctypes.c_void_p * max(len(tables), 1))(*[tb.handle.value for tb in tables])
     if stream is None:
         stream = torch.cuda.current_stream(dev)
@@ -178,13 +215,14 @@ def hash_batch_regions(types, blob, obj_base, attr_len, tables, coords=False, st
     t = _u32_array(types)
     A = len(t)
     n = obj_base.numel()
-    for x in (blob, obj_base, attr_len):
-        assert x.is_cuda and x.is_contiguous()
-    assert attr_len.numel() == n * A
+    _check_packed(blob, obj_base, attr_len, A)
     dev = obj_base.device
     ids = torch.empty((len(tables), n), dtype=torch.int64, device=dev)
     if coords is True:
         coords = torch.empty((n, A), dtype=torch.int64, device=dev)
+    if coords is not None and coords is not False:
+        _check_out(coords, n * A, dev, "coords")
+    _check_status(status, dev)
     handles = (ctypes.c_void_p * max(len(tables), 1))(*[tb.handle.value for tb in tables])
     if stream is None:
         stream = torch.cuda.current_stream(dev)

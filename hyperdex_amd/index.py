@@ -63,14 +63,21 @@ def _ranges(ranges: Sequence[tuple]):
     return arr
 
 
-def search_regions(table: RegionTable, ranges: Sequence[tuple]) -> Tuple[np.ndarray, bool]:
+def search_regions(table: RegionTable, ranges: Sequence[tuple],
+                   has_replicas=None) -> Tuple[np.ndarray, bool]:
     """ranges: [(attr, hyperdatatype, start bytes | None, end bytes | None[, invalid])].
-    Returns (include u8[R], cleared): include[r] = 0 when a range rules region
-    r out; cleared when the reference returns an empty server list."""
+    has_replicas: u8[R] (0 = the region has no replicas and is skipped, as
+    configuration.cc:782-785 does) or None (all have).  Returns (include u8[R],
+    cleared): include[r] = 0 when region r is skipped or a range rules it out;
+    cleared when the reference returns an empty server list."""
     R = len(table.ids)
     include = np.zeros(max(R, 1), np.uint8)
     cleared = ctypes.c_int(0)
     arr = _ranges(ranges)
-    check(lib().hdx_search_regions(table.handle, arr, len(ranges), include.ctypes.data,
-                                   ctypes.byref(cleared)))
+    rep = None
+    if has_replicas is not None:
+        rep = np.ascontiguousarray(has_replicas, np.uint8)
+        assert rep.size == R, "has_replicas must hold one flag per region"
+    check(lib().hdx_search_regions(table.handle, arr, len(ranges), None if rep is None else rep.ctypes.data,
+                                   include.ctypes.data, ctypes.byref(cleared)))
     return include[:R], bool(cleared.value)

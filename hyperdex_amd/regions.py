@@ -27,7 +27,8 @@ class RegionTable:
         R = len(self.ids)
         assert self.lower.shape == (R, D) and self.upper.shape == (R, D)
         h = ctypes.c_void_p()
-        check(lib().hdx_region_table_create(D, R, self.attrs.ctypes.data, self.lower.ctypes.data,
+        self._lib = lib()  # destroyed by the library that created it
+        check(self._lib.hdx_region_table_create(D, R, self.attrs.ctypes.data, self.lower.ctypes.data,
                                             self.upper.ctypes.data, self.ids.ctypes.data,
                                             ctypes.byref(h)))
         self._h = h
@@ -38,7 +39,7 @@ class RegionTable:
 
     def close(self):
         if getattr(self, "_h", None):
-            lib().hdx_region_table_destroy(self._h)
+            self._lib.hdx_region_table_destroy(self._h)
             self._h = None
 
     def __del__(self):

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define HDX_ABI_VERSION 1
+#define HDX_ABI_VERSION 2
 #define HDX_MAX_ATTRS 256
 
 typedef enum hdx_status {
@@ -76,6 +76,15 @@ const char* hdx_version(void);
  * gfx950 part.  Optional: every entry point initialises lazily on device 0
  * or on the thread's current HIP device. */
 hdx_status hdx_init(int device);
+/* Checks that every device in device_mask (bit d = HIP ordinal d) is a
+ * visible gfx950 part, binds the calling thread to the lowest one and creates
+ * its stream (hdx_init(device_mask)). */
+hdx_status hdx_init_mask(uint64_t device_mask);
+/* Frees every thread's library scratch (streams, pinned and device staging)
+ * after waiting for the work queued on it.  No call may be in progress;
+ * region tables and batchers are the caller's to destroy.  Threads rebind
+ * lazily on their next call. */
+hdx_status hdx_shutdown(void);
 /* Number of HIP devices visible (0 without a GPU; never initialises one). */
 int hdx_device_count(void);
 /* Message for the last non-OK status returned on this thread. */
@@ -240,16 +249,18 @@ typedef struct hdx_range {
     uint32_t reserved;
 } hdx_range;
 /* The region test of configuration::lookup_search (common/configuration.cc:
- * 736-858) for one subspace: include[r] = 0 when a range excludes region r
- * of `table` (a STRING range with start == end whose hash lies outside the
- * region's box on that dimension; an INT64/FLOAT range whose hashed start is
- * above the box or hashed end below it), else 1.  *cleared = 1 when the
+ * 736-858) for one subspace: include[r] = 0 when region r of `table` has no
+ * replicas (has_replicas[r] == 0; skipped before any test, :782-785) or a
+ * range excludes it (a STRING range with start == end whose hash lies outside
+ * the region's box on that dimension; an INT64/FLOAT range whose hashed start
+ * is above the box or hashed end below it), else 1.  *cleared = 1 when the
  * reference would return an empty server list (an invalid range, or a region
- * box with lower > upper on a ranged dimension); include[] is then all 0.
- * Regions without replicas are the caller's to skip, as the reference does.
- * Endpoint hashes are computed on the device.  Host pointers; synchronous. */
+ * with replicas whose box has lower > upper on a ranged dimension reached
+ * before the region is excluded, :808-813); include[] is then all 0.
+ * has_replicas may be NULL (every region has replicas).  Endpoint hashes are
+ * computed on the device.  Host pointers; synchronous. */
 hdx_status hdx_search_regions(hdx_region_table table, const hdx_range* ranges, uint32_t nranges,
-                              uint8_t* include, int* cleared);
+                              const uint8_t* has_replicas, uint8_t* include, int* cleared);
 
 /* ---- daemon batching shim --------------------------------- */
 

@@ -1,6 +1,13 @@
 /*
- * hdxhash_debug.h — tuning hooks of libhdxhash.so (not part of the drop-in
- * boundary; used by scripts/ab_variants.py for interleaved A/B timing).
+ * hdxhash_debug.h — measurement and tuning hooks (not part of the drop-in
+ * boundary).
+ *
+ * Both libraries: hdxdbg_kernel_for (which kernel the automatic policy runs)
+ * and hdxdbg_stream_probe (bench.py's practical HBM ceiling).
+ * libhdxhash_dbg.so only (HDX_DEBUG_BUILD, hyperdex_amd/csrc/Makefile):
+ * hdxdbg_set_kernel_variant / hdxdbg_kernel_variant, used by
+ * scripts/ab_variants.py and the variant parity tests.  The product library
+ * has no kernel selection and no environment switches.
  */
 #ifndef HDXHASH_DEBUG_H
 #define HDXHASH_DEBUG_H
@@ -11,7 +18,7 @@
 extern "C" {
 #endif
 
-/* Select the hash kernel variant for subsequent launches in this process
+/* [debug library only] Select the hash kernel variant for subsequent launches in this process
  * (see hyperdex_amd/csrc/hdx_kernels.hip; -1 = automatic per schema);
  * returns the previous selection, or -2 for an unknown variant (nothing
  * changed). */

@@ -9,11 +9,19 @@
 // e::slice (libe), hyperdex::schema / attribute (common/schema.h,
 // common/attribute.h) and enum hyperdatatype (include/hyperdex.h).
 //
+// These are the per-object calls of the client (point_leader), the search
+// planner (lookup_search) and the daemon's write path: they run on the host
+// CPU inside libhdxhash.so (hyperdex_amd/csrc/hdx_cpu.cpp), pure, reentrant,
+// with no allocation and no GPU needed — a client host without an MI355X
+// links this header unchanged.  Bulk work goes to the batched C-ABI
+// (hdx_hash_batch_device / _host, hdx_batcher_*), which runs the gfx950
+// kernels.
+//
 // Semantics are the reference's bit for bit.  Where the reference asserts —
 // unknown type (hash.cc:38), int64/float/timestamp value not 0 or 8 bytes
-// (datatype_int64.cc:233, datatype_float.cc:204) — and wherever the GPU path
-// fails (no device, HIP error), these functions print the library's message
-// and abort(): there is no silent fallback.
+// (datatype_int64.cc:233, datatype_float.cc:204) — these functions print the
+// library's message and abort(), in every build (the reference's asserts
+// compile out under NDEBUG; then it reads the wrong-sized value anyway).
 #ifndef hyperdex_common_hash_h_
 #define hyperdex_common_hash_h_
 
@@ -62,8 +70,7 @@ hash(const schema& sc,
      const e::slice& key,
      uint64_t* h)
 {
-    const uint32_t t = static_cast<uint32_t>(sc.attrs[0].type);
-    hdx_dropin::check(hdx_hash_key(&t, 1, key.data(), key.size(), h), "hash(schema, key)");
+    *h = hash(sc.attrs[0].type, key);
 }
 
 inline void
@@ -72,32 +79,13 @@ hash(const schema& sc,
      const std::vector<e::slice>& value,
      uint64_t* hs)
 {
-    uint32_t types[HDX_MAX_ATTRS];
-    const uint8_t* ptrs[HDX_MAX_ATTRS];
-    size_t lens[HDX_MAX_ATTRS];
-    const size_t A = sc.attrs_sz;
+    // common/hash.cc:63-67: hs[0] from the key, hs[i] from value[i - 1]
+    hs[0] = hash(sc.attrs[0].type, key);
 
-    if (A == 0 || A > HDX_MAX_ATTRS)
+    for (size_t i = 1; i < sc.attrs_sz; ++i)
     {
-        fprintf(stderr, "hyperdex::hash(schema, key, value): %zu attributes\n", A);
-        abort();
+        hs[i] = hash(sc.attrs[i].type, value[i - 1]);
     }
-
-    for (size_t i = 0; i < A; ++i)
-    {
-        types[i] = static_cast<uint32_t>(sc.attrs[i].type);
-    }
-
-    // value[i - 1] is attribute i, as in common/hash.cc:63-67
-    for (size_t i = 1; i < A; ++i)
-    {
-        ptrs[i - 1] = value[i - 1].data();
-        lens[i - 1] = value[i - 1].size();
-    }
-
-    hdx_dropin::check(hdx_hash_object(types, static_cast<uint32_t>(A), key.data(), key.size(),
-                                      ptrs, lens, hs),
-                      "hash(schema, key, value)");
 }
 
 END_HYPERDEX_NAMESPACE

@@ -480,8 +480,8 @@ static int slice_eq(const uint8_t* a, uint64_t al, const uint8_t* b, uint64_t bl
 }
 
 int hdxo_search_regions(uint32_t D, uint32_t R, const uint16_t* attrs, const uint64_t* lower,
-                        const uint64_t* upper, const hdxo_range* ranges, uint32_t nranges,
-                        uint8_t* include) {
+                        const uint64_t* upper, const uint8_t* has_replicas, const hdxo_range* ranges,
+                        uint32_t nranges, uint8_t* include) {
     for (uint32_t i = 0; i < nranges; ++i) /* :761-768 */
         if (ranges[i].invalid) {
             memset(include, 0, R);
@@ -489,6 +489,10 @@ int hdxo_search_regions(uint32_t D, uint32_t R, const uint16_t* attrs, const uin
         }
     for (uint32_t j = 0; j < R; ++j) { /* :777 */
         int exclude = 0;
+        if (has_replicas && !has_replicas[j]) { /* :782-785: skipped before any test */
+            include[j] = 0;
+            continue;
+        }
         for (uint32_t k = 0; !exclude && k < nranges; ++k) { /* :789 */
             const hdxo_range* rg = &ranges[k];
             uint32_t attr = UINT16_MAX;

@@ -98,8 +98,8 @@ typedef struct hdxo_range {
  * include) when the reference clears the server list, else 0; -1 when a
  * numeric endpoint's size is not 0 or 8. */
 int hdxo_search_regions(uint32_t D, uint32_t R, const uint16_t* attrs, const uint64_t* lower,
-                        const uint64_t* upper, const hdxo_range* ranges, uint32_t nranges,
-                        uint8_t* include);
+                        const uint64_t* upper, const uint8_t* has_replicas, const hdxo_range* ranges,
+                        uint32_t nranges, uint8_t* include);
 
 #ifdef __cplusplus
 }

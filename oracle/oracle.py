@@ -47,7 +47,7 @@ def lib():
         L.hdxo_index_encode.restype = sz
         L.hdxo_index_encode.argtypes = [u32, vp, sz, vp, ctypes.POINTER(ctypes.c_int)]
         L.hdxo_search_regions.restype = ctypes.c_int
-        L.hdxo_search_regions.argtypes = [u32, u32, vp, vp, vp, vp, u32, vp]
+        L.hdxo_search_regions.argtypes = [u32, u32, vp, vp, vp, vp, vp, u32, vp]
         L.hdxo_hash_encoded.restype = ctypes.c_int64
         _LIB = L
     return _LIB
@@ -176,16 +176,20 @@ def make_ranges(ranges):
     return arr
 
 
-def search_regions(attrs, lower, upper, ranges):
-    """lookup_search's region loop for one subspace -> (include u8[R], cleared)."""
+def search_regions(attrs, lower, upper, ranges, has_replicas=None):
+    """lookup_search's region loop for one subspace -> (include u8[R], cleared).
+    has_replicas (u8[R] or None = every region has replicas): regions without
+    replicas are skipped first (configuration.cc:782-785)."""
     attrs = np.ascontiguousarray(attrs, np.uint16)
     lower = np.ascontiguousarray(lower, np.uint64)
     upper = np.ascontiguousarray(upper, np.uint64)
     R = lower.shape[0] if lower.ndim == 2 else lower.size // max(len(attrs), 1)
     include = np.zeros(max(R, 1), np.uint8)
     arr = make_ranges(ranges)
+    rep = None if has_replicas is None else np.ascontiguousarray(has_replicas, np.uint8)
     rc = lib().hdxo_search_regions(len(attrs), R, attrs.ctypes.data, lower.ctypes.data,
-                                   upper.ctypes.data, arr, len(ranges), include.ctypes.data)
+                                   upper.ctypes.data, None if rep is None else rep.ctypes.data, arr,
+                                   len(ranges), include.ctypes.data)
     if rc < 0:
         raise ValueError("numeric endpoint not 0 or 8 bytes")
     return include[:R], bool(rc)

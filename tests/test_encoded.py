@@ -3,7 +3,7 @@
 import numpy as np
 import pytest
 
-from hyperdex_amd import synth
+from hyperdex_amd import _lib, synth
 
 
 def test_oracle_decodes_what_encode_wrote(oracle):
@@ -175,10 +175,7 @@ def test_gpu_encoded_scattered_layout(oracle, variant):
 
     import hyperdex_amd as hdx
     dev = torch.device("cuda", 0)
-    lib = hdx.lib()
-    prev = lib.hdxdbg_set_kernel_variant(variant)
-    assert prev != -2
-    try:
+    with _lib.debug_library(variant):
         for cfg, n in (("cfg3b", 700), ("mixed", 300), ("cfg2", 129)):
             types, blob, base, lens = synth.make_batch_host(cfg, n, seed=n + 11)
             enc = synth.encode_values_host(types, blob, base, lens, first_version=9)
@@ -189,8 +186,6 @@ def test_gpu_encoded_scattered_layout(oracle, variant):
             torch.cuda.synchronize()
             assert np.array_equal(got.cpu().numpy().view(np.uint64), want), (cfg, n)
             assert np.array_equal(versions.cpu().numpy().view(np.uint64), wver), (cfg, n)
-    finally:
-        lib.hdxdbg_set_kernel_variant(prev)
 
 
 @pytest.mark.gpu
@@ -203,10 +198,7 @@ def test_gpu_encoded_every_variant(oracle, variant):
 
     import hyperdex_amd as hdx
     dev = torch.device("cuda", 0)
-    lib = hdx.lib()
-    prev = lib.hdxdbg_set_kernel_variant(variant)
-    assert prev != -2
-    try:
+    with _lib.debug_library(variant):
         cases = [("cfg3b", 1001), ("cfg2", 997), ("mixed", 500), ("cfg1", 33), ("wide", 61),
                  ("keyonly_long", 40), ("cfg3b", 1), ("cfg3b", 15), ("cfg3b", 16)]
         for cfg, n in cases:
@@ -220,8 +212,6 @@ def test_gpu_encoded_every_variant(oracle, variant):
             torch.cuda.synchronize()
             assert np.array_equal(got.cpu().numpy().view(np.uint64), want), (cfg, n)
             assert np.array_equal(versions.cpu().numpy().view(np.uint64), wver), (cfg, n)
-    finally:
-        lib.hdxdbg_set_kernel_variant(prev)
 
 
 @pytest.mark.gpu

@@ -298,10 +298,7 @@ def test_every_kernel_variant_matches_oracle(oracle, torch_dev, variant):
     §4.3), and scripts/ab_variants.py times them: each must be bit-exact on
     every config, on ragged object counts and on shuffled objects."""
     torch, dev = torch_dev
-    lib = _lib.lib()
-    prev = lib.hdxdbg_set_kernel_variant(variant)
-    assert prev != -2
-    try:
+    with _lib.debug_library(variant):
         for cfg, n in [("cfg1", 777), ("cfg2", 1001), ("cfg3a", 257), ("cfg3b", 1500),
                        ("mixed", 900), ("wide", 131), ("keyonly_long", 70)]:
             types, blob, base, lens = synth.make_batch_host(cfg, n, seed=variant * 100 + n)
@@ -318,5 +315,3 @@ def test_every_kernel_variant_matches_oracle(oracle, torch_dev, variant):
         A = len(types)
         check_batch(oracle, torch, dev, types, blob, base[perm],
                     lens.reshape(999, A)[perm].reshape(-1))
-    finally:
-        lib.hdxdbg_set_kernel_variant(prev)

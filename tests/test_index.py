@@ -134,6 +134,29 @@ def test_oracle_search_semantics(oracle):
     assert cl
 
 
+def test_oracle_search_skips_replicaless_regions_first(oracle):
+    """configuration.cc:782-785 skips a region without replicas before the
+    lower > upper clear of :808-813: an empty box on a replica-less region
+    does not clear the search, and the region is never included."""
+    q = 2**62
+    attrs = [3]
+    lower = np.array([[0], [q], [2 * q], [3 * q]], np.uint64)
+    upper = np.array([[q - 1], [2 * q - 1], [3 * q - 1], [2**64 - 1]], np.uint64)
+    i64 = lambda x: struct.pack("<q", x)  # noqa: E731
+    bad_lo = lower.copy()
+    bad_lo[1, 0] = upper[1, 0] + np.uint64(1)  # region 1: lower > upper
+    rg = [(3, INT64, i64(-2**62), None)]
+    inc, cl = oracle.search_regions(attrs, bad_lo, upper, rg)
+    assert cl and not inc.any()  # with replicas everywhere the list is cleared
+    inc, cl = oracle.search_regions(attrs, bad_lo, upper, rg, has_replicas=[1, 0, 1, 1])
+    assert not cl and list(inc) == [0, 0, 1, 1]
+    inc, cl = oracle.search_regions(attrs, lower, upper, [], has_replicas=[1, 0, 0, 1])
+    assert not cl and list(inc) == [1, 0, 0, 1]
+    # an invalid range clears before any region is visited (:762-769)
+    inc, cl = oracle.search_regions(attrs, lower, upper, [(3, INT64, i64(0), None, True)], has_replicas=[0] * 4)
+    assert cl
+
+
 def _random_search_case(rng, oracle):
     D = int(rng.integers(1, 5))
     A = 8
@@ -265,12 +288,35 @@ def test_gpu_search_regions_matches_oracle(oracle):
     rng = np.random.default_rng(11)
     for case in range(300):
         attrs, lo, up, ranges = _random_search_case(rng, oracle)
-        want, wcl = oracle.search_regions(attrs, lo, up, ranges)
+        rep = None
+        if case % 3 == 1:  # some regions without replicas (incl. empty boxes)
+            rep = (rng.random(len(lo)) < 0.7).astype(np.uint8)
+        want, wcl = oracle.search_regions(attrs, lo, up, ranges, has_replicas=rep)
         table = hdx.RegionTable(attrs, lo, up, np.arange(1, len(lo) + 1, dtype=np.uint64))
-        got, cl = hdx.search_regions(table, ranges)
+        got, cl = hdx.search_regions(table, ranges, has_replicas=rep)
         table.close()
         assert cl == wcl, case
         assert np.array_equal(got, want), case
+
+
+@pytest.mark.gpu
+def test_gpu_search_replicaless_empty_box(oracle):
+    """A replica-less region with an empty box (lower > upper) on a ranged
+    dimension neither clears the search nor appears in it."""
+    import hyperdex_amd as hdx
+    lo, up = oracle.partition(2, 16)
+    lo, up = lo.copy(), up.copy()
+    lo[5, 1], up[5, 1] = up[5, 1], lo[5, 1]
+    rep = np.ones(len(lo), np.uint8)
+    rg = [(4, INT64, struct.pack("<q", -5), struct.pack("<q", 2**50))]
+    table = hdx.RegionTable([2, 4], lo, up, np.arange(1, len(lo) + 1, dtype=np.uint64))
+    inc, cl = hdx.search_regions(table, rg, has_replicas=rep)
+    assert cl and not inc.any()
+    rep[5] = 0
+    inc, cl = hdx.search_regions(table, rg, has_replicas=rep)
+    want, wcl = oracle.search_regions([2, 4], lo, up, rg, has_replicas=rep)
+    assert not cl and not wcl and inc[5] == 0 and np.array_equal(inc, want) and inc.any()
+    table.close()
 
 
 @pytest.mark.gpu

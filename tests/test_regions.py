@@ -98,8 +98,10 @@ def test_gpu_lookup_index_vs_scan(oracle, R, scan, monkeypatch):
     2^64-1, and duplicated boxes (first one wins)."""
     import torch
 
-    from hyperdex_amd import regions
-    if scan:
+    import contextlib
+
+    from hyperdex_amd import _lib, regions
+    if scan:  # an A/B switch of the debug library only
         monkeypatch.setenv("HDX_REGION_SCAN", "1")
     rng = np.random.default_rng(R + 7)
     A, attrs = 9, [8, 2]
@@ -114,9 +116,11 @@ def test_gpu_lookup_index_vs_scan(oracle, R, scan, monkeypatch):
     ids = rng.integers(1, 2**63, R, dtype=np.uint64)
     coords = _coords(rng, 20000, A, lo, up, attrs)
     want = oracle.lookup_region(attrs, lo, up, ids, coords)
-    t = regions.RegionTable(attrs, lo, up, ids)
-    got = regions.lookup_region(t, torch.from_numpy(coords.view(np.int64)).to(torch.device("cuda", 0)))
-    torch.cuda.synchronize()
+    with _lib.debug_library() if scan else contextlib.nullcontext():
+        t = regions.RegionTable(attrs, lo, up, ids)
+        got = regions.lookup_region(t, torch.from_numpy(coords.view(np.int64)).to(torch.device("cuda", 0)))
+        torch.cuda.synchronize()
+        t.close()
     assert np.array_equal(got.cpu().numpy().view(np.uint64), want)
 
 
@@ -178,3 +182,37 @@ def test_gpu_batch_regions_fused(oracle, cfg, n, with_coords):
         assert np.array_equal(coords.cpu().numpy().view(np.uint64), want_coords)
     for t in tables:
         t.close()
+
+
+@pytest.mark.gpu
+def test_gpu_tables_from_another_device_are_rejected(oracle):
+    """A region table records the device it was created on; the fused and
+    plain lookups refuse a table of another device (HDX_E_INVALID) instead of
+    reading that device's memory.  One GPU here, so the table's
+    device field (the first int of hdx_region_table_s, hdx_host.h) is
+    rewritten for the check and restored."""
+    import ctypes
+
+    import torch
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import _lib, regions, synth
+    dev = torch.device("cuda", 0)
+    types, blob, base, lens = synth.make_batch_device("cfg2", 1000, device=dev)
+    lo, up = oracle.partition(1, 64)
+    t = regions.RegionTable([0], lo, up, np.arange(1, 65, dtype=np.uint64))
+    field = ctypes.c_int.from_address(t.handle.value)
+    assert field.value == 0
+    coords = hdx.hash_batch(types, blob, base, lens)
+    try:
+        field.value = 5
+        for call in (lambda: hdx.hash_batch_regions(types, blob, base, lens, [t]),
+                     lambda: regions.lookup_region(t, coords)):
+            with pytest.raises(hdx.HdxError) as e:
+                call()
+            assert e.value.status == _lib.HDX_E_INVALID
+    finally:
+        field.value = 0
+    hdx.hash_batch_regions(types, blob, base, lens, [t])
+    torch.cuda.synchronize()
+    t.close()
