@@ -10,6 +10,13 @@ Multi-GPU (torchrun, one rank per GPU): each rank owns its own 10M-object
 shard (weak scaling, no collective in the timed region); the RCCL all-gather
 of the coordinates is timed separately and reported as `allgather`.
 
+Config 4 rides along in every line as `config4`: one batch
+of 100M config-3b objects split over the N ranks by payload bytes
+(hyperdex_amd.dist.shard_ranges), each rank hashing its shard straight into
+its rows of the full coordinate matrix (hash phase, max over ranks), then the
+in-place RCCL all-gather of those rows over xGMI (reported apart), so the
+1/2/4/8-GPU runs give config 4's strong-scaling curve.
+
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -36,7 +43,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="cfg3a")
-    ap.add_argument("--objects", type=int, default=10_000_000, help="objects per GPU")
+    ap.add_argument("--objects", type=int, default=0,
+                    help="objects per GPU (default 10M; 50M for cfg5, BASELINE config 5)")
+    ap.add_argument("--config4-objects", type=int, default=100_000_000,
+                    help="config 4: objects of the whole sharded batch (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-allgather", action="store_true")
@@ -82,7 +92,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return tuple(float(v) for v in t.tolist())
 
-    cfg, n = args.config, args.objects
+    cfg, n = args.config, args.objects or (50_000_000 if args.config == "cfg5" else 10_000_000)
     stream = torch.cuda.current_stream(dev)
     if cfg == "cfg5":
         # config 5: reindex sweep over stored objects (values in the daemon's
@@ -143,6 +153,7 @@ def main():
     else:  # payload + 4 B length + 8 B coordinate per attribute
         algo_bytes = payload + n * A * ALGO_EXTRA_PER_ATTR
     achieved = algo_bytes / (kernel_ms / 1e3) / 1e9
+    traffic, traffic_src = measured_traffic(args.traffic, cfg, n)
 
     result = {
         "metric": "hashed GiB/s (device-resident) + Mobjects/s, 16-attr×64B batches",
@@ -166,7 +177,8 @@ def main():
                    "parallelism": "shard%d" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                     "traffic": measured_traffic(args.traffic, cfg, n),
+                     "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel_ms": round(kernel_ms, 4),
                      "algorithmic_bytes_per_launch": algo_bytes,
                      "kernel": hdx.hashing.kernel_for(types, n)[1]},
@@ -203,6 +215,10 @@ def main():
         # BASELINE's third config with its mixed attribute types, measured the
         # same way in the same run (the headline line stays config 3a's)
         result["secondary"] = {"cfg3b": time_config("cfg3b", n, dev, stream)}
+
+    if args.config4_objects and cfg != "cfg5":
+        result["config4"] = time_config4(args.config4_objects, world, rank, dev, stream, max_over_ranks,
+                                         backend, gather=not args.no_allgather)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if cfg == "cfg5":
@@ -252,6 +268,104 @@ def time_allgather(coords, world, dev, backend, max_over_ranks, reps=3):
     res["d2h_local_shard_ms"] = round(d2h * 1e3, 3)
     res["d2h_GBps_per_gpu"] = round(coords.numel() * 8 / d2h / 1e9, 2)
     del host
+    return res
+
+
+def time_config4(n_total, world, rank, dev, stream, max_over_ranks, backend, gather=True, steps=5):
+    """Config 4: one batch of n_total config-3b objects split
+    over the ranks by payload bytes.  Every rank derives the same cuts from
+    the batch's lengths (dist.shard_ranges on the device), generates its shard
+    in HBM, hashes it straight into its rows of the full (n_total, 17)
+    coordinate matrix (timed with HIP events, max over ranks = the hash
+    phase), then the rows are all-gathered in place (RCCL over xGMI; timed
+    apart), and copied to pinned host memory as the cheaper gather-to-host
+    alternative.  Strong scaling: the batch is the same at every N."""
+    import torch
+    import torch.distributed as dist
+
+    from hyperdex_amd import _lib, synth
+    from hyperdex_amd import dist as hdist
+    from hyperdex_amd.hashing import hash_batch
+    rules = synth.CONFIGS["cfg3b"]
+    A = len(rules)
+    cr = synth.c_rules(rules)
+    lib = _lib.lib()
+    # the whole batch's lengths, in chunks (identical on every rank), -> sizes
+    sizes = torch.empty(n_total, dtype=torch.int64, device=dev)
+    chunk = 8_000_000
+    tmp = torch.empty(chunk * A, dtype=torch.int32, device=dev)
+    for f in range(0, n_total, chunk):
+        c = min(chunk, n_total - f)
+        _lib.check(lib.hdx_synth_lengths(cr, A, synth.SEED, f, c, tmp.data_ptr(), stream.cuda_stream))
+        sizes[f:f + c] = tmp[:c * A].view(c, A).to(torch.int64).sum(dim=1)
+    del tmp
+    ranges = hdist.shard_ranges(n_total, world, sizes)
+    counts = [c for _, c in ranges]
+    first, cnt = ranges[rank]
+    shard_bytes = int(sizes[first:first + cnt].sum().item())
+    del sizes
+    types, blob, base, lens = synth.make_batch_device("cfg3b", cnt, first=first, device=dev)
+    out = torch.empty((n_total, A), dtype=torch.int64, device=dev)
+    mine = hdist.rank_rows(out, counts, rank)
+
+    def run():
+        hash_batch(types, blob, base, lens, coords=mine, stream=stream)
+    run()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    for s, e in ev:
+        s.record(stream)
+        run()
+        e.record(stream)
+    torch.cuda.synchronize()
+    (hash_ms,) = max_over_ranks(float(np.mean([s.elapsed_time(e) for s, e in ev])))
+    payload_total = float(shard_bytes)
+    if world > 1:
+        t = torch.tensor([payload_total], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(t)
+        payload_total = float(t.item())
+    algo_rank = shard_bytes + cnt * A * ALGO_EXTRA_PER_ATTR
+    res = {"workload": "config 4: %dM config-3b objects sharded over %d GPU(s) by payload bytes"
+                       % (n_total // 1_000_000, world),
+           "objects": n_total, "objects_per_rank": counts, "hash_ms": round(hash_ms, 4),
+           "mobjects_per_s": round(n_total / (hash_ms / 1e3) / 1e6, 1),
+           "GiB_s": round(payload_total / (hash_ms / 1e3) / 2**30, 2),
+           "rank0_roofline_frac": round(algo_rank / (hash_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+           "scaling": "strong"}
+    if gather and world > 1:
+        src = mine if backend == "nccl" else mine[: min(cnt, 100_000)].cpu()
+        cnts = counts if backend == "nccl" else [min(c, 100_000) for c in counts]
+        gout = out if backend == "nccl" else None
+        hdist.allgather_coords(src, cnts, out=gout)
+        torch.cuda.synchronize()
+        dist.barrier()
+        reps = 3
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            hdist.allgather_coords(src, cnts, out=gout)
+        torch.cuda.synchronize()
+        (dt,) = max_over_ranks((time.perf_counter() - t0) / reps)
+        nbytes = int(sum(cnts)) * A * 8
+        res["allgather"] = {"ms": round(dt * 1e3, 3), "bytes": nbytes, "backend": backend,
+                            "equal_counts": len(set(cnts)) == 1,
+                            "algbw_GBps": round(nbytes / dt / 1e9, 2),
+                            "busbw_GBps": round(nbytes * (world - 1) / world / dt / 1e9, 2)}
+        res["end_to_end_ms"] = round(hash_ms + dt * 1e3, 3)
+    # gather to host instead: every rank copies its rows to pinned memory at once
+    host = torch.empty(mine.shape, dtype=mine.dtype, pin_memory=True)
+    host.copy_(mine, non_blocking=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    host.copy_(mine, non_blocking=True)
+    torch.cuda.synchronize()
+    (d2h,) = max_over_ranks(time.perf_counter() - t0)
+    res["d2h_local_rows_ms"] = round(d2h * 1e3, 3)
+    del host, out, mine, blob, base, lens
+    torch.cuda.empty_cache()
     return res
 
 
@@ -433,19 +547,39 @@ def time_fused_batch(types, blob, base, lens, n, A, dev, stream, max_over_ranks,
 
 def latest_traffic_file():
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")),
+                   key=lambda p: int(os.path.basename(os.path.dirname(p))[1:] or 0))
     return files[-1] if files else ""
+
+
+def source_digest():
+    """sha256 over the kernel and C-ABI sources (what the PMC counters measured):
+    a traffic.json recorded from other sources is not this build's traffic."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    pats = ("hyperdex_amd/csrc/*.hip", "hyperdex_amd/csrc/*.h", "hyperdex_amd/csrc/*.cpp",
+            "hyperdex_amd/csrc/Makefile", "include/*.h")
+    for f in sorted(p for pat in pats for p in glob.glob(os.path.join(ROOT, pat))):
+        h.update(os.path.relpath(f, ROOT).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
 
 
 def measured_traffic(path, cfg, n):
     """HBM bytes per launch for this config from the committed PMC summary
-    (scripts/gpu_profile.sh -> scripts/traffic_from_pmc.py), scaled to n."""
+    (scripts/profile_r2.sh -> scripts/traffic_from_pmc.py), scaled to n, or
+    (None, why) when the file was measured on other kernel sources."""
     try:
-        rec = json.load(open(path))[cfg]
+        doc = json.load(open(path))
+        rec = doc[cfg]
     except (OSError, KeyError, ValueError):
-        return None
+        return None, "no PMC record for %s" % cfg
+    if doc.get("source_digest") != source_digest():
+        return None, "%s measured other kernel sources (digest %s, this build %s)" % (
+            os.path.relpath(path, ROOT), doc.get("source_digest"), source_digest())
     per_obj = rec["traffic_bytes"] / rec.get("objects", 10_000_000)
-    return int(per_obj * n)
+    return int(per_obj * n), "%s (rocprofv3 PMC, digest %s)" % (os.path.relpath(path, ROOT), source_digest())
 
 
 def time_host_path(types, blob, base, lens, A, n_host=2_000_000):
@@ -485,7 +619,7 @@ def cpu_baseline(types, blob, base, lens, A, seconds, coords):
     on a bounded sample of the same batch.  Also verifies the sample's GPU
     coordinates against it (a failed check aborts the bench)."""
     from oracle import oracle
-    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")), 16)
+    threads = len(os.sched_getaffinity(0))  # every core this process may run on
     ns = min(200_000, base.numel())
     nb = int((base[ns - 1] + lens.view(-1, A)[ns - 1].to(dtype=base.dtype).sum()).item())
     hb = blob[:nb].cpu().numpy()
@@ -520,7 +654,18 @@ def cpu_baseline(types, blob, base, lens, A, seconds, coords):
             "single_thread_GiB_s": round(one_b / 2**30, 3),
             "sample": "%d objects (%.0f MB) of the same batch, %d passes, oracle/hdx_oracle.c -O2 "
                       "pthreads; verified equal to the GPU coords" % (ns, nb / 1e6, reps),
-            "cpu_model": model}
+            "cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": threads,
+            "cgroup_cpu_quota_cores": cgroup_cpu_quota(),
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def cgroup_cpu_quota():
+    """CPU cores the cgroup allows (cpu.max quota / period), None if unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
 
 
 def cpu_baseline_encoded(types, enc, A, seconds, coords):

@@ -30,8 +30,9 @@ def main():
     import torch
 
     import hyperdex_amd as hdx
-    from hyperdex_amd import synth
-    lib = hdx.lib()
+    from hyperdex_amd import _lib, synth
+    ctx = _lib.debug_library()  # the A/B selection lives in libhdxhash_dbg.so only
+    lib = ctx.__enter__()
     dev = torch.device("cuda", 0)
     variants = [int(v) for v in args.variants.split(",")]
     checked = set(int(v) for v in args.check.split(",")) if args.check else set(variants) - {40, 41, 57, 58}

@@ -19,9 +19,9 @@ def main():
     import torch
 
     import hyperdex_amd as hdx
-    from hyperdex_amd import synth
-    if a.variant >= 0:
-        assert hdx.lib().hdxdbg_set_kernel_variant(a.variant) >= -1
+    from hyperdex_amd import _lib, synth
+    if a.variant >= 0:  # a selected variant runs from the debug library
+        _lib.debug_library(a.variant).__enter__()
     dev = torch.device("cuda", 0)
     if a.config == "cfg5":  # stored-object sweep over config-3b objects
         types, *enc = synth.make_encoded_device("cfg3b", a.objects, device=dev)

@@ -37,6 +37,13 @@ def main(fetch_dir, write_dir, config, out, objects="10000000"):
     data = {}
     if os.path.exists(out):
         data = json.load(open(out))
+    # the kernel sources these counters measured (bench.py refuses other sources' traffic)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    digest = bench.source_digest()
+    if data.get("source_digest") not in (None, digest):
+        data = {}  # an older build's records are not this build's traffic
+    data["source_digest"] = digest
     data[config] = rec
     json.dump(data, open(out, "w"), indent=1)
     print(json.dumps(rec))

@@ -1,4 +1,7 @@
-"""Sharded batches on world_size 2 (gloo, CPU): shard_ranges + allgather_coords.
+"""Sharded batches on world_size 2 and 3 (gloo, CPU): shard_ranges +
+hash_sharded + allgather_coords — the code path bench.py's config 4 runs
+(byte-balanced shards, each rank hashing straight into its rows of the full
+coordinate matrix, the all-gather filling the rest in place).
 
 The per-shard coordinates come from the oracle here (no GPU on this host);
 the GPU path runs the same functions over RCCL in bench.py --gpus N."""
@@ -34,6 +37,16 @@ def test_shard_ranges_byte_balanced():
         assert max(per) - min(per) <= 2 * sizes.max()
 
 
+def test_shard_ranges_torch_matches_numpy():
+    """bench.py computes the byte-balanced cuts on the device (torch); they
+    equal the host form's."""
+    rng = np.random.default_rng(5)
+    for n in (0, 1, 17, 5000):
+        sizes = rng.integers(0, 3000, n)
+        for world in (1, 2, 3, 8):
+            assert hdist.shard_ranges(n, world, torch.from_numpy(sizes)) == hdist.shard_ranges(n, world, sizes)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -47,19 +60,32 @@ def _worker(rank, world, port, ret):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle
-    n = 301
-    types, blob, base, lens = synth.make_batch_host("cfg3b", n, seed=42)
-    A = len(types)
-    sizes = lens.reshape(n, A).astype(np.int64).sum(axis=1)
-    ranges = hdist.shard_ranges(n, world, sizes)
-    first, cnt = ranges[rank]
-    local, err = oracle.hash_batch(types, blob, base[first:first + cnt],
-                                   lens[first * A:(first + cnt) * A])
-    assert err == 0
-    full = hdist.allgather_coords(torch.from_numpy(local.view(np.int64).copy()),
-                                  [c for _, c in ranges])
-    want, _ = oracle.hash_batch(types, blob, base, lens)
-    ret[rank] = bool(np.array_equal(full.numpy().view(np.uint64), want))
+    ok = True
+    for n in (301, 64):  # byte-balanced (unequal counts), then an even split
+        types, blob, base, lens = synth.make_batch_host("cfg3b", n, seed=42)
+        A = len(types)
+        sizes = torch.from_numpy(lens.reshape(n, A).astype(np.int64).sum(axis=1))
+        ranges = hdist.shard_ranges(n, world, sizes if n == 301 else None)
+        counts = [c for _, c in ranges]
+        first, cnt = ranges[rank]
+
+        def oracle_into(t, b, o, l, coords):  # stands in for the gfx950 kernel
+            got, err = oracle.hash_batch(t, b, o.numpy().view(np.uint64), l.numpy().view(np.uint32))
+            assert err == 0
+            coords.copy_(torch.from_numpy(got.view(np.int64)))
+
+        out = torch.full((n, A), -1, dtype=torch.int64)
+        mine = hdist.rank_rows(out, counts, rank)
+        full = hdist.hash_sharded(types, blob, torch.from_numpy(base[first:first + cnt].view(np.int64)),
+                                  torch.from_numpy(lens[first * A:(first + cnt) * A].view(np.int32)),
+                                  counts, out=out, hash_fn=oracle_into)
+        want, _ = oracle.hash_batch(types, blob, base, lens)
+        ok &= full.data_ptr() == out.data_ptr() == mine.data_ptr() - first * A * 8  # in place
+        ok &= bool(np.array_equal(full.numpy().view(np.uint64), want))
+        # a separately hashed block is copied into place, then gathered
+        again = hdist.allgather_coords(mine.clone(), counts)
+        ok &= bool(np.array_equal(again.numpy().view(np.uint64), want))
+    ret[rank] = ok
     dist.destroy_process_group()
 
 
@@ -85,5 +111,9 @@ def test_hash_sharded_rccl_world1():
         want = hashing.hash_batch(types, blob, base, lens)
         torch.cuda.synchronize()
         assert torch.equal(full, want)
+        out = torch.empty((5000, len(types)), dtype=torch.int64, device=dev)
+        assert hdist.hash_sharded(types, blob, base, lens, [5000], out=out).data_ptr() == out.data_ptr()
+        torch.cuda.synchronize()
+        assert torch.equal(out, want)
     finally:
         dist.destroy_process_group()
