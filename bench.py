@@ -619,7 +619,13 @@ def cpu_baseline(types, blob, base, lens, A, seconds, coords):
     on a bounded sample of the same batch.  Also verifies the sample's GPU
     coordinates against it (a failed check aborts the bench)."""
     from oracle import oracle
-    threads = len(os.sched_getaffinity(0))  # every core this process may run on
+    # every core this process may use: the affinity set, capped by the cgroup's
+    # CPU quota (on the GPU box 256 logical CPUs are visible but cpu.max allows
+    # 16 cores; 256 threads under that quota measured 3x slower than 16)
+    quota = cgroup_cpu_quota()
+    threads = len(os.sched_getaffinity(0))
+    if quota:
+        threads = max(1, min(threads, int(quota)))
     ns = min(200_000, base.numel())
     nb = int((base[ns - 1] + lens.view(-1, A)[ns - 1].to(dtype=base.dtype).sum()).item())
     hb = blob[:nb].cpu().numpy()
@@ -655,7 +661,7 @@ def cpu_baseline(types, blob, base, lens, A, seconds, coords):
             "sample": "%d objects (%.0f MB) of the same batch, %d passes, oracle/hdx_oracle.c -O2 "
                       "pthreads; verified equal to the GPU coords" % (ns, nb / 1e6, reps),
             "cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": threads,
-            "cgroup_cpu_quota_cores": cgroup_cpu_quota(),
+            "cgroup_cpu_quota_cores": quota,
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 

@@ -11,13 +11,15 @@
 //                     outside the lock, then sleep on the slot's generation;
 //   flush thread      seals the FILLING slot as soon as no batch is in flight,
 //                     when it is full, or max_delay after its first object;
-//                     waits for the slot's writers to finish, then launches the
-//                     hash kernel and one lookup kernel for all tables on the
-//                     slot's own stream.  By default the kernels read the
-//                     pinned staging and write coordinates / region ids into
-//                     pinned memory in place (two launches per batch, no
-//                     copies); HDX_BATCHER_STAGE_DEVICE stages through HBM
-//                     (H2D, kernels, D2H) instead;
+//                     waits for the slot's writers to finish, then launches,
+//                     on the slot's own stream, ONE kernel that hashes the
+//                     batch and looks every object up in the space's tables
+//                     (hash_regroup_regions_kernel, <= 4 tables; more tables:
+//                     the hash kernel + one lookup kernel for all of them).
+//                     By default the kernel reads the pinned staging and
+//                     writes coordinates / region ids into pinned memory in
+//                     place (no copies); HDX_BATCHER_STAGE_DEVICE stages
+//                     through HBM (H2D, kernel, D2H) instead;
 //   completion thread waits for each shipped slot's stream in order, publishes
 //                     the status and wakes the slot's callers, who copy their
 //                     rows out; the last reader frees the slot.
@@ -182,8 +184,8 @@ hdx_status alloc_slot(hdx_batcher_s* b, Slot& s, uint32_t cap_obj, uint64_t cap_
     return HDX_OK;
 }
 
-// Hash kernel + one lookup kernel for all tables on the slot's stream
-// (asynchronous), with H2D / D2H around them when staging through HBM.
+// One fused hash + lookup launch on the slot's stream (asynchronous; two
+// launches beyond 4 tables), with H2D / D2H around it when staging through HBM.
 hipError_t ship(hdx_batcher_s* b, Slot& s) {
     hipError_t e;
     const uint32_t n = s.nobj;
@@ -205,9 +207,29 @@ hipError_t ship(hdx_batcher_s* b, Slot& s) {
     a.A = b->A;
     std::memcpy(a.codes, b->codes, b->A);
     finalize_args(a);
-    SHIP_TRY(launch_hash_batch(a, s.stream));
     const size_t region_base = (size_t)s.cap_obj * b->A;
-    if (!b->tables.empty()) {
+    if (!b->tables.empty() && b->tables.size() <= kMaxSweepTables && b->A <= 128) {
+        // one launch: hash + every table's lookup_region (hash_regroup_regions_kernel)
+        a.T = (uint32_t)b->tables.size();
+        for (uint32_t t = 0; t < a.T; ++t) {
+            const hdx_region_table tb = b->tables[t];
+            a.t[t].index = tb->d_index;
+            a.t[t].lower = tb->d_lower;
+            a.t[t].upper = tb->d_upper;
+            a.t[t].ids = tb->d_ids;
+            a.t[t].out = s.d_out + region_base + (size_t)t * s.cap_obj;
+            a.t[t].W = tb->W;
+            a.t[t].D = tb->D;
+            a.t[t].R = tb->R;
+            a.t[t].index_words = tb->index_words;
+            std::memcpy(a.t[t].attrs, tb->attrs, sizeof a.t[t].attrs);
+        }
+        SHIP_TRY(launch_hash_batch_regions(a, s.stream));
+    } else {
+        SHIP_TRY(launch_hash_batch(a, s.stream));
+    }
+    if (b->tables.size() > kMaxSweepTables || (!b->tables.empty() && b->A > 128)) {
+        // more tables than the fused kernel takes: one lookup kernel for all of them
         MultiRegionArgs r{};
         r.coords = s.d_out;
         r.out = s.d_out + region_base;

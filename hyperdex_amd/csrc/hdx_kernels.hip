@@ -382,6 +382,209 @@ hash_regroup_regions_kernel(const BatchArgs args) {
     regroup_body<C, true, SORT, true, A4, false, ASORT, ORDER, true>(args, lds, tbl);
 }
 
+// ===========================================================================
+// Workgroup-sorted kernel (variants 60-65): the class sort of the regroup
+// kernel over the whole workgroup's 4 * C * 64 slots instead of one wave's
+// C * 64.  A wave's share of the work and of the L2 working set is the same as
+// a C-chunk regroup wave (C passes of 64 slots, one 8.7 KB window of config
+// 3b per 2 chunks), but the sort window is four times larger, so far fewer
+// passes mix CityHash regimes and > 64-byte loop counts:
+//   phase 1  each wave describes its C chunks ({pointer, length, code} into
+//            the workgroup's LDS, as the regroup kernel does) and counts its
+//            slots per class (ballots);
+//   barrier  per-class totals -> each wave's base in the class-sorted order;
+//            every slot writes its local index at its sorted position;
+//   barrier  passes of 64 sorted slots: static (wave w takes passes w, w+4,
+//            ...) or dynamic (an LDS counter hands out passes, costliest
+//            classes first); A4 loads with the next pass in flight; each
+//            coordinate is stored straight to its slot (the workgroup's
+//            4 * C * 64 coordinates are one contiguous 4-8 KB range, merged
+//            in L2).
+// ORDER 10: classes by falling cost (> 64 B by blocks 4+, 3, 2, 1; 17..32;
+// <= 16; 33..64; numerics); ORDER 11: rising cost.
+// ===========================================================================
+constexpr int kWgClasses = 9;  // 8 work classes + the padding slots past the batch end
+
+template <int ORDER>
+__device__ __forceinline__ uint32_t wg_class(uint32_t code, uint32_t n, bool valid) {
+    if (!valid) return 8;
+    uint32_t k;  // 0 = cheapest .. 7 = costliest
+    if (code != CODE_STRING) {
+        k = 0;
+    } else if (n > 64) {
+        const uint32_t b = (n - 1) >> 6;
+        k = b >= 4 ? 7u : 3u + b;
+    } else {
+        k = n > 32 ? 1u : n <= 16 ? 2u : 3u;
+    }
+    return ORDER == 10 ? 7u - k : k;
+}
+
+template <int C>
+struct WgSortLds {
+    SlotDesc desc[4 * C * 64];
+    uint16_t perm[4 * C * 64];
+    uint32_t cnt[4][kWgClasses + 1];
+    uint32_t next;
+};
+
+template <int C, int ORDER, bool DYN>
+__global__ void __launch_bounds__(256)
+hash_wgsort_kernel(const BatchArgs args) {
+    __shared__ WgSortLds<C> lds;
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    constexpr uint32_t S = 4 * C * 64;  // slots per workgroup
+    const uint32_t A = args.A;
+    const uint64_t nslots = args.n * A;
+    const uint64_t qg = (uint64_t)blockIdx.x * S;  // < nslots (grid sized by the host)
+    const uint32_t nv = (uint32_t)min<uint64_t>(S, nslots - qg);  // valid slots of the workgroup
+    const uint64_t qw = qg + (uint64_t)w * (C * 64);
+    const bool wave_live = qw < nslots;  // trailing waves of the last workgroup have no slots
+
+    // ---- phase 1: descriptors + classes (the regroup kernel's, per wave) ------
+    uint32_t cls[C];
+    if (wave_live) {
+        uint64_t i0;
+        uint32_t j0;
+        split_slot(qw, A, args.inv_A, i0, j0);
+        uint32_t carry = 0;
+        for (uint32_t k = 0; k < j0; k += 64) {
+            const uint32_t idx = k + (uint32_t)lane;
+            const uint32_t v = idx < j0 ? args.attr_len[qw - j0 + idx] : 0u;
+            carry += wave_sum_dpp(v);
+        }
+        const uint64_t last_slot = nslots - 1;
+        uint32_t Lraw[C];
+#pragma unroll
+        for (int c = 0; c < C; ++c) Lraw[c] = args.attr_len[min(qw + c * 64 + lane, last_slot)];
+        uint32_t packed_codes = 0;
+        if (args.uniform_code == 0xffu) packed_codes = reinterpret_cast<const uint32_t*>(args.codes)[lane];
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const uint32_t t = j0 + (uint32_t)(c * 64 + lane);
+            const uint32_t di = div_small(t, args.a_magic);
+            const uint32_t j = t - di * A;
+            const bool valid = qw + c * 64 + lane < nslots;
+            const uint64_t il = valid ? i0 + di : i0;
+            const uint64_t base = args.obj_base[il];
+            const uint32_t L = valid ? Lraw[c] : 0u;
+            const uint32_t Sx = wave_scan_dpp(L) - L;
+            const int head = lane - (int)j;
+            const uint32_t head_sx = __shfl(Sx, head < 0 ? 0 : head, 64);
+            const uint32_t off = head >= 0 ? Sx - head_sx : carry + Sx;
+            carry = __builtin_amdgcn_readlane(off + L, 63);
+            uint32_t code = args.uniform_code != 0xffu
+                                ? args.uniform_code
+                                : (__shfl(packed_codes, (int)(j >> 2), 64) >> (8 * (j & 3))) & 0xffu;
+            if (!valid) code = CODE_ZERO;
+            SlotDesc d;
+            d.p = args.blob + base + off;
+            d.n = L;
+            d.code_slot = code;
+            lds.desc[w * (C * 64) + c * 64 + lane] = d;
+            cls[c] = wg_class<ORDER>(code, L, valid);
+        }
+    } else {
+#pragma unroll
+        for (int c = 0; c < C; ++c) cls[c] = 8;
+    }
+    // per-class counts of this wave and each slot's rank within them
+    uint32_t rank[C];
+    uint32_t mycnt = 0;  // lane k < kWgClasses: this wave's slots of class k
+#pragma unroll
+    for (int k = 0; k < kWgClasses; ++k) {
+        uint32_t run = 0;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const uint64_t m = __ballot(cls[c] == (uint32_t)k);
+            if (cls[c] == (uint32_t)k)
+                rank[c] = run + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            run += (uint32_t)__popcll(m);
+        }
+        if (lane == k) mycnt = run;
+    }
+    if (lane < kWgClasses) lds.cnt[w][lane] = mycnt;
+    if (DYN && threadIdx.x == 0) lds.next = 0;
+    __syncthreads();
+
+    // ---- sorted positions: class start + this wave's base within the class ----
+    uint32_t base_k = 0;
+    if (lane < kWgClasses) {
+        uint32_t tot = 0, before = 0;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const uint32_t x = lds.cnt[v][lane];
+            tot += x;
+            before += v < w ? x : 0u;
+        }
+        base_k = before + (wave_scan_dpp(tot) - tot);  // lanes >= kWgClasses add 0 to the scan
+    } else {
+        (void)wave_scan_dpp(0u);
+    }
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const uint32_t pos = __shfl(base_k, (int)cls[c], 64) + rank[c];
+        lds.perm[pos] = (uint16_t)(w * (C * 64) + c * 64 + lane);
+    }
+    __syncthreads();
+
+    // ---- phase 2: class-homogeneous passes, next pass in flight --------------
+    const uint32_t npass = (nv + 63) / 64;
+    struct Pass {
+        uint32_t s;  // local slot, or ~0u for a padding lane
+        SlotDesc d;
+        Raw blk;
+    };
+    auto load_pass = [&](uint32_t p, Pass& P) {
+        const uint32_t idx = p * 64 + (uint32_t)lane;
+        const bool act = p < npass && idx < nv;
+        P.s = act ? (uint32_t)lds.perm[idx] : ~0u;
+        if (act) {
+            P.d = lds.desc[P.s];
+        } else {
+            P.d.p = g_zero_pad;
+            P.d.n = 0;
+            P.d.code_slot = CODE_ZERO;
+        }
+        P.blk = issue_any<true>(P.d.code_slot & 0xffu, P.d.p, P.d.n);
+    };
+    auto grab = [&](uint32_t t) -> uint32_t {
+        if constexpr (DYN) {
+            uint32_t p = 0;
+            if (lane == 0) p = __hip_atomic_fetch_add(&lds.next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return __builtin_amdgcn_readfirstlane(p);
+        } else {
+            return (uint32_t)w + 4 * t;
+        }
+    };
+    bool bad = false;
+    Pass P0, P1;
+    uint32_t pcur = grab(0);
+    load_pass(pcur, P0);
+    for (uint32_t t = 0; pcur < npass; ++t) {
+        Pass& cur = (t & 1) ? P1 : P0;
+        Pass& nxt = (t & 1) ? P0 : P1;
+        const uint32_t pnext = grab(t + 1);
+        if (pnext < npass) load_pass(pnext, nxt);
+        const uint64_t h = hash_blk<false, false, true>(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n,
+                                                        consume_any<true>(cur.blk), bad);
+        if (cur.s != ~0u) args.coords[qg + cur.s] = h;
+        pcur = pnext;
+    }
+    if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
+}
+
+template <int C, int ORDER, bool DYN>
+static hipError_t launch_wgsort(const BatchArgs& args, hipStream_t stream) {
+    const uint64_t S = 4 * C * 64;
+    const uint64_t blocks = (args.n * args.A + S - 1) / S;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((hash_wgsort_kernel<C, ORDER, DYN>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    return hipGetLastError();
+}
+
 template <int C, bool NT, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false,
           bool ASORT = false, int ORDER = 0>
 static hipError_t launch_regroup(const BatchArgs& args, hipStream_t stream) {
@@ -425,6 +628,12 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 38: return launch_regroup<2, true, true, true, true, false, true>(args, stream);
         case 39: return launch_regroup<8, true, true, true, false, false, true>(args, stream);
         case 45: return launch_regroup<2, true, true, true, true, false, true, 2>(args, stream);
+        case 60: return launch_wgsort<2, 10, false>(args, stream);
+        case 61: return launch_wgsort<2, 10, true>(args, stream);
+        case 62: return launch_wgsort<2, 11, false>(args, stream);
+        case 63: return launch_wgsort<4, 10, true>(args, stream);
+        case 64: return launch_wgsort<1, 10, true>(args, stream);
+        case 65: return launch_wgsort<3, 10, true>(args, stream);
         // debug shapes: WRONG coordinates, debug library only
         case 40: return launch_chunk<true, false, 1>(args, stream);  // loads only
         case 41: return launch_chunk<true, false, 2>(args, stream);  // arithmetic only
@@ -489,6 +698,7 @@ static bool known_variant(int v) {
     switch (v) {
         case -1: case 12: case 18: case 19: case 20: case 21: case 25: case 26: case 30: case 31: case 35: case 37:
         case 38: case 39: case 44: case 45: case 46:
+        case 60: case 61: case 62: case 63: case 64: case 65:
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;
