@@ -428,7 +428,7 @@ struct WgSortLds {
     uint32_t next;
 };
 
-template <int C, int ORDER, bool DYN>
+template <int C, int ORDER, bool DYN, bool PARK = false, bool NOSORT = false>
 __global__ void __launch_bounds__(256)
 hash_wgsort_kernel(const BatchArgs args) {
     __shared__ WgSortLds<C> lds;
@@ -524,8 +524,9 @@ hash_wgsort_kernel(const BatchArgs args) {
     }
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-        const uint32_t pos = __shfl(base_k, (int)cls[c], 64) + rank[c];
-        lds.perm[pos] = (uint16_t)(w * (C * 64) + c * 64 + lane);
+        const uint32_t me = w * (C * 64) + c * 64 + lane;
+        const uint32_t pos = NOSORT ? me : __shfl(base_k, (int)cls[c], 64) + rank[c];
+        lds.perm[pos] = (uint16_t)me;
     }
     __syncthreads();
 
@@ -559,29 +560,48 @@ hash_wgsort_kernel(const BatchArgs args) {
         }
     };
     bool bad = false;
+    auto hash_store = [&](const Pass& P) {
+        const uint64_t h = hash_blk<false, false, true>(P.d.code_slot & 0xffu, P.d.p, P.d.n,
+                                                        consume_any<true>(P.blk), bad);
+        if (P.s != ~0u) {
+            if (PARK) reinterpret_cast<uint64_t*>(lds.desc)[2 * P.s] = h;  // over its consumed descriptor
+            else args.coords[qg + P.s] = h;
+        }
+    };
+    // two named register sets, unrolled by hand: a runtime-selected reference
+    // to either would put both on scratch
     Pass P0, P1;
-    uint32_t pcur = grab(0);
-    load_pass(pcur, P0);
-    for (uint32_t t = 0; pcur < npass; ++t) {
-        Pass& cur = (t & 1) ? P1 : P0;
-        Pass& nxt = (t & 1) ? P0 : P1;
-        const uint32_t pnext = grab(t + 1);
-        if (pnext < npass) load_pass(pnext, nxt);
-        const uint64_t h = hash_blk<false, false, true>(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n,
-                                                        consume_any<true>(cur.blk), bad);
-        if (cur.s != ~0u) args.coords[qg + cur.s] = h;
-        pcur = pnext;
+    uint32_t t = 0;
+    uint32_t p0 = grab(t++);
+    if (p0 < npass) load_pass(p0, P0);
+    while (p0 < npass) {
+        const uint32_t p1 = grab(t++);
+        if (p1 < npass) load_pass(p1, P1);
+        hash_store(P0);
+        if (p1 >= npass) break;
+        p0 = grab(t++);
+        if (p0 < npass) load_pass(p0, P0);
+        hash_store(P1);
+    }
+    if constexpr (PARK) {  // every coordinate parked: coalesced stores in slot order
+        __syncthreads();
+        const uint64_t* res = reinterpret_cast<const uint64_t*>(lds.desc);
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const uint32_t sl = w * (C * 64) + c * 64 + lane;
+            if (sl < nv) __builtin_nontemporal_store(res[2 * sl], args.coords + qg + sl);
+        }
     }
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <int C, int ORDER, bool DYN>
+template <int C, int ORDER, bool DYN, bool PARK = false, bool NOSORT = false>
 static hipError_t launch_wgsort(const BatchArgs& args, hipStream_t stream) {
     const uint64_t S = 4 * C * 64;
     const uint64_t blocks = (args.n * args.A + S - 1) / S;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_wgsort_kernel<C, ORDER, DYN>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_wgsort_kernel<C, ORDER, DYN, PARK, NOSORT>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
     return hipGetLastError();
 }
 
@@ -634,6 +654,10 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 63: return launch_wgsort<4, 10, true>(args, stream);
         case 64: return launch_wgsort<1, 10, true>(args, stream);
         case 65: return launch_wgsort<3, 10, true>(args, stream);
+        case 66: return launch_wgsort<2, 10, true, true>(args, stream);
+        case 67: return launch_wgsort<2, 10, true, true, true>(args, stream);
+        case 68: return launch_wgsort<1, 10, true, true>(args, stream);
+        case 69: return launch_wgsort<4, 10, true, true>(args, stream);
         // debug shapes: WRONG coordinates, debug library only
         case 40: return launch_chunk<true, false, 1>(args, stream);  // loads only
         case 41: return launch_chunk<true, false, 2>(args, stream);  // arithmetic only
@@ -698,7 +722,7 @@ static bool known_variant(int v) {
     switch (v) {
         case -1: case 12: case 18: case 19: case 20: case 21: case 25: case 26: case 30: case 31: case 35: case 37:
         case 38: case 39: case 44: case 45: case 46:
-        case 60: case 61: case 62: case 63: case 64: case 65:
+        case 60: case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;
