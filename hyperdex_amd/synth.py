@@ -57,6 +57,10 @@ CONFIGS = {
     # test-only: many attributes, all strings of every length class
     "wide": [Rule(dt.HYPERDATATYPE_STRING, UNIFORM, 0, 130)] * 70,
     "keyonly_long": [Rule(dt.HYPERDATATYPE_STRING, UNIFORM, 200, 4000)],
+    # measurement-only: 17 attributes of one CityHash regime / loop count each
+    "u8": [_s(8)] * 17, "u24": [_s(24)] * 17, "u48": [_s(48)] * 17, "u100": [_s(100)] * 17,
+    "u150": [_s(150)] * 17, "u190": [_s(190)] * 17,
+    "num": [_n(dt.HYPERDATATYPE_INT64)] * 17, "flt": [_n(dt.HYPERDATATYPE_FLOAT)] * 17,
 }
 
 

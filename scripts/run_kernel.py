@@ -20,8 +20,10 @@ def main():
 
     import hyperdex_amd as hdx
     from hyperdex_amd import _lib, synth
-    if a.variant >= 0:  # a selected variant runs from the debug library
-        _lib.debug_library(a.variant).__enter__()
+    ctx = None
+    if a.variant >= 0:  # a selected variant runs from the debug library (keep ctx alive:
+        ctx = _lib.debug_library(a.variant)  # a collected context manager restores the product lib)
+        ctx.__enter__()
     dev = torch.device("cuda", 0)
     if a.config == "cfg5":  # stored-object sweep over config-3b objects
         types, *enc = synth.make_encoded_device("cfg3b", a.objects, device=dev)
