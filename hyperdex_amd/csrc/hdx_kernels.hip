@@ -383,6 +383,173 @@ hash_regroup_regions_kernel(const BatchArgs args) {
 }
 
 // ===========================================================================
+// Typed regroup kernel (variants 70-73): the regroup kernel's wave-local class
+// sort (ORDER 1), with the non-string slots (int64 / float / timestamps /
+// non-hashable, class 0) taken out of the 64-lane passes: they are hashed in
+// a lean loop of their own — two dword loads and two v_alignbyte per value,
+// no descriptor-driven 16-byte pieces, no CityHash code in the loop — and
+// only the strings, sorted by regime and loop count, fill the passes
+// (DESIGN.md §4.9).  Config 3b measured 373 VALU per 128 numeric slots through
+// the string-shaped passes (profiles/r2/regime_costs_v44.txt).
+// ===========================================================================
+template <int C>
+struct TypedLds {
+    SlotDesc desc[4][C * 64];
+    uint16_t perm[4][C * 64];
+    uint32_t cnt[4][kClasses];
+};
+
+template <int C>
+__global__ void __launch_bounds__(256)
+hash_typed_kernel(const BatchArgs args) {
+    __shared__ TypedLds<C> lds;
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    SlotDesc* desc = lds.desc[w];
+    uint16_t* perm = lds.perm[w];
+    uint64_t* res = reinterpret_cast<uint64_t*>(desc);  // res[2*s] = first 8 bytes of desc[s]
+
+    const uint64_t wave = (uint64_t)blockIdx.x * 4 + w;
+    const uint32_t A = args.A;
+    const uint64_t nslots = args.n * A;
+    const uint64_t qw = wave * (uint64_t)(C * 64);
+    if (qw >= nslots) return;  // no workgroup barrier anywhere: waves are independent
+
+    uint64_t i0;
+    uint32_t j0;
+    split_slot(qw, A, args.inv_A, i0, j0);
+    uint32_t carry = 0;
+    for (uint32_t k = 0; k < j0; k += 64) {
+        const uint32_t idx = k + (uint32_t)lane;
+        const uint32_t v = idx < j0 ? args.attr_len[qw - j0 + idx] : 0u;
+        carry += wave_sum_dpp(v);
+    }
+    const uint64_t last_slot = nslots - 1;
+    uint32_t Lraw[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) Lraw[c] = args.attr_len[min(qw + c * 64 + lane, last_slot)];
+    uint32_t packed_codes = 0;
+    if (args.uniform_code == 0xffu) packed_codes = reinterpret_cast<const uint32_t*>(args.codes)[lane];
+
+    // ---- phase 1: descriptors + classes (ORDER 1: class 0 = every non-string)
+    uint32_t cls[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const uint32_t t = j0 + (uint32_t)(c * 64 + lane);
+        const uint32_t di = div_small(t, args.a_magic);
+        const uint32_t j = t - di * A;
+        const bool valid = qw + c * 64 + lane < nslots;
+        const uint64_t il = valid ? i0 + di : i0;
+        const uint64_t base = args.obj_base[il];
+        const uint32_t L = valid ? Lraw[c] : 0u;
+        const uint32_t Sx = wave_scan_dpp(L) - L;
+        const int head = lane - (int)j;
+        const uint32_t head_sx = __shfl(Sx, head < 0 ? 0 : head, 64);
+        const uint32_t off = head >= 0 ? Sx - head_sx : carry + Sx;
+        carry = __builtin_amdgcn_readlane(off + L, 63);
+        uint32_t code = args.uniform_code != 0xffu
+                            ? args.uniform_code
+                            : (__shfl(packed_codes, (int)(j >> 2), 64) >> (8 * (j & 3))) & 0xffu;
+        if (!valid) code = CODE_ZERO;
+        SlotDesc d;
+        d.p = args.blob + base + off;
+        d.n = L;
+        d.code_slot = code | ((uint32_t)(c * 64 + lane) << 8);
+        desc[c * 64 + lane] = d;
+        cls[c] = work_class<1>(code, L, valid);
+    }
+
+    // ---- counting sort by class (LDS fetch-add, wave-local) -----------------
+    const uint32_t c00 = __builtin_amdgcn_readfirstlane(cls[0]);
+    bool uniform = true;
+#pragma unroll
+    for (int c = 0; c < C; ++c) uniform &= __all(cls[c] == c00);
+    uint32_t n0;  // sorted positions [0, n0) hold the non-string slots
+    if (!uniform) {
+        uint32_t* cnt = lds.cnt[w];
+        if (lane < kClasses) cnt[lane] = 0;
+#pragma unroll
+        for (int c = 0; c < C; ++c)
+            __hip_atomic_fetch_add(&cnt[cls[c]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        const uint32_t k = lane < kClasses ? cnt[lane] : 0u;
+        const uint32_t start = wave_scan_dpp(k) - k;
+        n0 = __builtin_amdgcn_readlane(start + k, 0);
+        if (lane < kClasses) cnt[lane] = start;
+#pragma unroll
+        for (int c = 0; c < C; ++c) {
+            const uint32_t pos = __hip_atomic_fetch_add(&cnt[cls[c]], 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_WAVEFRONT);
+            perm[pos] = (uint16_t)(c * 64 + lane);
+        }
+    } else {
+        n0 = c00 == 0 ? (uint32_t)(C * 64) : 0u;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // ---- phase 2a: the non-string slots, lean ---------------------------------
+    bool bad = false;
+    for (uint32_t k = lane; k < n0; k += 64) {
+        const uint32_t s = uniform ? k : perm[k];
+        const SlotDesc d = desc[s];
+        res[2 * s] = hash_numeric_slot(d.code_slot & 0xffu, d.p, d.n, bad);
+    }
+
+    // ---- phase 2b: string passes, next pass in flight -------------------------
+    const uint32_t npass = ((uint32_t)(C * 64) - n0 + 63) / 64;
+    struct Pass {
+        SlotDesc d;
+        Raw blk;
+    };
+    auto load_pass = [&](int t, Pass& P) {
+        const uint32_t k = n0 + (uint32_t)(t * 64 + lane);
+        if (k < (uint32_t)(C * 64)) {
+            P.d = desc[uniform ? k : perm[k]];
+        } else {  // past the wave's slots: hashes the zero pad, never stored
+            P.d.p = g_zero_pad;
+            P.d.n = 0;
+            P.d.code_slot = CODE_ZERO | (0xffffu << 8);
+        }
+        P.blk = issue_any<true>(P.d.code_slot & 0xffu, P.d.p, P.d.n);
+    };
+    Pass P0, P1;
+    if (npass > 0) load_pass(0, P0);
+#pragma unroll
+    for (int t = 0; t < C; ++t) {
+        if ((uint32_t)t >= npass) break;
+        Pass& cur = (t & 1) ? P1 : P0;
+        Pass& nxt = (t & 1) ? P0 : P1;
+        if ((uint32_t)t + 1 < npass) load_pass(t + 1, nxt);
+        const uint64_t h = hash_blk<false, false, true>(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n,
+                                                        consume_any<true>(cur.blk), bad);
+        const uint32_t s = cur.d.code_slot >> 8;
+        if (s != 0xffffu) res[2 * s] = h;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // ---- phase 3: coalesced stores in slot order ------------------------------
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+        const uint64_t q = qw + c * 64 + lane;
+        if (q < nslots) __builtin_nontemporal_store(res[2 * (c * 64 + lane)], args.coords + q);
+    }
+    if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
+}
+
+template <int C>
+static hipError_t launch_typed(const BatchArgs& args, hipStream_t stream) {
+    const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
+    const uint64_t blocks = (waves + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((hash_typed_kernel<C>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    return hipGetLastError();
+}
+
+// ===========================================================================
 // Workgroup-sorted kernel (variants 60-65): the class sort of the regroup
 // kernel over the whole workgroup's 4 * C * 64 slots instead of one wave's
 // C * 64.  A wave's share of the work and of the L2 working set is the same as
@@ -648,6 +815,10 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 38: return launch_regroup<2, true, true, true, true, false, true>(args, stream);
         case 39: return launch_regroup<8, true, true, true, false, false, true>(args, stream);
         case 45: return launch_regroup<2, true, true, true, true, false, true, 2>(args, stream);
+        case 70: return launch_typed<2>(args, stream);
+        case 71: return launch_typed<3>(args, stream);
+        case 72: return launch_typed<4>(args, stream);
+        case 73: return launch_typed<6>(args, stream);
         case 60: return launch_wgsort<2, 10, false>(args, stream);
         case 61: return launch_wgsort<2, 10, true>(args, stream);
         case 62: return launch_wgsort<2, 11, false>(args, stream);
@@ -723,6 +894,7 @@ static bool known_variant(int v) {
         case -1: case 12: case 18: case 19: case 20: case 21: case 25: case 26: case 30: case 31: case 35: case 37:
         case 38: case 39: case 44: case 45: case 46:
         case 60: case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
+        case 70: case 71: case 72: case 73:
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;

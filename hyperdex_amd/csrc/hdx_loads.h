@@ -365,6 +365,24 @@ __device__ __forceinline__ uint64_t hash_blk(uint32_t code, const uint8_t* p, ui
     return hash_numeric(code, bits);
 }
 
+// A numeric (or non-hashable) slot on its own: the dwords holding its first
+// and last byte (never outside the value's pages) and two v_alignbyte —
+// instead of a string slot's four 16-byte pieces.  Never called on strings.
+__device__ __forceinline__ uint64_t hash_numeric_slot(uint32_t code, const uint8_t* p, uint32_t n, bool& bad) {
+    if (code == CODE_ZERO) return 0;
+    uint64_t bits = 0;
+    if (n == 8) {
+        const uint8_t* a = dw_floor(p);
+        const uint32_t r = (uint32_t)(uintptr_t)p & 3;
+        const uint32_t d0 = gld4(a), d1 = gld4(a + 4), d2 = gld4(dw_floor(p + 7));
+        bits = pack64(__builtin_amdgcn_alignbyte(d1, d0, r), __builtin_amdgcn_alignbyte(d2, d1, r));
+    } else if (n != 0) {
+        bad = true;
+        return 0;
+    }
+    return hash_numeric(code, bits);
+}
+
 // Debug shapes (variants 40/41).  touch_blk: the loads a slot's
 // hash issues (its block plus every > 64-byte loop block), folded by XOR, no
 // hash arithmetic.  fake_block: a block made from the address, no loads.
