@@ -488,15 +488,9 @@ hash_typed_kernel(const BatchArgs args) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    // ---- phase 2a: the non-string slots, lean ---------------------------------
-    bool bad = false;
-    for (uint32_t k = lane; k < n0; k += 64) {
-        const uint32_t s = uniform ? k : perm[k];
-        const SlotDesc d = desc[s];
-        res[2 * s] = hash_numeric_slot(d.code_slot & 0xffu, d.p, d.n, bad);
-    }
-
-    // ---- phase 2b: string passes, next pass in flight -------------------------
+    // ---- phase 2: string passes (next pass in flight) and the non-string
+    // slots; the first string pass's bytes and every non-string value are
+    // requested before anything is consumed, so the wave waits on memory once
     const uint32_t npass = ((uint32_t)(C * 64) - n0 + 63) / 64;
     struct Pass {
         SlotDesc d;
@@ -515,6 +509,51 @@ hash_typed_kernel(const BatchArgs args) {
     };
     Pass P0, P1;
     if (npass > 0) load_pass(0, P0);
+
+    // non-string slots: descriptors and value dwords of every sub-pass first
+    bool bad = false;
+    uint32_t nslot[C], nd0[C], nd1[C], nd2[C], ncode[C], nlen[C], nsh[C];
+#pragma unroll
+    for (int u = 0; u < C; ++u) {
+        const uint32_t k = (uint32_t)(u * 64 + lane);
+        nslot[u] = 0xffffu;
+        nd0[u] = nd1[u] = nd2[u] = 0;
+        ncode[u] = CODE_ZERO;
+        nlen[u] = 0;
+        nsh[u] = 0;
+        if ((uint32_t)(u * 64) < n0 && k < n0) {
+            const uint32_t sl = uniform ? k : perm[k];
+            const SlotDesc d = desc[sl];
+            nslot[u] = sl;
+            ncode[u] = d.code_slot & 0xffu;
+            nlen[u] = d.n;
+            if (ncode[u] != CODE_ZERO && d.n == 8) {
+                const uint8_t* a = dw_floor(d.p);
+                nsh[u] = (uint32_t)(uintptr_t)d.p & 3;
+                nd0[u] = gld4(a);
+                nd1[u] = gld4(a + 4);
+                nd2[u] = gld4(dw_floor(d.p + 7));
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < C; ++u) {
+        if (nslot[u] == 0xffffu) continue;
+        uint64_t h = 0;
+        if (ncode[u] != CODE_ZERO) {
+            if (nlen[u] == 8) {
+                h = hash_numeric(ncode[u], pack64(__builtin_amdgcn_alignbyte(nd1[u], nd0[u], nsh[u]),
+                                                  __builtin_amdgcn_alignbyte(nd2[u], nd1[u], nsh[u])));
+            } else if (nlen[u] == 0) {
+                h = hash_numeric(ncode[u], 0);
+            } else {
+                bad = true;
+            }
+        }
+        res[2 * nslot[u]] = h;
+    }
+
+    // strings
 #pragma unroll
     for (int t = 0; t < C; ++t) {
         if ((uint32_t)t >= npass) break;
