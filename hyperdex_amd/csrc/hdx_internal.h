@@ -41,11 +41,14 @@ struct BatchArgs {
     uint8_t codes[HDX_MAX_ATTRS];
     // fused region lookup (hash_regroup_regions_kernel): T tables, K whole
     // objects per wave, lds_tables u64 words of LDS table copies per workgroup
-    uint32_t T, K, lds_tables, pad2_;
+    uint32_t T, K, lds_tables, win_bytes;  // win_bytes: the staged kernels' LDS window (hdx_staged.hip)
     SweepTable t[kMaxSweepTables];
 };
 
 hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream);
+// LDS-staged hashing of packed batches (hdx_staged.hip): K = slots / A objects
+// per wave, a win_bytes window (multiple of 1 KiB, <= 64 KiB); A <= 64.
+hipError_t launch_hash_staged(const BatchArgs& args, hipStream_t stream, uint32_t slots, uint32_t win_bytes);
 // hash + lookup_region in one launch (args.T tables in args.t, A <= 128)
 hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream);
 // Fills args.uniform_code from args.codes[0..A), and inv_A / a_magic from A.

@@ -1,0 +1,136 @@
+// hdx_lds_hash.h — hashing slots whose bytes are staged in LDS (device code).
+//
+// The staged kernels (hdx_staged.hip) copy a group of objects' bytes into a
+// wave-private LDS window with coalesced LDS DMA (global_load_lds_dwordx4:
+// 1 KiB per wave-instruction, 8 cache lines, instead of 64 lines for a
+// per-lane gather), then hash out of LDS.  Every LDS read here is a
+// dword-aligned ds_read_b32 / ds_read2_b32 through an address-space-3 pointer
+// (a misaligned wide LDS read is replayed; a generic pointer would become a
+// flat load that waits on every outstanding global load), and the bytes are
+// funnel-shifted into place with v_alignbyte exactly as the dword-aligned
+// global form (A4, hdx_loads.h) does, so the arithmetic is shared:
+// CityHash64 v1.1 (cityhash/city.cc:278-397), the ordered encodings and the
+// timestamp hash (hdx_device_hash.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hdx_device_hash.h"
+#include "hdx_loads.h"
+
+namespace hdx {
+
+typedef const __attribute__((address_space(3))) uint32_t* ldsw_t;  // LDS dwords
+typedef __attribute__((address_space(3))) uint32_t* ldsw_mut_t;
+
+__device__ __forceinline__ ldsw_t as_ldsw(const void* p) { return (ldsw_t)p; }
+
+// little-endian u32 at byte offset b of the window (any alignment)
+__device__ __forceinline__ uint32_t lds_u32(ldsw_t w, uint32_t b) {
+    const ldsw_t d = w + (b >> 2);
+    return __builtin_amdgcn_alignbyte(d[1], d[0], b & 3);
+}
+__device__ __forceinline__ uint32_t lds_be32(ldsw_t w, uint32_t b) { return __builtin_bswap32(lds_u32(w, b)); }
+
+// the 16 bytes at dword-aligned byte offset o
+__device__ __forceinline__ u64x2 lds16(ldsw_t w, int32_t o) {
+    const ldsw_t d = w + (o >> 2);
+    u64x2 v;
+    v.x = pack64(d[0], d[1]);
+    v.y = pack64(d[2], d[3]);
+    return v;
+}
+
+// A slot's A4 pieces (a4_offsets' layout, hdx_loads.h) out of the window;
+// a slot with nothing to read reads the window's first dwords.
+__device__ __forceinline__ Blk lds_block_a4(ldsw_t w, uint32_t code, uint32_t off, uint32_t n) {
+    const A4Offsets o = a4_offsets(code, off, n);
+    const int32_t base = o.any ? (int32_t)off : 0;
+    Raw r;
+    r.ra = o.ra;
+    r.rb = o.rb;
+    r.b.v0 = lds16(w, base + o.o0);
+    r.b.v1 = lds16(w, base + o.o1);
+    r.b.v2 = lds16(w, base + o.o2);
+    r.b.v3 = lds16(w, base + o.o3);
+    r.e1 = w[(base + o.e1) >> 2];
+    r.e3 = w[(base + o.e3) >> 2];
+    return funnel_raw(r);
+}
+
+// One 64-byte CityHash loop block at byte offset s: the 17 dwords from its
+// dword floor, funnel-shifted (every loop block ends before the value does).
+__device__ __forceinline__ Blk lds_block64(ldsw_t w, uint32_t s) {
+    const ldsw_t d = w + (s >> 2);
+    Blk64 b;
+    b.b.v0.x = pack64(d[0], d[1]);
+    b.b.v0.y = pack64(d[2], d[3]);
+    b.b.v1.x = pack64(d[4], d[5]);
+    b.b.v1.y = pack64(d[6], d[7]);
+    b.b.v2.x = pack64(d[8], d[9]);
+    b.b.v2.y = pack64(d[10], d[11]);
+    b.b.v3.x = pack64(d[12], d[13]);
+    b.b.v3.y = pack64(d[14], d[15]);
+    b.e = d[16];
+    return use64<true>(b, s & 3);
+}
+
+// city.cc:361-397 for n > 64: the tail block t in registers, the loop blocks
+// read from the window (city_gt64_reg's arithmetic).
+__device__ __forceinline__ uint64_t city_gt64_lds(ldsw_t w, uint32_t off, uint32_t n, const Blk& t) {
+    const u64x2 e0 = t.v0, e1 = t.v1, e2 = t.v2, e3 = t.v3;
+    uint64_t x = e1.y;
+    uint64_t y = e3.x + e0.y;
+    uint64_t z = mix16(e1.x + n, e2.y, KMUL);
+    uint64_t v0, v1, w0, w1;
+    weak32(e0.x, e0.y, e1.x, e1.y, n, z, v0, v1);
+    weak32(e2.x, e2.y, e3.x, e3.y, y + K1, x, w0, w1);
+    const uint32_t blocks = (n - 1) >> 6;
+    Blk b = lds_block64(w, off);
+    x = x * K1 + b.v0.x;
+    for (uint32_t k = 0;;) {
+        x = ror(x + y + v0 + b.v0.y, 37) * K1;
+        y = ror(y + v1 + b.v3.x, 42) * K1;
+        x ^= w1;
+        y += v0 + b.v2.y;
+        z = ror(z + w0, 33) * K1;
+        uint64_t nv0, nv1, nw0, nw1;
+        weak32(b.v0.x, b.v0.y, b.v1.x, b.v1.y, v1 * K1, x + w0, nv0, nv1);
+        weak32(b.v2.x, b.v2.y, b.v3.x, b.v3.y, z + w1, y + b.v1.x, nw0, nw1);
+        v0 = nv0; v1 = nv1; w0 = nw0; w1 = nw1;
+        const uint64_t tt = z; z = x; x = tt;
+        if (++k == blocks) break;
+        b = lds_block64(w, off + 64 * k);
+    }
+    return mix16(mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z, mix16(v1, w1, KMUL) + x, KMUL);
+}
+
+// hash(type, slice) of a string slot at byte offset off of the window
+// (hash_blk's regimes on the A4 piece layout).
+__device__ __forceinline__ uint64_t hash_string_lds(ldsw_t w, uint32_t off, uint32_t n) {
+    const Blk b = lds_block_a4(w, CODE_STRING, off, n);
+    if (n > 64) return city_gt64_lds(w, off, n, b);
+    if (n > 32) return city_33to64(b.v0, b.v1, b.v2, b.v3, n);
+    if (n > 16) return city_17to32(b.v1, b.v3, n);
+    return city_le16_reg(n == 16 ? b.v1 : window16(b.v1, b.v3, off & 15), n);
+}
+
+// A numeric (or non-hashable) slot at byte offset off of the window: the
+// dwords holding its first and last byte, two v_alignbyte.
+__device__ __forceinline__ uint64_t hash_numeric_lds(ldsw_t w, uint32_t code, uint32_t off, uint32_t n, bool& bad) {
+    if (code == CODE_ZERO) return 0;
+    uint64_t bits = 0;
+    if (n == 8) {
+        const ldsw_t d = w + (off >> 2);
+        const uint32_t r = off & 3;
+        const uint32_t d0 = d[0], d1 = d[1], d2 = w[(off + 7) >> 2];
+        bits = pack64(__builtin_amdgcn_alignbyte(d1, d0, r), __builtin_amdgcn_alignbyte(d2, d1, r));
+    } else if (n != 0) {
+        bad = true;
+        return 0;
+    }
+    return hash_numeric(code, bits);
+}
+
+}  // namespace hdx
