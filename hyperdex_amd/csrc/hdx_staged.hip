@@ -225,7 +225,8 @@ static hipError_t launch_staged_nch(BatchArgs args, hipStream_t stream) {
 hipError_t launch_hash_staged(const BatchArgs& a, hipStream_t stream, uint32_t slots, uint32_t win_bytes) {
     BatchArgs args = a;
     if (args.n == 0) return hipSuccess;
-    if (args.A > 64 || slots > kStagedSlotsMax || win_bytes % 1024 || win_bytes > 65536) return hipErrorInvalidValue;
+    if (slots > kStagedSlotsMax || win_bytes % 1024 || win_bytes > 65536) return hipErrorInvalidValue;
+    if (args.A > 64) return launch_hash_batch_variant(args, stream, 44);  // wider schemas: the regroup kernel
     args.K = slots / args.A;
     if (args.K == 0) args.K = 1;
     if (args.K > 64) args.K = 64;
