@@ -858,6 +858,9 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 81: return launch_hash_staged(args, stream, 128, 12288);
         case 82: return launch_hash_staged(args, stream, 256, 20480);
         case 83: return launch_hash_staged(args, stream, 128, 10240);
+        case 84: return launch_hash_staged(args, stream, 128, 9216);
+        case 85: return launch_hash_staged(args, stream, 96, 7168);
+        case 86: return launch_hash_staged(args, stream, 64, 5120);
         case 70: return launch_typed<2>(args, stream);
         case 71: return launch_typed<3>(args, stream);
         case 72: return launch_typed<4>(args, stream);
@@ -937,7 +940,7 @@ static bool known_variant(int v) {
         case -1: case 12: case 18: case 19: case 20: case 21: case 25: case 26: case 30: case 31: case 35: case 37:
         case 38: case 39: case 44: case 45: case 46:
         case 60: case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
-        case 70: case 71: case 72: case 73: case 80: case 81: case 82: case 83:
+        case 70: case 71: case 72: case 73: case 80: case 81: case 82: case 83: case 84: case 85: case 86:
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;

@@ -51,14 +51,18 @@ struct alignas(8) StDesc {
     uint32_t len;
 };
 
-// Per-wave LDS layout (dynamic shared memory, 16-byte aligned):
-//   window  [win_bytes + 64]   the group's bytes (+ slack for the A4 over-reads)
-//   desc    [256] StDesc       slot descriptors, then the parked coordinates
-//   obase   [64] u64           object bases (global form)
-//   perm    [256] u16, cnt [8] u32, codes [256] u8
-__host__ __device__ constexpr uint32_t staged_lds_bytes(uint32_t win) {
-    return win + 64 + kStagedSlotsMax * 8 + 64 * 8 + kStagedSlotsMax * 2 + kStagedClasses * 4 + 256;
-}
+// Per-wave LDS: the window (dynamic shared memory, win_bytes + 64 bytes of
+// slack for the A4 over-reads) and the metadata below (static: a separate
+// object, so the compiler sees that descriptor work does not touch the bytes
+// the LDS-DMA is still writing, and does not wait for the DMA before it).
+struct StagedMeta {
+    StDesc desc[kStagedSlotsMax];  // slot descriptors, then the parked coordinates
+    uint64_t obase[64];            // object bases (global form)
+    uint16_t perm[kStagedSlotsMax];
+    uint32_t cnt[kStagedClasses];
+    uint8_t codes[256];
+};
+__host__ __device__ constexpr uint32_t staged_lds_bytes(uint32_t win) { return win + 64; }
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
     return pack64(__builtin_amdgcn_readlane((uint32_t)v, l), __builtin_amdgcn_readlane((uint32_t)(v >> 32), l));
@@ -76,13 +80,14 @@ template <int NCH /* ceil(K*A/64), compile-time upper bound */>
 __global__ void __launch_bounds__(64)
 hash_staged_kernel(const BatchArgs args) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    __shared__ StagedMeta meta;
     const uint32_t WB = args.win_bytes;
     uint8_t* win = smem;
-    StDesc* desc = reinterpret_cast<StDesc*>(smem + WB + 64);
-    uint64_t* obase = reinterpret_cast<uint64_t*>(smem + WB + 64 + kStagedSlotsMax * 8);
-    uint16_t* perm = reinterpret_cast<uint16_t*>(smem + WB + 64 + kStagedSlotsMax * 8 + 64 * 8);
-    uint32_t* cnt = reinterpret_cast<uint32_t*>(smem + WB + 64 + kStagedSlotsMax * 8 + 64 * 8 + kStagedSlotsMax * 2);
-    uint8_t* codes = reinterpret_cast<uint8_t*>(cnt + kStagedClasses);
+    StDesc* desc = meta.desc;
+    uint64_t* obase = meta.obase;
+    uint16_t* perm = meta.perm;
+    uint32_t* cnt = meta.cnt;
+    uint8_t* codes = meta.codes;
     const ldsw_t w = as_ldsw(win);
 
     const int lane = threadIdx.x;
@@ -93,7 +98,27 @@ hash_staged_kernel(const BatchArgs args) {
     const uint32_t ns = nobj * A;  // slots of the group (<= 256)
     const uint64_t q0 = o0 * A;
 
-    // ---- 1. lengths, in-object offsets, object sizes --------------------------
+    // ---- 1. the group's byte range; its bytes -> LDS as early as possible -----
+    // With a next group and back-to-back objects the range is [obj_base[o0],
+    // obj_base[o0 + K]): the DMA goes out before the lengths are back (checked
+    // below; a group that turns out not to be contiguous is hashed from global
+    // memory instead).  The last group waits for its lengths.
+    const uint8_t* blob = args.blob;
+    const uint64_t b0 = args.obj_base[o0];
+    const bool has_next = o0 + K < args.n;
+    const uint64_t b_next = has_next ? args.obj_base[o0 + K] : 0;
+    const uint32_t lead = (uint32_t)((uintptr_t)(blob + b0) & 15);
+    const uint8_t* s16 = blob + b0 - lead;
+    bool early = has_next && b_next > b0 && ((lead + (b_next - b0) + 15) & ~15ull) <= WB;
+    uint32_t early_units = early ? (uint32_t)((lead + (b_next - b0) + 15) >> 4) : 0u;
+    for (uint32_t u0 = 0; u0 < early_units; u0 += 64) {
+        const uint32_t u = u0 + (uint32_t)lane;
+        if (u < early_units)
+            __builtin_amdgcn_global_load_lds((const void*)(s16 + 16ull * u),
+                                             (__attribute__((address_space(3))) void*)(win + 16 * u0), 16, 0, 0);
+    }
+
+    // ---- 2. lengths, in-object offsets, object sizes --------------------------
     uint32_t L[NCH], off[NCH], code[NCH];
     const uint32_t packed_codes = reinterpret_cast<const uint32_t*>(args.codes)[lane];
     reinterpret_cast<uint32_t*>(codes)[lane] = packed_codes;  // the code table, for per-lane lookups
@@ -125,20 +150,14 @@ hash_staged_kernel(const BatchArgs args) {
     const uint64_t mysize = (uint32_t)lane < nobj ? obase[lane] : 0;
     wave_lds_sync();
     if ((uint32_t)lane < nobj) obase[lane] = mybase;
-    // back to back in the blob, and the cover of 16-byte units fits the window
+    // back to back in the blob (and, with a next group, ending where it starts)
     const uint64_t nextb = pack64((uint32_t)__shfl_down((int)(uint32_t)mybase, 1, 64),
                                   (uint32_t)__shfl_down((int)(uint32_t)(mybase >> 32), 1, 64));
     const bool runs = __all((uint32_t)lane + 1 >= nobj || nextb == mybase + mysize);
-    const uint64_t b0 = readlane64(mybase, 0);
     const uint64_t bend = readlane64(mybase + mysize, (int)nobj - 1);
-    const uint8_t* src0 = args.blob + b0;
-    const uint32_t lead = (uint32_t)((uintptr_t)src0 & 15);
     const uint64_t cover = (lead + (bend - b0) + 15) & ~15ull;
-    const bool staged = runs && cover <= WB;
-
-    // ---- 2. the group's bytes -> LDS (one LDS-DMA round trip) -----------------
-    if (staged) {
-        const uint8_t* s16 = src0 - lead;
+    const bool staged = runs && cover <= WB && (!early || bend == b_next);
+    if (staged && !early) {  // the last group: its bytes now
         const uint32_t units = (uint32_t)(cover >> 4);
         for (uint32_t u0 = 0; u0 < units; u0 += 64) {
             const uint32_t u = u0 + (uint32_t)lane;
