@@ -383,6 +383,103 @@ hash_regroup_regions_kernel(const BatchArgs args) {
 }
 
 // ===========================================================================
+// Column kernel (variants 90-92): one lane per object, the attributes walked
+// in schema order.  For narrow schemas whose per-attribute work is the same on
+// every lane (config 2: a 64-byte key and four int64; config 1), the type
+// dispatch is wave-uniform (codes[j] is a kernel argument), no slot scan or
+// descriptor is needed, and a value's loads are only the ones its type needs:
+// a string's dword-aligned A4 pieces, a numeric's two dwords + one.  The
+// next attribute's loads are in flight while the current one is hashed; the
+// wave's 64 * A coordinates are parked in LDS and stored coalesced.
+// ===========================================================================
+template <int AMAX>
+__global__ void __launch_bounds__(256)
+hash_column_kernel(const BatchArgs args) {
+    __shared__ uint64_t park[4][64 * AMAX];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    const uint64_t i0 = ((uint64_t)blockIdx.x * 4 + w) * 64;
+    if (i0 >= args.n) return;
+    const uint32_t A = args.A;
+    const uint32_t nobj = (uint32_t)min<uint64_t>(64, args.n - i0);
+    const bool valid = (uint32_t)lane < nobj;
+    const uint64_t i = i0 + (valid ? lane : 0);
+    uint32_t L[AMAX], off[AMAX];
+    uint32_t run = 0;
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j) L[j] = (j < (int)A && valid) ? args.attr_len[i * A + j] : 0u;
+    const uint8_t* base = args.blob + args.obj_base[i];
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j) {
+        off[j] = run;
+        run += L[j];
+    }
+    struct Att {
+        Raw blk;
+        uint32_t d0, d1, d2;
+    };
+    auto issue = [&](int j, Att& a) {
+        const uint32_t code = args.codes[j];  // wave-uniform
+        const uint8_t* p = base + off[j];
+        if (code == CODE_STRING) {
+            a.blk = issue_any<true>(CODE_STRING, valid ? p : g_zero_pad, L[j]);
+        } else if (code != CODE_ZERO && L[j] == 8) {
+            const uint8_t* q = dw_floor(p);
+            a.d0 = gld4(q);
+            a.d1 = gld4(q + 4);
+            a.d2 = gld4(dw_floor(p + 7));
+        }
+    };
+    bool bad = false;
+    auto consume = [&](int j, Att& a) -> uint64_t {
+        const uint32_t code = args.codes[j];
+        const uint8_t* p = base + off[j];
+        if (code == CODE_STRING)
+            return hash_blk<false, false, true>(CODE_STRING, valid ? p : g_zero_pad, L[j], consume_any<true>(a.blk), bad);
+        if (code == CODE_ZERO) return 0;
+        if (L[j] == 8) {
+            const uint32_t r = (uint32_t)(uintptr_t)p & 3;
+            return hash_numeric(code, pack64(__builtin_amdgcn_alignbyte(a.d1, a.d0, r),
+                                             __builtin_amdgcn_alignbyte(a.d2, a.d1, r)));
+        }
+        if (L[j] != 0) {
+            bad = true;
+            return 0;
+        }
+        return hash_numeric(code, 0);
+    };
+    Att P0, P1;
+    issue(0, P0);
+#pragma unroll
+    for (int j = 0; j < AMAX; ++j) {
+        if (j >= (int)A) break;
+        Att& cur = (j & 1) ? P1 : P0;
+        Att& nxt = (j & 1) ? P0 : P1;
+        if (j + 1 < (int)A && j + 1 < AMAX) issue(j + 1, nxt);
+        const uint64_t h = consume(j, cur);
+        park[w][lane * A + j] = h;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t total = nobj * A;
+    for (uint32_t t = (uint32_t)lane; t < total; t += 64)
+        __builtin_nontemporal_store(park[w][t], args.coords + i0 * A + t);
+    if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
+}
+
+template <int AMAX>
+static hipError_t launch_column(const BatchArgs& args, hipStream_t stream) {
+    if (args.A > AMAX) return hipErrorInvalidValue;
+    const uint64_t waves = (args.n + 63) / 64;
+    const uint64_t blocks = (waves + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((hash_column_kernel<AMAX>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    return hipGetLastError();
+}
+
+// ===========================================================================
 // Typed regroup kernel (variants 70-73): the regroup kernel's wave-local class
 // sort (ORDER 1), with the non-string slots (int64 / float / timestamps /
 // non-hashable, class 0) taken out of the 64-lane passes: they are hashed in
@@ -854,6 +951,9 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 38: return launch_regroup<2, true, true, true, true, false, true>(args, stream);
         case 39: return launch_regroup<8, true, true, true, false, false, true>(args, stream);
         case 45: return launch_regroup<2, true, true, true, true, false, true, 2>(args, stream);
+        case 90: return args.A <= 2 ? launch_column<2>(args, stream) : args.A <= 5 ? launch_column<5>(args, stream)
+                                                             : args.A <= 8 ? launch_column<8>(args, stream)
+                                                                           : launch_hash_batch_variant(args, stream, 44);
         case 80: return launch_hash_staged(args, stream, 192, 16384);
         case 81: return launch_hash_staged(args, stream, 128, 12288);
         case 82: return launch_hash_staged(args, stream, 256, 20480);
@@ -940,7 +1040,7 @@ static bool known_variant(int v) {
         case -1: case 12: case 18: case 19: case 20: case 21: case 25: case 26: case 30: case 31: case 35: case 37:
         case 38: case 39: case 44: case 45: case 46:
         case 60: case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
-        case 70: case 71: case 72: case 73: case 80: case 81: case 82: case 83: case 84: case 85: case 86:
+        case 70: case 71: case 72: case 73: case 80: case 81: case 82: case 83: case 84: case 85: case 86: case 90:
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;

@@ -28,8 +28,13 @@
 #include "hdx_lds_hash.h"
 #include "hdx_loads.h"
 
+#ifndef HDX_DEBUG_BUILD
+#define HDX_DEBUG_BUILD 0
+#endif
+
 namespace hdx {
 
+#if HDX_DEBUG_BUILD  // an A/B experiment: not in the product library
 namespace {
 
 constexpr uint32_t kStagedSlotsMax = 256;  // K * A <= this (descriptor / perm arrays)
@@ -258,5 +263,6 @@ hipError_t launch_hash_staged(const BatchArgs& a, hipStream_t stream, uint32_t s
         default: return launch_staged_nch<4>(args, stream);
     }
 }
+#endif  // HDX_DEBUG_BUILD
 
 }  // namespace hdx
