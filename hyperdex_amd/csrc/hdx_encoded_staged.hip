@@ -1,0 +1,228 @@
+// hdx_encoded_staged.hip — the reindex sweep with each group of stored
+// objects staged in LDS (variants 95-98).
+//
+// Same contract as hash_encoded_kernel (hdx_encoded.hip): every value
+// [u64 BE version][u16 BE count]{[u32 BE len][bytes]}*count
+// (daemon/datalayer_encodings.cc:139-217) is decoded and its attributes and
+// key hashed (common/hash.cc:56-68) into coords, row-major; an undecodable
+// value gives zero coordinates, version 0 and HDX_E_BADENC.
+//
+// The gather sweep walks each value's length prefixes in global memory and
+// then re-reads the values to hash them: the walk touches every line, the
+// lines are evicted before the hash passes, so the values cross
+// HBM twice.  Here one wave owns G objects:
+//   1. per object its key and value chunks (16-byte units) are copied into a
+//      wave-private LDS window by LDS DMA, object by object (lane = chunk;
+//      per-lane sources, so any layout works) — the bytes cross HBM once;
+//   2. lane = object walks its value's prefixes in LDS (dword-aligned
+//      ds_read + v_alignbyte: no HBM round trip per prefix);
+//   3. passes of 64 slots in slot order hash out of LDS (hdx_lds_hash.h) and
+//      store their coordinates coalesced.
+// A group that does not fit the window is walked and hashed from global
+// memory in the same wave (identical results).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hdx_device_hash.h"
+#include "hdx_internal.h"
+#include "hdx_lds_hash.h"
+#include "hdx_loads.h"
+
+#ifndef HDX_DEBUG_BUILD
+#define HDX_DEBUG_BUILD 0
+#endif
+
+namespace hdx {
+
+namespace {
+
+typedef uint32_t __attribute__((aligned(1))) eu32_u;
+typedef uint64_t __attribute__((aligned(1))) eu64_u;
+typedef uint16_t __attribute__((aligned(1))) eu16_u;
+
+__device__ __forceinline__ uint32_t g_be32(const uint8_t* p) {
+    return __builtin_bswap32(*(const __attribute__((address_space(1))) eu32_u*)p);
+}
+__device__ __forceinline__ uint64_t g_be64(const uint8_t* p) {
+    return __builtin_bswap64(*(const __attribute__((address_space(1))) eu64_u*)p);
+}
+__device__ __forceinline__ uint32_t g_be16(const uint8_t* p) {
+    const uint16_t v = *(const __attribute__((address_space(1))) eu16_u*)p;
+    return (uint32_t)(uint16_t)((v >> 8) | (v << 8));
+}
+
+constexpr uint32_t kEZero = 0xffffffffu;
+constexpr uint32_t kEncStagedSlots = 1024;  // G * A <= this
+
+struct alignas(8) EDesc {
+    uint32_t off;  // staged: byte offset in the window; global: offset in the value (key: 0)
+    uint32_t len;
+};
+
+// Static LDS (a separate object from the window: descriptor work never waits
+// for the window's DMA).
+struct EncStagedMeta {
+    EDesc desc[kEncStagedSlots];
+    uint64_t voff[64], koff[64];
+    uint8_t codes[256];
+};
+
+}  // namespace
+
+template <int G>
+__global__ void __launch_bounds__(64)
+hash_encoded_staged_kernel(const EncodedArgs a, uint32_t WB) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t win[];
+    __shared__ EncStagedMeta meta;
+    const ldsw_t w = as_ldsw(win);
+    const int lane = threadIdx.x;
+    const uint32_t A = a.A;
+    const uint64_t o0 = (uint64_t)blockIdx.x * G;
+    if (o0 >= a.n) return;
+    const uint32_t nobj = (uint32_t)min<uint64_t>(G, a.n - o0);
+    const bool mine = (uint32_t)lane < nobj;
+    reinterpret_cast<uint32_t*>(meta.codes)[lane] = reinterpret_cast<const uint32_t*>(a.codes)[lane];
+
+    // ---- metadata, chunk counts, window placement ------------------------------
+    const uint64_t i = o0 + (mine ? lane : 0);
+    const uint64_t voff = mine ? a.val_off[i] : 0, koff = mine ? a.key_off[i] : 0;
+    const uint32_t vlen = mine ? a.val_len[i] : 0u, klen = mine ? a.key_len[i] : 0u;
+    const uint8_t* vsrc = a.vals + voff;
+    const uint8_t* ksrc = a.keys + koff;
+    const uint32_t vlead = (uint32_t)((uintptr_t)vsrc & 15), klead = (uint32_t)((uintptr_t)ksrc & 15);
+    // 16-byte units covering the key and the value (64-bit: a value may be huge)
+    const uint64_t kch = mine ? ((uint64_t)klead + klen + 15) >> 4 : 0;
+    const uint64_t vch = mine ? ((uint64_t)vlead + vlen + 15) >> 4 : 0;
+    const uint64_t nch = kch + vch;
+    const uint32_t nch32 = nch > 0xffffu ? 0xffffu : (uint32_t)nch;
+    const uint32_t cstart = wave_scan_dpp(nch32) - nch32;  // object's first unit in the window
+    const uint32_t total = __builtin_amdgcn_readlane(cstart + nch32, 63);
+    const bool staged = __all(!mine || nch <= 0xffffu) && (uint64_t)total * 16 <= WB;
+    if (mine) {
+        meta.voff[lane] = voff;
+        meta.koff[lane] = koff;
+    }
+
+    // ---- 1. keys + values -> LDS, object by object ------------------------------
+    if (staged) {
+        for (uint32_t o = 0; o < nobj; ++o) {
+            const uint32_t ko = __builtin_amdgcn_readlane((uint32_t)kch, (int)o);
+            const uint32_t no = __builtin_amdgcn_readlane(nch32, (int)o);
+            const uint32_t st = __builtin_amdgcn_readlane(cstart, (int)o);
+            const uint64_t ka = pack64(__builtin_amdgcn_readlane((uint32_t)(uintptr_t)(ksrc - klead), (int)o),
+                                       __builtin_amdgcn_readlane((uint32_t)((uintptr_t)(ksrc - klead) >> 32), (int)o));
+            const uint64_t va = pack64(__builtin_amdgcn_readlane((uint32_t)(uintptr_t)(vsrc - vlead), (int)o),
+                                       __builtin_amdgcn_readlane((uint32_t)((uintptr_t)(vsrc - vlead) >> 32), (int)o));
+            for (uint32_t c0 = 0; c0 < no; c0 += 64) {
+                const uint32_t c = c0 + (uint32_t)lane;
+                if (c < no) {
+                    const uint64_t src = c < ko ? ka + 16ull * c : va + 16ull * (c - ko);
+                    __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)src,
+                                                     (__attribute__((address_space(3))) void*)(win + 16 * (st + c0)),
+                                                     16, 0, 0);
+                }
+            }
+        }
+    }
+
+    // ---- 2. decode_value (datalayer_encodings.cc:168-217), lane = object --------
+    bool ok = mine && vlen >= 10;
+    uint64_t version = 0;
+    EDesc* desc = meta.desc;
+    if (staged) {
+        const uint32_t kb = cstart * 16 + klead;               // key byte 0 in the window
+        const uint32_t vb = (cstart + (uint32_t)kch) * 16 + vlead;  // value byte 0
+        if (ok) version = ((uint64_t)lds_be32(w, vb) << 32) | lds_be32(w, vb + 4);
+        ok = ok && (lds_be32(w, vb + 6) & 0xffffu) == A - 1;
+        if (mine) desc[lane * A] = EDesc{kb, klen};
+        uint32_t pos = 10;
+        for (uint32_t k = 0; k + 1 < A; ++k) {
+            uint32_t len = 0;
+            if (ok) {
+                if (vlen - pos < 4) {
+                    ok = false;
+                } else {
+                    len = lds_be32(w, vb + pos);
+                    pos += 4;
+                    if (len > vlen - pos) ok = false;  // the reference does not check this (:201-213)
+                }
+            }
+            if (mine) desc[lane * A + 1 + k] = EDesc{ok ? vb + pos : kEZero, ok ? len : 0u};
+            if (ok) pos += len;
+        }
+    } else {
+        if (ok) version = g_be64(vsrc);
+        ok = ok && g_be16(vsrc + 8) == A - 1;
+        if (mine) desc[lane * A] = EDesc{0u, klen};
+        uint32_t pos = 10;
+        for (uint32_t k = 0; k + 1 < A; ++k) {
+            uint32_t len = 0;
+            if (ok) {
+                if (vlen - pos < 4) {
+                    ok = false;
+                } else {
+                    len = g_be32(vsrc + pos);
+                    pos += 4;
+                    if (len > vlen - pos) ok = false;
+                }
+            }
+            if (mine) desc[lane * A + 1 + k] = EDesc{ok ? pos : kEZero, ok ? len : 0u};
+            if (ok) pos += len;
+        }
+    }
+    if (mine && !ok)  // undecodable: every coordinate of the object is 0
+        for (uint32_t j = 0; j < A; ++j) desc[lane * A + j] = EDesc{kEZero, 0u};
+    if (mine && a.versions) a.versions[i] = ok ? version : 0;
+    const bool any_bad = __any(mine && !ok);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // ---- 3. passes of 64 slots in slot order -----------------------------------
+    const uint32_t ns = nobj * A;
+    bool bad = false;
+    uint64_t* out = a.coords + o0 * A;
+    for (uint32_t s = (uint32_t)lane; s < ns; s += 64) {
+        const uint32_t o = div_small(s, a.a_magic), j = s - o * A;
+        const EDesc d = desc[s];
+        const uint32_t code = meta.codes[j];
+        uint64_t h = 0;
+        if (d.off != kEZero) {
+            if (staged) {
+                h = code == CODE_STRING ? hash_string_lds(w, d.off, d.len) : hash_numeric_lds(w, code, d.off, d.len, bad);
+            } else {
+                const uint8_t* p = (j == 0 ? a.keys + meta.koff[o] : a.vals + meta.voff[o]) + d.off;
+                h = code == CODE_STRING
+                        ? hash_blk<false, false, true>(CODE_STRING, p, d.len,
+                                                       consume_any<true>(issue_any<true>(CODE_STRING, p, d.len)), bad)
+                        : hash_numeric_slot(code, p, d.len, bad);
+            }
+        }
+        __builtin_nontemporal_store(h, out + s);
+    }
+    if (a.status && lane == 0 && any_bad) atomicOr(a.status, 1u << 6 /* HDX_E_BADENC */);
+    if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
+}
+
+template <int G>
+static hipError_t launch_enc_staged_g(const EncodedArgs& a, uint32_t WB, hipStream_t stream) {
+    if ((uint64_t)G * a.A > kEncStagedSlots) return hipErrorInvalidValue;
+    const uint64_t waves = (a.n + G - 1) / G;
+    if (waves > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((hash_encoded_staged_kernel<G>), dim3((uint32_t)waves), dim3(64), WB, stream, a, WB);
+    return hipGetLastError();
+}
+
+// G objects per wave (G * A <= 1024), an LDS window of WB bytes.
+hipError_t launch_hash_encoded_staged(const EncodedArgs& a, int G, uint32_t WB, hipStream_t stream) {
+    if (a.n == 0) return hipSuccess;
+    switch (G) {
+        case 4: return launch_enc_staged_g<4>(a, WB, stream);
+        case 8: return launch_enc_staged_g<8>(a, WB, stream);
+        case 12: return launch_enc_staged_g<12>(a, WB, stream);
+        case 16: return launch_enc_staged_g<16>(a, WB, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace hdx
