@@ -288,7 +288,7 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
         case 48: return launch_encoded<false, true, 0, 16>(a, stream);
         case 95: case 96: case 97: case 98: {  // LDS-staged (hdx_encoded_staged.hip)
             const int G = hash_variant() == 95 ? 8 : hash_variant() == 96 ? 16 : hash_variant() == 97 ? 12 : 4;
-            if ((uint64_t)G * a.A <= 1024)
+            if (a.A <= 64)
                 return launch_hash_encoded_staged(a, G, hash_variant() == 96 ? 24576 : hash_variant() == 97 ? 16384
                                                         : hash_variant() == 95 ? 12288 : 6144, stream);
             break;

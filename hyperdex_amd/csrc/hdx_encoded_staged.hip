@@ -52,7 +52,6 @@ __device__ __forceinline__ uint32_t g_be16(const uint8_t* p) {
 }
 
 constexpr uint32_t kEZero = 0xffffffffu;
-constexpr uint32_t kEncStagedSlots = 1024;  // G * A <= this
 
 struct alignas(8) EDesc {
     uint32_t off;  // staged: byte offset in the window; global: offset in the value (key: 0)
@@ -61,8 +60,9 @@ struct alignas(8) EDesc {
 
 // Static LDS (a separate object from the window: descriptor work never waits
 // for the window's DMA).
+template <int G>
 struct EncStagedMeta {
-    EDesc desc[kEncStagedSlots];
+    EDesc desc[G * 64];  // A <= 64
     uint64_t voff[64], koff[64];
     uint8_t codes[256];
 };
@@ -73,7 +73,7 @@ template <int G>
 __global__ void __launch_bounds__(64)
 hash_encoded_staged_kernel(const EncodedArgs a, uint32_t WB) {
     extern __shared__ __attribute__((aligned(16))) uint8_t win[];
-    __shared__ EncStagedMeta meta;
+    __shared__ EncStagedMeta<G> meta;
     const ldsw_t w = as_ldsw(win);
     const int lane = threadIdx.x;
     const uint32_t A = a.A;
@@ -123,6 +123,9 @@ hash_encoded_staged_kernel(const EncodedArgs a, uint32_t WB) {
                 }
             }
         }
+        // the window is read below: every LDS-DMA of this wave must have landed
+        // (the compiler does not order ds_read after global_load_lds by itself)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
 
     // ---- 2. decode_value (datalayer_encodings.cc:168-217), lane = object --------
@@ -206,14 +209,14 @@ hash_encoded_staged_kernel(const EncodedArgs a, uint32_t WB) {
 
 template <int G>
 static hipError_t launch_enc_staged_g(const EncodedArgs& a, uint32_t WB, hipStream_t stream) {
-    if ((uint64_t)G * a.A > kEncStagedSlots) return hipErrorInvalidValue;
+    if (a.A > 64) return hipErrorInvalidValue;
     const uint64_t waves = (a.n + G - 1) / G;
     if (waves > 0x7fffffffULL) return hipErrorInvalidValue;
     hipLaunchKernelGGL((hash_encoded_staged_kernel<G>), dim3((uint32_t)waves), dim3(64), WB, stream, a, WB);
     return hipGetLastError();
 }
 
-// G objects per wave (G * A <= 1024), an LDS window of WB bytes.
+// G objects per wave (A <= 64), an LDS window of WB bytes.
 hipError_t launch_hash_encoded_staged(const EncodedArgs& a, int G, uint32_t WB, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
     switch (G) {

@@ -132,7 +132,7 @@ struct EncodedArgs {
 
 hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream);
 // The sweep with each group of G objects staged in LDS (hdx_encoded_staged.hip):
-// G in {4, 8, 12, 16}, G * A <= 1024, an LDS window of WB bytes.
+// G in {4, 8, 12, 16}, A <= 64, an LDS window of WB bytes.
 hipError_t launch_hash_encoded_staged(const EncodedArgs& a, int G, uint32_t WB, hipStream_t stream);
 // HBM streaming probe (hdx_synth.hip): read `bytes` (write = 1: plus one
 // 8-byte store per 64 bytes read into sink[bytes / 64]).

@@ -171,6 +171,9 @@ hash_staged_kernel(const BatchArgs args) {
                                                  (__attribute__((address_space(3))) void*)(win + 16 * u0), 16, 0, 0);
         }
     }
+    // the window is read below: every LDS-DMA of this wave must have landed
+    // (the compiler does not order ds_read after global_load_lds by itself)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     // ---- 3. descriptors + counting sort by class ------------------------------
     uint32_t cls[NCH];
