@@ -286,13 +286,13 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
         case 58: return launch_encoded<false, true, 2>(a, stream);  // debug shape: phase 2 loads only (WRONG coords)
         case 47: return launch_encoded<false, true, 0, 64>(a, stream);
         case 48: return launch_encoded<false, true, 0, 16>(a, stream);
-        case 95: case 96: case 97: case 98: {  // LDS-staged (hdx_encoded_staged.hip)
-            const int G = hash_variant() == 95 ? 8 : hash_variant() == 96 ? 16 : hash_variant() == 97 ? 12 : 4;
-            if (a.A <= 64)
-                return launch_hash_encoded_staged(a, G, hash_variant() == 96 ? 24576 : hash_variant() == 97 ? 16384
-                                                        : hash_variant() == 95 ? 12288 : 6144, stream);
-            break;
-        }
+        // LDS-staged (hdx_encoded_staged.hip): 95 G=7 sorted 10 KiB, 96 G=11 sorted 14 KiB,
+        // 97 G=3 sorted 5 KiB, 98 G=4 unsorted 6 KiB, 99 G=15 sorted 20 KiB
+        case 95: if (a.A <= 32) return launch_hash_encoded_staged(a, 7, 10240, true, stream); break;
+        case 96: if (a.A <= 32) return launch_hash_encoded_staged(a, 11, 14336, true, stream); break;
+        case 97: if (a.A <= 32) return launch_hash_encoded_staged(a, 3, 5120, true, stream); break;
+        case 98: if (a.A <= 32) return launch_hash_encoded_staged(a, 4, 6144, false, stream); break;
+        case 99: if (a.A <= 32) return launch_hash_encoded_staged(a, 15, 20480, true, stream); break;
         default: break;
     }
 #endif

@@ -62,18 +62,21 @@ struct alignas(8) EDesc {
 // for the window's DMA).
 template <int G>
 struct EncStagedMeta {
-    EDesc desc[G * 64];  // A <= 64
-    uint64_t voff[64], koff[64];
+    EDesc desc[G * 32];      // A <= 32; then the parked coordinates (SORT)
+    uint16_t perm[G * 32];   // SORT: slots in class order
+    uint32_t cnt[8];
+    uint64_t voff[G], koff[G];
     uint8_t codes[256];
 };
 
 }  // namespace
 
-template <int G>
+template <int G, bool SORT>
 __global__ void __launch_bounds__(64)
 hash_encoded_staged_kernel(const EncodedArgs a, uint32_t WB) {
     extern __shared__ __attribute__((aligned(16))) uint8_t win[];
     __shared__ EncStagedMeta<G> meta;
+    static_assert(G <= 64, "G objects per wave");
     const ldsw_t w = as_ldsw(win);
     const int lane = threadIdx.x;
     const uint32_t A = a.A;
@@ -181,49 +184,106 @@ hash_encoded_staged_kernel(const EncodedArgs a, uint32_t WB) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
-    // ---- 3. passes of 64 slots in slot order -----------------------------------
+    // ---- 3. passes of 64 slots ---------------------------------------------------
+    // SORT: the non-string slots first (lean), then the strings by CityHash
+    // regime and loop count (the regroup kernel's ORDER 1 classes), every
+    // coordinate parked over its descriptor and stored in slot order; else
+    // slot order with direct coalesced stores.
     const uint32_t ns = nobj * A;
     bool bad = false;
     uint64_t* out = a.coords + o0 * A;
-    for (uint32_t s = (uint32_t)lane; s < ns; s += 64) {
+    auto hash_slot = [&](uint32_t s) -> uint64_t {
         const uint32_t o = div_small(s, a.a_magic), j = s - o * A;
         const EDesc d = desc[s];
         const uint32_t code = meta.codes[j];
-        uint64_t h = 0;
-        if (d.off != kEZero) {
-            if (staged) {
-                h = code == CODE_STRING ? hash_string_lds(w, d.off, d.len) : hash_numeric_lds(w, code, d.off, d.len, bad);
-            } else {
-                const uint8_t* p = (j == 0 ? a.keys + meta.koff[o] : a.vals + meta.voff[o]) + d.off;
-                h = code == CODE_STRING
-                        ? hash_blk<false, false, true>(CODE_STRING, p, d.len,
-                                                       consume_any<true>(issue_any<true>(CODE_STRING, p, d.len)), bad)
-                        : hash_numeric_slot(code, p, d.len, bad);
+        if (d.off == kEZero) return 0;
+        if (staged)
+            return code == CODE_STRING ? hash_string_lds(w, d.off, d.len) : hash_numeric_lds(w, code, d.off, d.len, bad);
+        const uint8_t* p = (j == 0 ? a.keys + meta.koff[o] : a.vals + meta.voff[o]) + d.off;
+        return code == CODE_STRING
+                   ? hash_blk<false, false, true>(CODE_STRING, p, d.len,
+                                                  consume_any<true>(issue_any<true>(CODE_STRING, p, d.len)), bad)
+                   : hash_numeric_slot(code, p, d.len, bad);
+    };
+    if constexpr (SORT) {
+        uint32_t* cnt = meta.cnt;
+        if (lane < 8) cnt[lane] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t cls[(G * 32 + 63) / 64];
+#pragma unroll
+        for (int c = 0; c < (G * 32 + 63) / 64; ++c) {
+            const uint32_t s = (uint32_t)(c * 64 + lane);
+            uint32_t k = 0;
+            if (s < ns) {
+                const uint32_t o = div_small(s, a.a_magic), j = s - o * A;
+                const EDesc d = desc[s];
+                const uint32_t n = d.len;
+                if (meta.codes[j] == CODE_STRING && d.off != kEZero)
+                    k = n > 64 ? (((n - 1) >> 6) >= 4 ? 7u : 3u + ((n - 1) >> 6)) : n > 32 ? 1u : n <= 16 ? 2u : 3u;
+                __hip_atomic_fetch_add(&cnt[k], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            }
+            cls[c] = k;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t kc = lane < 8 ? cnt[lane] : 0u;
+        const uint32_t start = wave_scan_dpp(kc) - kc;
+        if (lane < 8) cnt[lane] = start;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int c = 0; c < (G * 32 + 63) / 64; ++c) {
+            const uint32_t s = (uint32_t)(c * 64 + lane);
+            if (s < ns) {
+                const uint32_t pos = __hip_atomic_fetch_add(&cnt[cls[c]], 1u, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_WAVEFRONT);
+                meta.perm[pos] = (uint16_t)s;
             }
         }
-        __builtin_nontemporal_store(h, out + s);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint64_t* parked = reinterpret_cast<uint64_t*>(desc);
+        for (uint32_t t = (uint32_t)lane; t < ns; t += 64) {
+            const uint32_t s = meta.perm[t];
+            parked[s] = hash_slot(s);  // over its own, consumed, descriptor
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t s = (uint32_t)lane; s < ns; s += 64) __builtin_nontemporal_store(parked[s], out + s);
+    } else {
+        for (uint32_t s = (uint32_t)lane; s < ns; s += 64) __builtin_nontemporal_store(hash_slot(s), out + s);
     }
     if (a.status && lane == 0 && any_bad) atomicOr(a.status, 1u << 6 /* HDX_E_BADENC */);
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <int G>
+template <int G, bool SORT>
 static hipError_t launch_enc_staged_g(const EncodedArgs& a, uint32_t WB, hipStream_t stream) {
-    if (a.A > 64) return hipErrorInvalidValue;
+    if (a.A > 32) return hipErrorInvalidValue;
     const uint64_t waves = (a.n + G - 1) / G;
     if (waves > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_encoded_staged_kernel<G>), dim3((uint32_t)waves), dim3(64), WB, stream, a, WB);
+    hipLaunchKernelGGL((hash_encoded_staged_kernel<G, SORT>), dim3((uint32_t)waves), dim3(64), WB, stream, a, WB);
     return hipGetLastError();
 }
 
-// G objects per wave (A <= 64), an LDS window of WB bytes.
-hipError_t launch_hash_encoded_staged(const EncodedArgs& a, int G, uint32_t WB, hipStream_t stream) {
+// G objects per wave (A <= 32), an LDS window of WB bytes; SORT: class-sorted
+// passes with the coordinates parked in LDS.
+hipError_t launch_hash_encoded_staged(const EncodedArgs& a, int G, uint32_t WB, bool sort, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
-    switch (G) {
-        case 4: return launch_enc_staged_g<4>(a, WB, stream);
-        case 8: return launch_enc_staged_g<8>(a, WB, stream);
-        case 12: return launch_enc_staged_g<12>(a, WB, stream);
-        case 16: return launch_enc_staged_g<16>(a, WB, stream);
+    switch (G * 2 + (sort ? 1 : 0)) {
+        case 4 * 2: return launch_enc_staged_g<4, false>(a, WB, stream);
+        case 8 * 2: return launch_enc_staged_g<8, false>(a, WB, stream);
+        case 7 * 2: return launch_enc_staged_g<7, false>(a, WB, stream);
+        case 7 * 2 + 1: return launch_enc_staged_g<7, true>(a, WB, stream);
+        case 3 * 2 + 1: return launch_enc_staged_g<3, true>(a, WB, stream);
+        case 11 * 2 + 1: return launch_enc_staged_g<11, true>(a, WB, stream);
+        case 15 * 2 + 1: return launch_enc_staged_g<15, true>(a, WB, stream);
         default: return hipErrorInvalidValue;
     }
 }

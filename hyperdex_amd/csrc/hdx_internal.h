@@ -132,8 +132,8 @@ struct EncodedArgs {
 
 hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream);
 // The sweep with each group of G objects staged in LDS (hdx_encoded_staged.hip):
-// G in {4, 8, 12, 16}, A <= 64, an LDS window of WB bytes.
-hipError_t launch_hash_encoded_staged(const EncodedArgs& a, int G, uint32_t WB, hipStream_t stream);
+// G objects per wave, A <= 32, an LDS window of WB bytes, class-sorted passes.
+hipError_t launch_hash_encoded_staged(const EncodedArgs& a, int G, uint32_t WB, bool sort, hipStream_t stream);
 // HBM streaming probe (hdx_synth.hip): read `bytes` (write = 1: plus one
 // 8-byte store per 64 bytes read into sink[bytes / 64]).
 hipError_t launch_stream_probe(const uint8_t* src, uint64_t bytes, uint64_t* sink, int write, hipStream_t s);

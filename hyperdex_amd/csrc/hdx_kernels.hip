@@ -1041,7 +1041,7 @@ static bool known_variant(int v) {
         case 38: case 39: case 44: case 45: case 46:
         case 60: case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
         case 70: case 71: case 72: case 73: case 80: case 81: case 82: case 83: case 84: case 85: case 86: case 90:
-        case 95: case 96: case 97: case 98:
+        case 95: case 96: case 97: case 98: case 99:
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;
