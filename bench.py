@@ -614,18 +614,37 @@ def time_host_path(types, blob, base, lens, A, n_host=2_000_000):
             "mobjects_per_s": round(n / dt / 1e6, 2)}
 
 
+def cpu_threads():
+    """Every core this process may use: the affinity set, capped by the cgroup's
+    CPU quota (on the GPU box 256 logical CPUs are visible but cpu.max allows
+    16 cores; 256 threads under that quota measured 3x slower than 16)."""
+    quota = cgroup_cpu_quota()
+    threads = len(os.sched_getaffinity(0))
+    if quota:
+        threads = max(1, min(threads, int(quota)))
+    return threads, quota
+
+
+def host_info(threads, quota):
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "threads": threads, "cgroup_cpu_quota_cores": quota,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(types, blob, base, lens, A, seconds, coords):
     """The oracle (C restatement of common/hash.cc, -O2) on this host's cores,
     on a bounded sample of the same batch.  Also verifies the sample's GPU
     coordinates against it (a failed check aborts the bench)."""
     from oracle import oracle
-    # every core this process may use: the affinity set, capped by the cgroup's
-    # CPU quota (on the GPU box 256 logical CPUs are visible but cpu.max allows
-    # 16 cores; 256 threads under that quota measured 3x slower than 16)
-    quota = cgroup_cpu_quota()
-    threads = len(os.sched_getaffinity(0))
-    if quota:
-        threads = max(1, min(threads, int(quota)))
+    threads, quota = cpu_threads()
     ns = min(200_000, base.numel())
     nb = int((base[ns - 1] + lens.view(-1, A)[ns - 1].to(dtype=base.dtype).sum()).item())
     hb = blob[:nb].cpu().numpy()
@@ -647,22 +666,12 @@ def cpu_baseline(types, blob, base, lens, A, seconds, coords):
 
     multi_b, multi_o, reps = rate(threads, seconds)
     one_b, one_o, _ = rate(1, max(2.0, seconds / 5))
-    model = ""
-    try:
-        for line in open("/proc/cpuinfo"):
-            if line.startswith("model name"):
-                model = line.split(":", 1)[1].strip()
-                break
-    except OSError:
-        pass
     return {"value": round(multi_b / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
             "mobjects_per_s": round(multi_o / 1e6, 3),
             "single_thread_GiB_s": round(one_b / 2**30, 3),
             "sample": "%d objects (%.0f MB) of the same batch, %d passes, oracle/hdx_oracle.c -O2 "
                       "pthreads; verified equal to the GPU coords" % (ns, nb / 1e6, reps),
-            "cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": threads,
-            "cgroup_cpu_quota_cores": quota,
-            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+            **host_info(threads, quota)}
 
 
 def cgroup_cpu_quota():
@@ -675,11 +684,15 @@ def cgroup_cpu_quota():
 
 
 def cpu_baseline_encoded(types, enc, A, seconds, coords):
-    """Config 5 CPU baseline: the oracle's decode_value + hash (single thread;
-    the oracle has no threaded form of the sweep) on a 20 k-object sample."""
+    """Config 5 CPU baseline: the oracle's decode_value + hash on the same
+    cores as cpu_baseline (one oracle call per thread over its own chunk of a
+    20 k-objects-per-thread sample; ctypes drops the GIL for each call)."""
+    from concurrent.futures import ThreadPoolExecutor
+
     from oracle import oracle
+    threads, quota = cpu_threads()
     keys, key_off, key_len, vals, val_off, val_len = enc
-    ns = min(20_000, val_off.numel())
+    ns = min(20_000 * threads, val_off.numel())
     ko = key_off[:ns].cpu().numpy().view(np.uint64)
     kl = key_len[:ns].cpu().numpy().view(np.uint32)
     vo = val_off[:ns].cpu().numpy().view(np.uint64)
@@ -687,21 +700,31 @@ def cpu_baseline_encoded(types, enc, A, seconds, coords):
     kend = int((ko.astype(np.uint64) + kl).max())
     vend = int((vo.astype(np.uint64) + vl).max())
     hk, hv = keys[:kend].cpu().numpy(), vals[:vend].cpu().numpy()
-    want, _, bad = oracle.hash_encoded(types, hk, ko, kl, hv, vo, vl)
-    if bad.any() or not np.array_equal(coords[:ns].cpu().numpy().view(np.uint64), want):
-        raise SystemExit("cpu_baseline: GPU coordinates differ from the oracle")
-    nbytes = int(kl.sum()) + int(vl.sum())
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        oracle.hash_encoded(types, hk, ko, kl, hv, vo, vl)
-        reps += 1
-        dt = time.perf_counter() - t0
-        if dt >= seconds:
-            break
-    return {"value": round(reps * nbytes / dt / 2**30, 3), "unit": "GiB/s", "cores": 1,
+    cuts = np.linspace(0, ns, threads + 1).astype(np.int64)
+    chunks = [(ko[c0:c1], kl[c0:c1], vo[c0:c1], vl[c0:c1]) for c0, c1 in zip(cuts[:-1], cuts[1:]) if c1 > c0]
+
+    def one(ch):
+        return oracle.hash_encoded(types, hk, ch[0], ch[1], hv, ch[2], ch[3])
+
+    with ThreadPoolExecutor(len(chunks)) as pool:
+        parts = list(pool.map(one, chunks))
+        want = np.concatenate([p[0] for p in parts])
+        bad = np.concatenate([p[2] for p in parts])
+        if bad.any() or not np.array_equal(coords[:ns].cpu().numpy().view(np.uint64), want):
+            raise SystemExit("cpu_baseline: GPU coordinates differ from the oracle")
+        nbytes = int(kl.sum()) + int(vl.sum())
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            list(pool.map(one, chunks))
+            reps += 1
+            dt = time.perf_counter() - t0
+            if dt >= seconds:
+                break
+    return {"value": round(reps * nbytes / dt / 2**30, 3), "unit": "GiB/s", "cores": len(chunks),
             "kind": "port", "mobjects_per_s": round(reps * ns / dt / 1e6, 3),
-            "sample": "%d stored objects (%.0f MB), %d passes, oracle hdxo_hash_encoded -O2, 1 thread; "
-                      "verified equal to the GPU coords" % (ns, nbytes / 1e6, reps)}
+            "sample": "%d stored objects (%.0f MB), %d passes, oracle hdxo_hash_encoded -O2, %d threads; "
+                      "verified equal to the GPU coords" % (ns, nbytes / 1e6, reps, len(chunks)),
+            **host_info(len(chunks), quota)}
 
 
 if __name__ == "__main__":
