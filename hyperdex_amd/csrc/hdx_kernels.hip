@@ -160,7 +160,8 @@ struct RegroupLds {
 // looks its objects up in the args.T region tables (configuration::
 // lookup_region, hdx_region_lookup.h; tbl = the workgroup's LDS copies) and
 // stores coordinates only when args.coords is set.
-template <int C, bool NT_STORE, bool SORT, bool DIRECT, bool A4, bool PIPE, bool ASORT, int ORDER, bool REG>
+template <int C, bool NT_STORE, bool SORT, bool DIRECT, bool A4, bool PIPE, bool ASORT, int ORDER, bool REG,
+          bool UNI = false>
 __device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C>& lds, const uint64_t* tbl) {
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
@@ -313,12 +314,12 @@ __device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
     if constexpr (REG) {
-        // ---- phase 2b: lookup_region, one lane per (table, object) ----------
+        // ---- phase 2b: lookup_region, one lane per object --------------------
+        // UNI: the tables in a wave-uniform loop (a table's fields are scalar
+        // loads, its attrs uniform LDS offsets); else one lane per (table,
+        // object) pair, each lane reading its own table's fields.
         const uint32_t K = args.K, nobj = (uint32_t)(o_end - o_begin);
-        for (uint32_t k = lane; k < args.T * K; k += 64) {
-            const uint32_t t = k / K, o = k - t * K;
-            if (o >= nobj) continue;
-            const SweepTable& tb = args.t[t];
+        auto lookup_one = [&](const SweepTable& tb, uint32_t o) {
             const uint64_t* po = res + 2ull * o * A;
             const auto coord = [&](uint32_t d) { return po[2 * tb.attrs[d]]; };
             uint64_t id;
@@ -334,6 +335,15 @@ __device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C
                 id = lookup_scan(tb.lower, tb.upper, tb.ids, tb.R, tb.D, h);
             }
             tb.out[o_begin + o] = id;
+        };
+        if constexpr (UNI) {
+            for (uint32_t t = 0; t < args.T; ++t)
+                for (uint32_t o = lane; o < nobj; o += 64) lookup_one(args.t[t], o);
+        } else {
+            for (uint32_t k = lane; k < args.T * K; k += 64) {
+                const uint32_t t = k / K, o = k - t * K;
+                if (o < nobj) lookup_one(args.t[t], o);
+            }
         }
         if (!args.coords) {
             if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
@@ -365,7 +375,7 @@ hash_regroup_kernel(const BatchArgs args) {
 // hash + lookup_region in one launch (hdx_hash_batch_regions_device).  The
 // workgroup first copies the indexed tables that fit into LDS (its only
 // barrier, before any wave may leave).
-template <int C, bool SORT, bool A4, bool ASORT, int ORDER>
+template <int C, bool SORT, bool A4, bool ASORT, int ORDER, bool UNI>
 __global__ void __launch_bounds__(256)
 hash_regroup_regions_kernel(const BatchArgs args) {
     __shared__ RegroupLds<C> lds;
@@ -379,7 +389,7 @@ hash_regroup_regions_kernel(const BatchArgs args) {
         }
         __syncthreads();
     }
-    regroup_body<C, true, SORT, true, A4, false, ASORT, ORDER, true>(args, lds, tbl);
+    regroup_body<C, true, SORT, true, A4, false, ASORT, ORDER, true, UNI>(args, lds, tbl);
 }
 
 // ===========================================================================
@@ -983,12 +993,12 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
     }
 }
 
-template <int C, bool SORT, bool A4, bool ASORT, int ORDER>
-static hipError_t launch_regroup_regions(BatchArgs args, hipStream_t stream) {
+template <int C, bool SORT, bool A4, bool ASORT, int ORDER, bool UNI = false>
+static hipError_t launch_regroup_regions(BatchArgs args, hipStream_t stream, bool lds_ok = true) {
     // stage indexed tables in LDS while they fit in 16 KiB together and the
     // workgroup's LDS stays within 80 KiB (two workgroups per CU)
     uint32_t words = 0;
-    const bool room = sizeof(RegroupLds<C>) + 16384 <= 81920;
+    const bool room = lds_ok && sizeof(RegroupLds<C>) + 16384 <= 81920;
     for (uint32_t t = 0; t < args.T; ++t) {
         SweepTable& tb = args.t[t];
         tb.lds_index = tb.lds_ids = 0xffffffffu;
@@ -1006,7 +1016,7 @@ static hipError_t launch_regroup_regions(BatchArgs args, hipStream_t stream) {
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_regroup_regions_kernel<C, SORT, A4, ASORT, ORDER>), dim3((uint32_t)blocks), dim3(256),
+    hipLaunchKernelGGL((hash_regroup_regions_kernel<C, SORT, A4, ASORT, ORDER, UNI>), dim3((uint32_t)blocks), dim3(256),
                        (size_t)words * 8, stream, args);
     return hipGetLastError();
 }
@@ -1014,19 +1024,48 @@ static hipError_t launch_regroup_regions(BatchArgs args, hipStream_t stream) {
 static int auto_variant(const BatchArgs& args);
 
 // The fused form follows the automatic policy's kind of pass shape with whole
-// objects per wave: uniform strings 8 unsorted chunks (the tables then fit in
-// LDS beside the descriptors: 1.97 vs 2.66 ms with 16 chunks and the tables in
-// global memory, config 3a); numeric-heavy 4 unsorted; complex types 8 sorted;
-// mixed strings 3 sorted with A4 loads (3.84 ms vs 4.32 / 3.89 / 4.15 with
-// 2 / 4 / 8, config 3b; profiles/r1/fused_batch_regions.jsonl).
-// A <= 128 (checked by the caller).
+// objects per wave, the tables looked up in a wave-uniform loop (UNI; one lane
+// per (table, object) pair was 0.60 vs 0.47 ms on config 2): uniform strings 8
+// unsorted chunks (the tables then fit in LDS beside the descriptors: 1.97 vs
+// 2.66 ms with 16 chunks and the tables in global memory, config 3a), 2 below
+// 32 M slots (config 1: 0.158 vs 0.178 ms with 8); numeric-heavy 4 unsorted;
+// complex types 8 sorted; mixed strings 3 sorted with A4 loads (config 3b:
+// 3.83 vs 4.26 ms with 2; profiles/r1/fused_batch_regions.jsonl,
+// profiles/r2/ab_fused.jsonl).  A <= 128 (checked by the caller).
+#if HDX_DEBUG_BUILD
+int hash_variant();
+// Debug library only: the fused forms for interleaved A/B (variants 100-119).
+static hipError_t launch_fused_debug(const BatchArgs& args, hipStream_t stream, int v) {
+    switch (v) {
+        case 100: return launch_regroup_regions<4, false, false, false, 0, false>(args, stream);
+        case 101: return launch_regroup_regions<4, false, false, false, 0, true>(args, stream);
+        case 102: return launch_regroup_regions<2, false, false, false, 0, true>(args, stream);
+        case 103: return launch_regroup_regions<8, false, false, false, 0, true>(args, stream);
+        case 104: return launch_regroup_regions<4, false, false, false, 0, true>(args, stream, false);
+        case 105: return launch_regroup_regions<3, true, true, true, 1, false>(args, stream);
+        case 106: return launch_regroup_regions<3, true, true, true, 1, true>(args, stream);
+        case 107: return launch_regroup_regions<2, true, true, true, 1, true>(args, stream);
+        case 108: return launch_regroup_regions<8, false, false, false, 0, false>(args, stream);
+        case 109: return launch_regroup_regions<8, false, false, false, 0, true>(args, stream);
+        case 110: return launch_regroup_regions<1, false, false, false, 0, true>(args, stream);
+        case 111: return launch_regroup_regions<4, true, true, true, 1, true>(args, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+#endif
+
 hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream) {
     if (args.n == 0) return hipSuccess;
+#if HDX_DEBUG_BUILD
+    const int v = hash_variant();
+    if (v >= 100 && v < 120) return launch_fused_debug(args, stream, v);
+#endif
     switch (auto_variant(args)) {
-        case 25: case 20: case 12: return launch_regroup_regions<8, false, false, false, 0>(args, stream);
-        case 21: return launch_regroup_regions<4, false, false, false, 0>(args, stream);
-        case 46: return launch_regroup_regions<8, true, false, true, 1>(args, stream);
-        default: return launch_regroup_regions<3, true, true, true, 1>(args, stream);
+        case 25: case 20: return launch_regroup_regions<8, false, false, false, 0, true>(args, stream);
+        case 12: return launch_regroup_regions<2, false, false, false, 0, true>(args, stream);
+        case 21: return launch_regroup_regions<4, false, false, false, 0, true>(args, stream);
+        case 46: return launch_regroup_regions<8, true, false, true, 1, true>(args, stream);
+        default: return launch_regroup_regions<3, true, true, true, 1, true>(args, stream);
     }
 }
 
@@ -1042,6 +1081,8 @@ static bool known_variant(int v) {
         case 60: case 61: case 62: case 63: case 64: case 65: case 66: case 67: case 68: case 69:
         case 70: case 71: case 72: case 73: case 80: case 81: case 82: case 83: case 84: case 85: case 86: case 90:
         case 95: case 96: case 97: case 98: case 99:
+        case 100: case 101: case 102: case 103: case 104: case 105: case 106: case 107: case 108: case 109:
+        case 110: case 111:  // fused hash + lookup_region forms (launch_fused_debug)
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;

@@ -9,6 +9,9 @@
 namespace hdx {
 
 constexpr uint32_t kMaxLookupDims = 16;
+// u64 words of a dimension's 257 u16 bucket starts (region_index_build),
+// stored just below its boundaries
+constexpr uint32_t kIndexBucketWords = 65;
 
 // Region id of coordinates hd(0..D) through the interval index idx (hd reads
 // one coordinate, so a caller holding them in LDS need not copy them out).
@@ -20,13 +23,22 @@ __device__ __forceinline__ uint64_t lookup_indexed_fn(const uint64_t* idx, uint3
     for (uint32_t d = 0; d < kMaxLookupDims; ++d) {
         if (d >= D) break;
         const uint64_t hdr = idx[d];
-        const uint32_t m = (uint32_t)(hdr & 0xffff);
         const uint64_t* B = idx + ((hdr >> 16) & 0xffffff);
-        // number of boundaries <= h[d]: fixed-step binary search (same steps on every lane)
+        // number of boundaries <= h[d]: the top byte's bucket bounds it to
+        // [start[b], start[b + 1]], then a binary search over that range
         const uint64_t hv = hd(d);
-        uint32_t pos = 0;
-        for (uint32_t step = m ? 1u << (31 - __builtin_clz(m)) : 0u; step; step >>= 1)
-            if (pos + step <= m && B[pos + step - 1] <= hv) pos += step;
+        const uint16_t* start = reinterpret_cast<const uint16_t*>(B - kIndexBucketWords);
+        const uint32_t b = (uint32_t)(hv >> 56);
+        uint32_t pos = start[b], cnt = start[b + 1] - pos;
+        while (cnt) {
+            const uint32_t half = cnt >> 1;
+            if (B[pos + half] <= hv) {
+                pos += half + 1;
+                cnt -= half + 1;
+            } else {
+                cnt = half;
+            }
+        }
         const uint64_t* mask = idx + (hdr >> 40) + (size_t)pos * W;
 #pragma unroll
         for (uint32_t w = 0; w < 4; ++w)

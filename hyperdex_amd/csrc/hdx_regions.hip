@@ -13,6 +13,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstring>
 
 #include "hdx_internal.h"
 #include "hdx_region_lookup.h"
@@ -29,7 +30,11 @@ namespace hdx {
 // reference's first-match scan (configuration.cc:698-735), overlapping or
 // empty boxes included, at D binary searches instead of up to R*D compares.
 // Layout, u64 words: D headers (m | boundaries offset << 16 | masks offset
-// << 40), then per dimension its m sorted boundaries and (m + 1) * W mask words.
+// << 40), then per dimension: kIndexBucketWords words of u16 bucket starts
+// (start[b] = boundaries <= b << 56, b = 0..256, so a coordinate whose top
+// byte is b has its interval in [start[b], start[b + 1]]: the search is over
+// that range only — zero or one step for the reference's equal partitions),
+// its m sorted boundaries, and (m + 1) * W mask words.
 // ---------------------------------------------------------------------------
 void region_index_build(uint32_t D, uint32_t R, const uint64_t* lower, const uint64_t* upper,
                         std::vector<uint64_t>& index, uint32_t& W) {
@@ -47,7 +52,15 @@ void region_index_build(uint32_t D, uint32_t R, const uint64_t* lower, const uin
         }
         std::sort(pts.begin(), pts.end());
         pts.erase(std::unique(pts.begin(), pts.end()), pts.end());
-        const uint64_t m = pts.size(), boff = index.size();
+        const uint64_t m = pts.size();
+        uint16_t start[kIndexBucketWords * 4] = {};
+        for (uint32_t b = 0; b <= 256; ++b)
+            start[b] = (uint16_t)(b == 256 ? m
+                                           : std::upper_bound(pts.begin(), pts.end(), (uint64_t)b << 56) - pts.begin());
+        const size_t soff = index.size();
+        index.resize(soff + kIndexBucketWords);
+        std::memcpy(&index[soff], start, sizeof start);
+        const uint64_t boff = index.size();
         index.insert(index.end(), pts.begin(), pts.end());
         const uint64_t moff = index.size();
         for (uint64_t i = 0; i <= m; ++i) {
