@@ -40,19 +40,32 @@ def main():
     dev = torch.device("cuda", 0)
     forms = [int(v) for v in args.forms.split(",")]
     for cfg in args.configs.split(","):
-        types, blob, base, lens = synth.make_batch_device(cfg, args.objects, device=dev)
+        if cfg == "cfg5":  # the stored-object sweep: forms 47 (64 objects per wave)
+            types, *enc = synth.make_encoded_device("cfg3b", args.objects, device=dev)
+            blob = base = lens = None
+
+            def hash_into(coords):
+                hdx.hash_encoded(types, *enc, coords=coords)
+
+            def fused():
+                return hdx.hash_encoded_regions(types, *enc, tables)
+        else:
+            types, blob, base, lens = synth.make_batch_device(cfg, args.objects, device=dev)
+
+            def hash_into(coords):
+                hdx.hash_batch(types, blob, base, lens, coords=coords)
+
+            def fused():
+                return hdx.hash_batch_regions(types, blob, base, lens, tables)
         A = len(types)
         tables = bench.key_subspace_tables(A)
         coords = torch.empty((args.objects, A), dtype=torch.int64, device=dev)
         outs = [torch.empty(args.objects, dtype=torch.int64, device=dev) for _ in tables]
 
         def separate():
-            hdx.hash_batch(types, blob, base, lens, coords=coords)
+            hash_into(coords)
             for t, o in zip(tables, outs):
                 hdx.lookup_region(t, coords, out=o)
-
-        def fused():
-            return hdx.hash_batch_regions(types, blob, base, lens, tables)
 
         times = {v: [] for v in [-2, -1] + forms}
         for rep in range(args.reps + 1):
@@ -79,6 +92,8 @@ def main():
         for t in tables:
             t.close()
         del blob, base, lens, coords, outs
+        if cfg == "cfg5":
+            del enc
         torch.cuda.empty_cache()
 
 
