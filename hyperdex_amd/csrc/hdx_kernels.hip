@@ -17,6 +17,8 @@
 // windows with and without pipelining) are no longer built; their results are
 // in DESIGN.md §4 and the logs.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 #include <stdlib.h>
 
@@ -162,14 +164,15 @@ struct RegroupLds {
 // stores coordinates only when args.coords is set.
 template <int C, bool NT_STORE, bool SORT, bool DIRECT, bool A4, bool PIPE, bool ASORT, int ORDER, bool REG,
           bool UNI = false>
-__device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C>& lds, const uint64_t* tbl) {
+__device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C>& lds, const uint64_t* tbl,
+                                             uint64_t wave = ~0ull) {
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     SlotDesc* desc = lds.desc[w];
     uint16_t* perm = lds.perm[w];
     uint64_t* res = reinterpret_cast<uint64_t*>(desc);  // res[2*s] = first 8 bytes of desc[s]
 
-    const uint64_t wave = (uint64_t)blockIdx.x * 4 + w;
+    if (wave == ~0ull) wave = (uint64_t)blockIdx.x * 4 + w;
     const uint32_t A = args.A;
     uint64_t qw, nslots, o_begin = 0, o_end = 0;  // nslots: end of this wave's slots
     if constexpr (REG) {
@@ -371,6 +374,37 @@ hash_regroup_kernel(const BatchArgs args) {
     __shared__ RegroupLds<C> lds;
     regroup_body<C, NT_STORE, SORT, DIRECT, A4, PIPE, ASORT, ORDER, false>(args, lds, nullptr);
 }
+
+#if HDX_DEBUG_BUILD
+// Debug: the same kernel held to WPE waves per SIMD (amdgpu_waves_per_eu caps
+// the VGPRs at 512 / WPE), for occupancy A/B (variants 140-147).
+template <int WPE, int C, bool NT_STORE, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false,
+          bool ASORT = false, int ORDER = 0>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, 8)))
+hash_regroup_wpe_kernel(const BatchArgs args) {
+    __shared__ RegroupLds<C> lds;
+    regroup_body<C, NT_STORE, SORT, DIRECT, A4, PIPE, ASORT, ORDER, false>(args, lds, nullptr);
+}
+#endif
+
+#if HDX_DEBUG_BUILD
+// Debug: a fixed grid whose waves stride over the C * 64-slot windows
+// (variants 150-152), against the one-window-per-wave launch.
+template <int C, bool NT_STORE, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false,
+          bool ASORT = false, int ORDER = 0>
+__global__ void __launch_bounds__(256)
+hash_regroup_stride_kernel(const BatchArgs args) {
+    __shared__ RegroupLds<C> lds;
+    const uint64_t windows = (args.n * args.A + C * 64 - 1) / (C * 64);
+    const uint64_t stride = (uint64_t)gridDim.x * 4;
+    for (uint64_t wv = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); wv < windows; wv += stride) {
+        regroup_body<C, NT_STORE, SORT, DIRECT, A4, PIPE, ASORT, ORDER, false>(args, lds, nullptr, wv);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+#endif
 
 // hash + lookup_region in one launch (hdx_hash_batch_regions_device).  The
 // workgroup first copies the indexed tables that fit into LDS (its only
@@ -930,6 +964,33 @@ static hipError_t launch_regroup(const BatchArgs& args, hipStream_t stream) {
     return hipGetLastError();
 }
 
+#if HDX_DEBUG_BUILD
+template <int WPE, int C, bool NT, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false,
+          bool ASORT = false, int ORDER = 0>
+static hipError_t launch_regroup_wpe(const BatchArgs& args, hipStream_t stream) {
+    const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
+    const uint64_t blocks = (waves + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((hash_regroup_wpe_kernel<WPE, C, NT, SORT, DIRECT, A4, PIPE, ASORT, ORDER>),
+                       dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    return hipGetLastError();
+}
+#endif
+
+#if HDX_DEBUG_BUILD
+template <int C, bool NT, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false,
+          bool ASORT = false, int ORDER = 0>
+static hipError_t launch_regroup_stride(const BatchArgs& args, hipStream_t stream, uint32_t wg_per_cu) {
+    const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
+    const uint64_t blocks = std::min<uint64_t>((waves + 3) / 4, 256ull * wg_per_cu);
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL((hash_regroup_stride_kernel<C, NT, SORT, DIRECT, A4, PIPE, ASORT, ORDER>),
+                       dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    return hipGetLastError();
+}
+#endif
+
 template <bool NT, bool PIPE = false, int SHAPE = 0, bool A4 = false>
 static hipError_t launch_chunk(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + 63) / 64;
@@ -985,6 +1046,20 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 67: return launch_wgsort<2, 10, true, true, true>(args, stream);
         case 68: return launch_wgsort<1, 10, true, true>(args, stream);
         case 69: return launch_wgsort<4, 10, true, true>(args, stream);
+        // occupancy A/B: 44 at 6 / 7 / 8 waves per SIMD, 21 at 8, 25 at 4 / 5, 46 at 5 / 6
+        case 140: return launch_regroup_wpe<6, 2, true, true, true, true, false, true, 1>(args, stream);
+        case 141: return launch_regroup_wpe<7, 2, true, true, true, true, false, true, 1>(args, stream);
+        case 142: return launch_regroup_wpe<8, 2, true, true, true, true, false, true, 1>(args, stream);
+        case 143: return launch_regroup_wpe<8, 4, true, false>(args, stream);
+        case 144: return launch_regroup_wpe<4, 16, true, false, false>(args, stream);
+        case 145: return launch_regroup_wpe<5, 16, true, false, false>(args, stream);
+        case 146: return launch_regroup_wpe<5, 8, true, true, true, false, false, true, 1>(args, stream);
+        case 147: return launch_regroup_wpe<6, 8, true, true, true, false, false, true, 1>(args, stream);
+        // fixed grids striding over the windows: 21 and 44 at 4 / 8 workgroups per CU
+        case 150: return launch_regroup_stride<4, true, false>(args, stream, 4);
+        case 151: return launch_regroup_stride<4, true, false>(args, stream, 8);
+        case 152: return launch_regroup_stride<2, true, true, true, true, false, true, 1>(args, stream, 4);
+        case 153: return launch_regroup_stride<2, true, true, true, true, false, true, 1>(args, stream, 8);
         // debug shapes: WRONG coordinates, debug library only
         case 40: return launch_chunk<true, false, 1>(args, stream);  // loads only
         case 41: return launch_chunk<true, false, 2>(args, stream);  // arithmetic only
@@ -1083,6 +1158,8 @@ static bool known_variant(int v) {
         case 95: case 96: case 97: case 98: case 99:
         case 100: case 101: case 102: case 103: case 104: case 105: case 106: case 107: case 108: case 109:
         case 110: case 111:  // fused hash + lookup_region forms (launch_fused_debug)
+        case 140: case 141: case 142: case 143: case 144: case 145: case 146: case 147:
+        case 150: case 151: case 152: case 153:
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;
