@@ -121,7 +121,8 @@ def main():
 
     # measured ceiling of this access shape beside the spec peak (uses coords
     # as its store target, so it runs before the hash fills them)
-    sp = stream_probe(blob, coords, stream) if cfg != "cfg5" and not args.no_stream_probe else None
+    sp = (stream_probe(blob, coords, stream, mix=write_mix(payload, n, A))
+          if cfg != "cfg5" and not args.no_stream_probe else None)
     for _ in range(args.warmup):
         launch()
     torch.cuda.synchronize()
@@ -186,7 +187,8 @@ def main():
 
     if sp is not None:
         result["roofline"]["stream_probe"] = sp
-        result["roofline"]["frac_of_probe"] = round(achieved / sp["read_write_1to8_GBps"], 4)
+        result["roofline"]["frac_of_probe"] = round(
+            achieved / sp.get("read_write_mix_GBps", sp["read_write_1to8_GBps"]), 4)
     if cfg == "cfg5":
         result["roofline"]["kernel"] = "void hdx::hash_encoded_kernel<false, true, 0, 32>(hdx::EncodedArgs)"
     if world > 1 and not args.no_allgather:
@@ -437,19 +439,26 @@ def time_regions(coords, world, dev, backend, max_over_ranks, stream, gather, re
     return res
 
 
-def stream_probe(blob, sink, stream, reps=10):
+def stream_probe(blob, sink, stream, mix=1, reps=10):
     """Practical HBM ceiling measured in the same run: a plain
     streaming read of the batch's bytes in the hash kernels' access shape
-    (hdxdbg_stream_probe), alone and with one 8-byte store per 64 bytes read
-    (the hash's 1:8 write mix on 64-byte attributes)."""
+    (hdxdbg_stream_probe), alone, with one 8-byte store per 64 bytes read (the
+    1:8 write mix of 64-byte attributes) and, when the config's own mix
+    differs, with `mix` stores per 64 bytes (config 2: 3, ≈ its 40 B written
+    per 116 B read)."""
     import torch
 
     import hyperdex_amd as hdx
     lib = hdx.lib()
-    nbytes = (blob.numel() // 4096) * 4096
-    nbytes = min(nbytes, sink.numel() * 64 // 4096 * 4096)  # one sink word per 64 bytes read
-    res = {"bytes": nbytes}
-    for key, write in (("read_GBps", 0), ("read_write_1to8_GBps", 1)):
+    res = {}
+    for key, write in (("read_GBps", 0), ("read_write_1to8_GBps", 1),
+                       ("read_write_mix_GBps", mix if mix != 1 else None)):
+        if write is None:
+            continue
+        nbytes = (blob.numel() // 4096) * 4096
+        nbytes = min(nbytes, sink.numel() * 64 // max(write, 1) // 4096 * 4096)
+        res.setdefault("bytes", nbytes)
+
         def go():
             rc = lib.hdxdbg_stream_probe(blob.data_ptr(), nbytes, sink.data_ptr(), write, stream.cuda_stream)
             assert rc == 0, rc
@@ -463,7 +472,15 @@ def stream_probe(blob, sink, stream, reps=10):
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / reps
         res[key] = round(nbytes * (1 + write / 8) / (ms / 1e3) / 1e9, 1)
+    if mix != 1:
+        res["mix_stores_per_64B"] = mix
     return res
+
+
+def write_mix(payload, n, A):
+    """8-byte coordinate stores per 64 bytes read for a packed batch (1..4)."""
+    reads = payload + 4 * n * A
+    return max(1, min(4, round(64 * (8 * n * A) / reads / 8))) if reads else 1
 
 
 def time_config(cfg, n, dev, stream, steps=10, warmup=2):

@@ -738,7 +738,7 @@ HDX_EXPORT int hdxdbg_kernel_variant(void) { return hash_variant(); }
 #endif
 
 HDX_EXPORT int hdxdbg_stream_probe(const void* src, uint64_t bytes, uint64_t* sink, int write, void* stream) {
-    if (!src || (write && !sink) || bytes % 4096) return HDX_E_INVALID;
+    if (!src || (write && !sink) || write < 0 || write > 4 || bytes % 4096) return HDX_E_INVALID;
     HIP_TRY(launch_stream_probe((const uint8_t*)src, bytes, sink, write, (hipStream_t)stream));
     return HDX_OK;
 }

@@ -163,7 +163,7 @@ struct RegroupLds {
 // lookup_region, hdx_region_lookup.h; tbl = the workgroup's LDS copies) and
 // stores coordinates only when args.coords is set.
 template <int C, bool NT_STORE, bool SORT, bool DIRECT, bool A4, bool PIPE, bool ASORT, int ORDER, bool REG,
-          bool UNI = false>
+          bool UNI = false, bool REGD = false>
 __device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C>& lds, const uint64_t* tbl,
                                              uint64_t wave = ~0ull) {
     const int lane = threadIdx.x & 63;
@@ -204,6 +204,10 @@ __device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C
     if (args.uniform_code == 0xffu) packed_codes = reinterpret_cast<const uint32_t*>(args.codes)[lane];
 
     // ---- phase 1: descriptors + classes -------------------------------------
+    // REGD (unsorted waves only): each lane keeps its C descriptors in
+    // registers — pass t's slot t * 64 + lane is the lane's own chunk-t slot
+    static_assert(!REGD || (!SORT && !REG), "register descriptors need slot-order passes");
+    SlotDesc dreg[REGD ? C : 1];
     uint32_t cls[C];
 #pragma unroll
     for (int c = 0; c < C; ++c) {
@@ -227,7 +231,8 @@ __device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C
         d.p = args.blob + base + off;
         d.n = L;
         d.code_slot = code | ((uint32_t)(c * 64 + lane) << 8);
-        desc[c * 64 + lane] = d;
+        if constexpr (REGD) dreg[c] = d;
+        else desc[c * 64 + lane] = d;
         cls[c] = work_class<ORDER>(code, L, valid);
     }
 
@@ -285,7 +290,8 @@ __device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C
     };
     auto load_pass = [&](int t, Pass& P) {
         const uint32_t s = uniform ? (uint32_t)(t * 64 + lane) : perm[t * 64 + lane];
-        P.d = desc[s];
+        if constexpr (REGD) P.d = dreg[t];
+        else P.d = desc[s];
         P.blk = issue_any<A4>(P.d.code_slot & 0xffu, P.d.p, P.d.n);
     };
     bool bad = false;
@@ -388,6 +394,14 @@ hash_regroup_wpe_kernel(const BatchArgs args) {
 #endif
 
 #if HDX_DEBUG_BUILD
+// Debug: unsorted waves with the descriptors in registers (variants 154/155).
+template <int C, bool NT_STORE>
+__global__ void __launch_bounds__(256)
+hash_regroup_regd_kernel(const BatchArgs args) {
+    __shared__ RegroupLds<C> lds;
+    regroup_body<C, NT_STORE, false, true, false, false, false, 0, false, false, true>(args, lds, nullptr);
+}
+
 // Debug: a fixed grid whose waves stride over the C * 64-slot windows
 // (variants 150-152), against the one-window-per-wave launch.
 template <int C, bool NT_STORE, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false,
@@ -979,6 +993,16 @@ static hipError_t launch_regroup_wpe(const BatchArgs& args, hipStream_t stream) 
 #endif
 
 #if HDX_DEBUG_BUILD
+template <int C>
+static hipError_t launch_regd(const BatchArgs& args, hipStream_t stream) {
+    const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
+    const uint64_t blocks = (waves + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((hash_regroup_regd_kernel<C, true>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    return hipGetLastError();
+}
+
 template <int C, bool NT, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false,
           bool ASORT = false, int ORDER = 0>
 static hipError_t launch_regroup_stride(const BatchArgs& args, hipStream_t stream, uint32_t wg_per_cu) {
@@ -1055,6 +1079,8 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 145: return launch_regroup_wpe<5, 16, true, false, false>(args, stream);
         case 146: return launch_regroup_wpe<5, 8, true, true, true, false, false, true, 1>(args, stream);
         case 147: return launch_regroup_wpe<6, 8, true, true, true, false, false, true, 1>(args, stream);
+        case 154: return launch_regd<4>(args, stream);
+        case 155: return launch_regd<8>(args, stream);
         // fixed grids striding over the windows: 21 and 44 at 4 / 8 workgroups per CU
         case 150: return launch_regroup_stride<4, true, false>(args, stream, 4);
         case 151: return launch_regroup_stride<4, true, false>(args, stream, 8);
@@ -1159,7 +1185,7 @@ static bool known_variant(int v) {
         case 100: case 101: case 102: case 103: case 104: case 105: case 106: case 107: case 108: case 109:
         case 110: case 111:  // fused hash + lookup_region forms (launch_fused_debug)
         case 140: case 141: case 142: case 143: case 144: case 145: case 146: case 147:
-        case 150: case 151: case 152: case 153:
+        case 150: case 151: case 152: case 153: case 154: case 155:
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;

@@ -170,10 +170,10 @@ hipError_t launch_synth_fill(const SynthArgs& a, const uint64_t* obj_base, const
 // Streaming probe (hdxdbg_stream_probe): the HBM rate of a plain read of
 // `bytes` in the hash kernels' access shape (one wave per 4 KiB chunk, each
 // lane 4 x 16 B of a 64-byte span — tools/membw.hip's fastest read shape),
-// optionally with one 8-byte non-temporal store per 64 bytes read (the 1:8
-// write mix of the 64-byte-attribute configs), so the bench can quote the
-// kernel against a measured ceiling beside the HBM3E spec.  bytes is a
-// multiple of 4096.
+// optionally with `write` (1..4) 8-byte non-temporal stores per 64 bytes read
+// (1: the 1:8 write mix of the 64-byte-attribute configs; 3: config 2's
+// ≈ 1:3), so the bench can quote the kernel against a measured ceiling of its
+// own read/write mix beside the HBM3E spec.  bytes is a multiple of 4096.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) stream_probe_kernel(const uint8_t* src, uint64_t chunks, uint64_t* sink,
                                                          int write) {
@@ -183,8 +183,10 @@ __global__ void __launch_bounds__(256) stream_probe_kernel(const uint8_t* src, u
     typedef uint64_t u64x2v __attribute__((ext_vector_type(2)));
     const u64x2v* p = reinterpret_cast<const u64x2v*>(src + c * 4096 + lane * 64);
     const u64x2v v = p[0] ^ p[1] ^ p[2] ^ p[3];
-    if (write) __builtin_nontemporal_store(v.x ^ v.y, sink + c * 64 + lane);
-    else if (sink && (v.x ^ v.y) == 0x9e3779b97f4a7c15ull) sink[0] = v.x;  // keeps the loads live
+    if (write) {
+        for (int k = 0; k < write; ++k)  // lane-contiguous: each pass one coalesced 512-byte row
+            __builtin_nontemporal_store(v.x ^ v.y ^ (uint64_t)k, sink + (c * write + k) * 64 + lane);
+    } else if (sink && (v.x ^ v.y) == 0x9e3779b97f4a7c15ull) sink[0] = v.x;  // keeps the loads live
 }
 
 hipError_t launch_stream_probe(const uint8_t* src, uint64_t bytes, uint64_t* sink, int write, hipStream_t s) {
