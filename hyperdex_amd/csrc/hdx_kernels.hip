@@ -163,7 +163,7 @@ struct RegroupLds {
 // lookup_region, hdx_region_lookup.h; tbl = the workgroup's LDS copies) and
 // stores coordinates only when args.coords is set.
 template <int C, bool NT_STORE, bool SORT, bool DIRECT, bool A4, bool PIPE, bool ASORT, int ORDER, bool REG,
-          bool UNI = false, bool REGD = false>
+          bool UNI = false, bool REGD = false, bool QUAD = false>
 __device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C>& lds, const uint64_t* tbl,
                                              uint64_t wave = ~0ull) {
     const int lane = threadIdx.x & 63;
@@ -302,8 +302,13 @@ __device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C
         Pass& cur = (t & 1) ? P1 : P0;
         Pass& nxt = (t & 1) ? P0 : P1;
         if (t + 1 < C) load_pass(t + 1, nxt);
-        const uint64_t h = hash_blk<PIPE, false, A4>(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n,
-                                                     consume_any<A4>(cur.blk), bad);
+        uint64_t h;
+        if constexpr (QUAD) {
+            static_assert(A4, "the quad-cooperative loop follows the A4 piece layout");
+            h = hash_blk_quad(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n, consume_any<A4>(cur.blk), bad);
+        } else {
+            h = hash_blk<PIPE, false, A4>(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n, consume_any<A4>(cur.blk), bad);
+        }
         if (DIRECT && uniform && !REG) {  // pass t is chunk t in slot order: store straight to HBM
             const uint64_t q = qw + t * 64 + lane;
             if (q < nslots) {
@@ -394,6 +399,15 @@ hash_regroup_wpe_kernel(const BatchArgs args) {
 #endif
 
 #if HDX_DEBUG_BUILD
+// Debug: the sorted A4 kernel with the > 64-byte loop's loads quad-cooperative
+// (variants 160/161: 2 / 4 chunks).
+template <int C>
+__global__ void __launch_bounds__(256)
+hash_regroup_quad_kernel(const BatchArgs args) {
+    __shared__ RegroupLds<C> lds;
+    regroup_body<C, true, true, true, true, false, true, 1, false, false, false, true>(args, lds, nullptr);
+}
+
 // Debug: unsorted waves with the descriptors in registers (variants 154/155).
 template <int C, bool NT_STORE>
 __global__ void __launch_bounds__(256)
@@ -994,6 +1008,16 @@ static hipError_t launch_regroup_wpe(const BatchArgs& args, hipStream_t stream) 
 
 #if HDX_DEBUG_BUILD
 template <int C>
+static hipError_t launch_quad(const BatchArgs& args, hipStream_t stream) {
+    const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
+    const uint64_t blocks = (waves + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((hash_regroup_quad_kernel<C>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    return hipGetLastError();
+}
+
+template <int C>
 static hipError_t launch_regd(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
     const uint64_t blocks = (waves + 3) / 4;
@@ -1079,6 +1103,8 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 145: return launch_regroup_wpe<5, 16, true, false, false>(args, stream);
         case 146: return launch_regroup_wpe<5, 8, true, true, true, false, false, true, 1>(args, stream);
         case 147: return launch_regroup_wpe<6, 8, true, true, true, false, false, true, 1>(args, stream);
+        case 160: return launch_quad<2>(args, stream);
+        case 161: return launch_quad<4>(args, stream);
         case 154: return launch_regd<4>(args, stream);
         case 155: return launch_regd<8>(args, stream);
         // fixed grids striding over the windows: 21 and 44 at 4 / 8 workgroups per CU
@@ -1185,7 +1211,7 @@ static bool known_variant(int v) {
         case 100: case 101: case 102: case 103: case 104: case 105: case 106: case 107: case 108: case 109:
         case 110: case 111:  // fused hash + lookup_region forms (launch_fused_debug)
         case 140: case 141: case 142: case 143: case 144: case 145: case 146: case 147:
-        case 150: case 151: case 152: case 153: case 154: case 155:
+        case 150: case 151: case 152: case 153: case 154: case 155: case 160: case 161:
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;

@@ -41,7 +41,9 @@ __device__ __forceinline__ uint64_t hash_numeric(uint32_t code, uint64_t bits) {
 //                    buffer are read safely — then a funnel shift (v_alignbyte)
 //                    recovers the value's bytes in registers.
 // ===========================================================================
-static __device__ __attribute__((aligned(64))) uint8_t g_zero_pad[64];  // per code object
+// 128 bytes: a quad-cooperative loop load (ld64_quad) of a lane with no block
+// reads 64 bytes + one dword here
+static __device__ __attribute__((aligned(64))) uint8_t g_zero_pad[128];  // per code object
 
 // 16-byte load through an explicit global (addrspace 1) pointer at any
 // alignment: keeps the access a global_load_dwordx4 (never flat_, whose
@@ -340,6 +342,99 @@ __device__ __forceinline__ uint64_t city_gt64_reg(const uint8_t* s, uint32_t n, 
     return mix16(mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z, mix16(v1, w1, KMUL) + x, KMUL);
 }
 
+// ---------------------------------------------------------------------------
+// Quad-cooperative loop loads.  The address unit's cost follows the distinct
+// 128-byte lines a wave-instruction touches (tools/tabench.hip: 6.9 ns per
+// instruction per CU for 1 KiB contiguous, 49 ns for 64 lanes in 64 lines,
+// L2-resident), and a lane-per-value 64-byte block costs four 16-byte loads
+// that each touch a line per lane.  Here the four lanes of a quad load each
+// other's blocks: in round j every lane of the quad reads its 16-byte piece
+// (lane & 3) of lane j's block, so one instruction touches 16 blocks (16-32
+// lines) instead of 64; a 4 x 4 transpose over the quad (two butterfly
+// stages of DPP quad_perm + v_cndmask) then gives each lane its own block.
+// ---------------------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ uint32_t qperm(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xf, 0xf, false);
+}
+template <int J>
+__device__ __forceinline__ const uint8_t* qbcast_ptr(const uint8_t* a) {
+    const uint64_t v = (uint64_t)(uintptr_t)a;
+    return (const uint8_t*)(uintptr_t)pack64(qperm<J * 0x55>((uint32_t)v), qperm<J * 0x55>((uint32_t)(v >> 32)));
+}
+// One butterfly stage over dword t of the element pair (m, mm = m ^ D):
+// the lane with bit D clear takes its partner's X[m] as its X[mm], the lane
+// with bit D set takes its partner's X[mm] as its X[m].
+template <int CTRL>
+__device__ __forceinline__ void qswap(uint32_t& xm, uint32_t& xmm, bool hi) {
+    const uint32_t recv = qperm<CTRL>(hi ? xm : xmm);
+    xm = hi ? recv : xm;
+    xmm = hi ? xmm : recv;
+}
+__device__ __forceinline__ void qswap16(u64x2& a, u64x2& b, bool hi, bool d1) {
+    uint32_t a0 = (uint32_t)a.x, a1 = (uint32_t)(a.x >> 32), a2 = (uint32_t)a.y, a3 = (uint32_t)(a.y >> 32);
+    uint32_t b0 = (uint32_t)b.x, b1 = (uint32_t)(b.x >> 32), b2 = (uint32_t)b.y, b3 = (uint32_t)(b.y >> 32);
+    if (d1) {  // partner lane ^ 1: quad_perm [1, 0, 3, 2]
+        qswap<0xB1>(a0, b0, hi); qswap<0xB1>(a1, b1, hi); qswap<0xB1>(a2, b2, hi); qswap<0xB1>(a3, b3, hi);
+    } else {   // partner lane ^ 2: quad_perm [2, 3, 0, 1]
+        qswap<0x4E>(a0, b0, hi); qswap<0x4E>(a1, b1, hi); qswap<0x4E>(a2, b2, hi); qswap<0x4E>(a3, b3, hi);
+    }
+    a.x = pack64(a0, a1); a.y = pack64(a2, a3);
+    b.x = pack64(b0, b1); b.y = pack64(b2, b3);
+}
+// The 64 bytes at dword-aligned a (and the dword after them) of every lane;
+// the whole wave must be active (quad partners read each other's addresses).
+__device__ __forceinline__ Blk64 ld64_quad(const uint8_t* a) {
+    const uint32_t i = threadIdx.x & 3;
+    Blk64 r;
+    r.b.v0 = gld16(qbcast_ptr<0>(a) + 16 * i);
+    r.b.v1 = gld16(qbcast_ptr<1>(a) + 16 * i);
+    r.b.v2 = gld16(qbcast_ptr<2>(a) + 16 * i);
+    r.b.v3 = gld16(qbcast_ptr<3>(a) + 16 * i);
+    r.e = gld4(a + 64);
+    // lane i now holds piece i of the quad's blocks 0..3: transpose
+    const bool b1 = (i & 2) != 0, b0 = (i & 1) != 0;
+    qswap16(r.b.v0, r.b.v2, b1, false);
+    qswap16(r.b.v1, r.b.v3, b1, false);
+    qswap16(r.b.v0, r.b.v1, b0, true);
+    qswap16(r.b.v2, r.b.v3, b0, true);
+    return r;
+}
+
+// city_gt64_reg with the loop's block loads quad-cooperative: called by the
+// whole wave (every lane takes part in the loads); g64 lanes get the hash.
+__device__ __forceinline__ uint64_t city_gt64_quad(const uint8_t* s, uint32_t n, const Blk& t, bool g64) {
+    const u64x2 e0 = t.v0, e1 = t.v1, e2 = t.v2, e3 = t.v3;
+    uint64_t x = e1.y;
+    uint64_t y = e3.x + e0.y;
+    uint64_t z = mix16(e1.x + n, e2.y, KMUL);
+    uint64_t v0, v1, w0, w1;
+    weak32(e0.x, e0.y, e1.x, e1.y, n, z, v0, v1);
+    weak32(e2.x, e2.y, e3.x, e3.y, y + K1, x, w0, w1);
+    const uint32_t blocks = g64 ? (n - 1) >> 6 : 0u;
+    const uint32_t sh = g64 ? (uint32_t)(uintptr_t)s & 3 : 0u;
+    for (uint32_t k = 0; __builtin_amdgcn_ballot_w64(k < blocks) != 0; ++k) {
+        const bool act = k < blocks;
+        const Blk64 raw = ld64_quad(act ? dw_floor(s + 64 * k) : g_zero_pad);
+        if (act) {
+            const Blk cur = use64<true>(raw, sh);
+            const u64x2 b0 = cur.v0, b1 = cur.v1, b2 = cur.v2, b3 = cur.v3;
+            if (k == 0) x = x * K1 + b0.x;
+            x = ror(x + y + v0 + b0.y, 37) * K1;
+            y = ror(y + v1 + b3.x, 42) * K1;
+            x ^= w1;
+            y += v0 + b2.y;
+            z = ror(z + w0, 33) * K1;
+            uint64_t nv0, nv1, nw0, nw1;
+            weak32(b0.x, b0.y, b1.x, b1.y, v1 * K1, x + w0, nv0, nv1);
+            weak32(b2.x, b2.y, b3.x, b3.y, z + w1, y + b1.x, nw0, nw1);
+            v0 = nv0; v1 = nv1; w0 = nw0; w1 = nw1;
+            const uint64_t tt = z; z = x; x = tt;
+        }
+    }
+    return mix16(mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z, mix16(v1, w1, KMUL) + x, KMUL);
+}
+
 // A4: the block comes from issue_block_a4 (16..32-byte, short and numeric
 // pieces in slots 1 and 3).
 template <bool PIPE = false, bool FAKE = false, bool A4 = false>
@@ -358,6 +453,31 @@ __device__ __forceinline__ uint64_t hash_blk(uint32_t code, const uint8_t* p, ui
     uint64_t bits = 0;
     if (n == 8) {
         bits = window8(f, g, sh);
+    } else if (n != 0) {
+        bad = true;
+        return 0;
+    }
+    return hash_numeric(code, bits);
+}
+
+// hash_blk (A4) with the > 64-byte loop quad-cooperative: called by the whole
+// wave; the loop runs, wave-uniformly, while any lane has a block left.
+__device__ __forceinline__ uint64_t hash_blk_quad(uint32_t code, const uint8_t* p, uint32_t n, const Blk& b,
+                                                  bool& bad) {
+    const bool g64 = code == CODE_STRING && n > 64;
+    uint64_t hg = 0;
+    if (__builtin_amdgcn_ballot_w64(g64) != 0) hg = city_gt64_quad(p, n, b, g64);
+    const uint32_t sh = (uint32_t)(uintptr_t)p & 15;
+    if (code == CODE_STRING) {
+        if (n > 64) return hg;
+        if (n > 32) return city_33to64(b.v0, b.v1, b.v2, b.v3, n);
+        if (n > 16) return city_17to32(b.v1, b.v3, n);
+        return city_le16_reg(n == 16 ? b.v1 : window16(b.v1, b.v3, sh), n);
+    }
+    if (code == CODE_ZERO) return 0;
+    uint64_t bits = 0;
+    if (n == 8) {
+        bits = window8(b.v1, b.v3, sh);
     } else if (n != 0) {
         bad = true;
         return 0;

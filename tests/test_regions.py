@@ -125,6 +125,38 @@ def test_gpu_lookup_index_vs_scan(oracle, R, scan, monkeypatch):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("R", [40, 256])
+def test_gpu_lookup_clustered_boundaries(oracle, R):
+    """The index's top-byte buckets (hdx_regions.hip region_index_build): box
+    edges crowded into two top-byte values (up to 2R boundaries in one bucket:
+    a multi-step search inside it), edges exactly on bucket starts (b << 56)
+    and one below, coordinates on and beside every edge."""
+    import torch
+
+    from hyperdex_amd import regions
+    rng = np.random.default_rng(R)
+    A, attrs = 4, [3, 1]
+    base = np.array([0x12 << 56, 0xfe << 56], np.uint64)
+    a = base[rng.integers(0, 2, size=(R, 2))] + rng.integers(0, 1 << 56, size=(R, 2), dtype=np.uint64)
+    b = base[rng.integers(0, 2, size=(R, 2))] + rng.integers(0, 1 << 56, size=(R, 2), dtype=np.uint64)
+    lo, up = np.minimum(a, b), np.maximum(a, b)
+    lo[0, 0], up[0, 0] = np.uint64(0x40 << 56), np.uint64((0x41 << 56) - 1)
+    lo[1, 1], up[1, 1] = np.uint64(0x41 << 56), U64MAX
+    ids = rng.integers(1, 2**63, R, dtype=np.uint64)
+    edges = np.concatenate([lo.ravel(), up.ravel(), up.ravel() + np.uint64(1), lo.ravel() - np.uint64(1)])
+    coords = rng.integers(0, 2**64, size=(40000, A), dtype=np.uint64)
+    for a_ in attrs:
+        coords[:30000, a_] = edges[rng.integers(0, len(edges), 30000)]
+    want = oracle.lookup_region(attrs, lo, up, ids, coords)
+    t = regions.RegionTable(attrs, lo, up, ids)
+    got = regions.lookup_region(t, torch.from_numpy(coords.view(np.int64)).to(torch.device("cuda", 0)))
+    torch.cuda.synchronize()
+    t.close()
+    assert (want != 0).sum() > 1000
+    assert np.array_equal(got.cpu().numpy().view(np.uint64), want)
+
+
+@pytest.mark.gpu
 def test_gpu_hash_then_point_leader(oracle):
     """hash -> lookup on subspace 0 (point_leader's region step) end to end."""
     import torch
@@ -182,6 +214,37 @@ def test_gpu_batch_regions_fused(oracle, cfg, n, with_coords):
         assert np.array_equal(coords.cpu().numpy().view(np.uint64), want_coords)
     for t in tables:
         t.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("form", list(range(100, 112)))
+def test_gpu_batch_regions_every_fused_form(oracle, form):
+    """The debug library's fused forms (hdx_kernels.hip launch_fused_debug:
+    chunks per wave, sorted or not, tables in LDS or global memory, the
+    per-lane or wave-uniform table loop) all give the oracle's region ids."""
+    import torch
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import RegionTable, _lib, synth
+    dev = torch.device("cuda", 0)
+    with _lib.debug_library(form):
+        for cfg, n in [("cfg2", 1537), ("cfg3b", 777), ("mixed", 300), ("cfg1", 129)]:
+            types, blob, base, lens = synth.make_batch_host(cfg, n, seed=form + n)
+            want_coords, _ = oracle.hash_batch(types, blob, base, lens)
+            A = len(types)
+            specs = [([0],) + tuple(oracle.partition(1, 64))]
+            if A >= 4:
+                specs.append(([1, 2, 3],) + tuple(oracle.partition(3, 64)))
+            tables = [RegionTable(at, lo, up, np.arange(1, len(lo) + 1, dtype=np.uint64)) for at, lo, up in specs]
+            ids = hdx.hash_batch_regions(types, torch.from_numpy(np.ascontiguousarray(blob)).to(dev),
+                                         torch.from_numpy(base.view(np.int64)).to(dev),
+                                         torch.from_numpy(lens.view(np.int32)).to(dev), tables)
+            torch.cuda.synchronize()
+            for k, (at, lo, up) in enumerate(specs):
+                want = oracle.lookup_region(at, lo, up, np.arange(1, len(lo) + 1, dtype=np.uint64), want_coords)
+                assert np.array_equal(ids[k].cpu().numpy().view(np.uint64), want), (cfg, k)
+            for t in tables:
+                t.close()
 
 
 @pytest.mark.gpu
