@@ -69,9 +69,10 @@ static bool sweep_region_lds() {
     return true;
 #endif
 }
-// Wave-private LDS: G object bases {value, key}, the code table, descriptors.
+// Wave-private LDS: G object bases {value, key}, the code table, the pass
+// attribute list (numeric walk), descriptors.
 __host__ __device__ constexpr size_t encoded_lds_per_wave(uint32_t A, uint32_t G = 64) {
-    return G * 16 + 256 + (size_t)G * A * sizeof(EncDesc);
+    return G * 16 + 512 + (size_t)G * A * sizeof(EncDesc);
 }
 
 // G objects per wave (lanes G..63 idle in phase 1).  SHAPE (debug variants
@@ -80,7 +81,12 @@ __host__ __device__ constexpr size_t encoded_lds_per_wave(uint32_t A, uint32_t G
 // objects' coordinates (G*A slots), so it also looks every object up in the
 // T region tables (hdx_region_lookup.h) — phase 2 parks each coordinate over
 // its consumed descriptor, phase 3 has one lane per object.
-template <bool TOUCH, bool A4 = false, int SHAPE = 0, int G = 64, bool REGIONS = false>
+// NW (numeric walk): the walk hashes every non-string value attribute as it
+// reads its prefix — the prefix and the 8 value bytes come from two loads
+// issued together, the type is wave-uniform (one schema) — and parks the
+// coordinate; the hash passes then cover only the key and the strings
+// (a.p2), and the wave stores its G * A coordinates from LDS at the end.
+template <bool TOUCH, bool A4 = false, int SHAPE = 0, int G = 64, bool REGIONS = false, bool NW = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8)))
 hash_encoded_kernel(const EncodedArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
@@ -102,7 +108,8 @@ hash_encoded_kernel(const EncodedArgs a) {
     uint8_t* wsmem = smem_raw + (REGIONS ? (size_t)a.lds_tables * 8 : 0) + (size_t)w * encoded_lds_per_wave(A, G);
     uint64_t* bases = reinterpret_cast<uint64_t*>(wsmem);           // [G][2]
     uint8_t* codes = wsmem + G * 16;                                 // [256]
-    EncDesc* desc = reinterpret_cast<EncDesc*>(wsmem + G * 16 + 256);
+    uint8_t* p2 = wsmem + G * 16 + 256;                              // [256]
+    EncDesc* desc = reinterpret_cast<EncDesc*>(wsmem + G * 16 + 512);
     bool bad = false;
     const uint64_t o0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + w) * G;
     if (o0 >= a.n) return;  // no barrier after this point: waves are independent
@@ -118,6 +125,8 @@ hash_encoded_kernel(const EncodedArgs a) {
         bases[2 * lane + 1] = koff;
     }
     for (uint32_t j = lane; j < A; j += 64) codes[j] = a.codes[j];
+    if constexpr (NW)
+        for (uint32_t j = lane; j < a.S; j += 64) p2[j] = a.p2[j];
 
     // phase 0: pull the value's lines toward L2 (independent loads, consumed late)
     uint32_t sink = 0;
@@ -133,8 +142,32 @@ hash_encoded_kernel(const EncodedArgs a) {
     ok = ok && load_be16(v + 8) == A - 1;
     if (valid) desc[lane * A] = EncDesc{0u, klen};
     uint32_t pos = 10;
+    uint64_t* parked = reinterpret_cast<uint64_t*>(desc);  // coordinate of slot s over desc[s]
     for (uint32_t k = 0; k + 1 < A; ++k) {
         uint32_t len = 0;
+        const uint32_t cj = a.codes[k + 1];  // wave-uniform (scalar load)
+        if (NW && cj != CODE_STRING) {
+            uint64_t h = 0;
+            if (ok) {
+                if (vlen - pos < 4) {
+                    ok = false;
+                } else {
+                    // the 8 value bytes are read with the prefix when the value has room for them
+                    const bool room = vlen - pos >= 12;
+                    len = load_be32(v + pos);
+                    const uint64_t bits = room ? *(const __attribute__((address_space(1))) u64_u*)(v + pos + 4) : 0;
+                    pos += 4;
+                    if (len > vlen - pos) ok = false;
+                    else if (cj == CODE_ZERO) h = 0;                  // datatype_info.cc:169-180
+                    else if (len == 8) h = hash_numeric(cj, bits);
+                    else if (len == 0) h = hash_numeric(cj, 0);
+                    else bad = true;                                   // the reference asserts
+                }
+            }
+            if (valid) parked[lane * A + 1 + k] = ok ? h : 0;
+            if (ok) pos += len;
+            continue;
+        }
         if (ok) {
             if (vlen - pos < 4) {
                 ok = false;
@@ -148,7 +181,10 @@ hash_encoded_kernel(const EncodedArgs a) {
         if (ok) pos += len;
     }
     if (valid && !ok)  // undecodable: every coordinate of the object is 0
-        for (uint32_t j = 0; j < A; ++j) desc[lane * A + j] = EncDesc{kZeroSlot, 0u};
+        for (uint32_t j = 0; j < A; ++j) {
+            if (NW && j > 0 && codes[j] != CODE_STRING) parked[lane * A + j] = 0;
+            else desc[lane * A + j] = EncDesc{kZeroSlot, 0u};
+        }
     if (valid && a.versions) a.versions[i] = ok ? version : 0;
     const bool any_bad = __any(valid && !ok);
     if (TOUCH) asm volatile("; touch sink %0" ::"v"(sink));  // keeps the phase-0 loads live
@@ -157,11 +193,13 @@ hash_encoded_kernel(const EncodedArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
     const uint32_t nslots = nobj * A;
-    // phase 2: passes of 64 slots (slot s = object * A + attribute).  The object's bases and the attribute's code are
+    // phase 2: passes of 64 slots (slot s = object * A + attribute; NW: pass
+    // slot q = object * S + its index in a.p2).  The object's bases and the attribute's code are
     // read from LDS, not from other lanes: in a partial pass the lanes past the
     // batch end are inactive, and a ds_bpermute from an inactive lane returns 0.
-    uint64_t* parked = reinterpret_cast<uint64_t*>(desc);  // REGIONS: coordinate of slot s over desc[s]
-    const uint32_t npass = SHAPE == 1 ? 0 : (nslots + 63) / 64;
+    constexpr bool PARK = REGIONS || NW;  // coordinates parked over their descriptors
+    const uint32_t nq = NW ? nobj * a.S : nslots;
+    const uint32_t npass = SHAPE == 1 ? 0 : (nq + 63) / 64;
     if (SHAPE == 1) {
         for (uint32_t s = lane; s < nslots; s += 64) a.coords[o0 * A + s] = desc[s].off;
         return;
@@ -174,12 +212,21 @@ hash_encoded_kernel(const EncodedArgs a) {
     };
     auto load_pass = [&](uint32_t t, Pass& P) {
         const uint32_t q = t * 64 + (uint32_t)lane;
-        const uint32_t s = min(q, nslots - 1);
-        const uint32_t obj = div_small(s, a.a_magic), j = s - obj * A;  // s < 64 * A
+        uint32_t s, obj, j;
+        if constexpr (NW) {
+            const uint32_t qq = min(q, nq - 1);
+            obj = div_small(qq, a.s_magic);
+            j = p2[qq - obj * a.S];
+            s = obj * A + j;
+        } else {
+            s = min(q, nslots - 1);
+            obj = div_small(s, a.a_magic);  // s < 64 * A
+            j = s - obj * A;
+        }
         const EncDesc d = desc[s];
         const uint64_t base = bases[2 * obj + (j == 0)];
-        const bool zero = d.off == kZeroSlot || q >= nslots;
-        P.s = q < nslots ? s : 0xffffffffu;
+        const bool zero = d.off == kZeroSlot || q >= nq;
+        P.s = q < nq ? s : 0xffffffffu;
         P.code = zero ? (uint32_t)CODE_ZERO : (uint32_t)codes[j];
         P.n = zero ? 0u : d.len;
         P.p = zero ? g_zero_pad : (j == 0 ? a.keys : a.vals) + base + d.off;
@@ -193,8 +240,8 @@ hash_encoded_kernel(const EncodedArgs a) {
             const uint64_t h = SHAPE == 2 ? touch_blk(P0.code, P0.p, P0.n, consume_any<A4>(P0.blk))
                                           : hash_blk<false, false, A4>(P0.code, P0.p, P0.n, consume_any<A4>(P0.blk), bad);
             if (P0.s != 0xffffffffu) {
-                if (!REGIONS || out) __builtin_nontemporal_store(h, out + P0.s);
-                if (REGIONS) parked[P0.s] = h;
+                if (!PARK) __builtin_nontemporal_store(h, out + P0.s);
+                else parked[P0.s] = h;
             }
         }
         if (t + 1 >= npass) break;
@@ -203,17 +250,21 @@ hash_encoded_kernel(const EncodedArgs a) {
             const uint64_t h = SHAPE == 2 ? touch_blk(P1.code, P1.p, P1.n, consume_any<A4>(P1.blk))
                                           : hash_blk<false, false, A4>(P1.code, P1.p, P1.n, consume_any<A4>(P1.blk), bad);
             if (P1.s != 0xffffffffu) {
-                if (!REGIONS || out) __builtin_nontemporal_store(h, out + P1.s);
-                if (REGIONS) parked[P1.s] = h;
+                if (!PARK) __builtin_nontemporal_store(h, out + P1.s);
+                else parked[P1.s] = h;
             }
         }
         if (t + 2 >= npass) break;
     }
-    if constexpr (REGIONS) {
-        // phase 3: lane = object; configuration::lookup_region per table
+    if constexpr (PARK) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (out)  // the wave's G * A coordinates, coalesced, in slot order
+            for (uint32_t s = lane; s < nslots; s += 64) __builtin_nontemporal_store(parked[s], out + s);
+    }
+    if constexpr (REGIONS) {
+        // phase 3: lane = object; configuration::lookup_region per table
         // the tables in a wave-uniform loop, one lane per object: a table's
         // fields are then scalar loads (one lane per (table, object) pair
         // read every field per lane: 0.60 vs 0.47 ms in the batch kernel's
@@ -240,7 +291,7 @@ hash_encoded_kernel(const EncodedArgs a) {
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <bool TOUCH, bool A4, int SHAPE = 0, int G = 64, bool REGIONS = false>
+template <bool TOUCH, bool A4, int SHAPE = 0, int G = 64, bool REGIONS = false, bool NW = false>
 static hipError_t launch_encoded(const EncodedArgs& a, hipStream_t stream) {
     // 4 waves per workgroup while they fit in 64 KiB of LDS (A <= 28 at G = 64), else 1
     const size_t per_wave = encoded_lds_per_wave(a.A, G);
@@ -248,7 +299,7 @@ static hipError_t launch_encoded(const EncodedArgs& a, hipStream_t stream) {
     const uint64_t waves = (a.n + G - 1) / G;
     uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_encoded_kernel<TOUCH, A4, SHAPE, G, REGIONS>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
+    hipLaunchKernelGGL((hash_encoded_kernel<TOUCH, A4, SHAPE, G, REGIONS, NW>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
                        waves_per_block * per_wave + (REGIONS ? (size_t)a.lds_tables * 8 : 0), stream, a);
     return hipGetLastError();
 }
@@ -257,6 +308,10 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
     if (a_in.n == 0) return hipSuccess;
     EncodedArgs a = a_in;
     a.a_magic = (uint32_t)(((1ull << 31) + a.A - 1) / a.A);
+    a.S = 0;
+    for (uint32_t j = 0; j < a.A; ++j)
+        if (j == 0 || a.codes[j] == CODE_STRING) a.p2[a.S++] = (uint8_t)j;
+    a.s_magic = (uint32_t)(((1ull << 31) + a.S - 1) / a.S);
     // default: dword-aligned loads (5.49 vs 6.14 ms per 10 M config-3b objects,
     // profiles/r1/ab_a4_cfg5.jsonl), 32 objects per wave (5.05 vs 5.31 ms for
     // 64 (variant 47) and 5.88 for 16 (48), ab_cfg5_objects_per_wave.jsonl);
@@ -291,6 +346,10 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
         case 57: return launch_encoded<false, true, 1>(a, stream);  // debug shape: the walk alone (WRONG coords)
         case 58: return launch_encoded<false, true, 2>(a, stream);  // debug shape: phase 2 loads only (WRONG coords)
         case 47: return launch_encoded<false, true, 0, 64>(a, stream);
+        // numeric walk (non-string value attributes hashed during the walk): 32 / 64 objects per wave
+        case 170: return launch_encoded<false, true, 0, 32, false, true>(a, stream);
+        case 171: return launch_encoded<false, true, 0, 64, false, true>(a, stream);
+        case 172: return launch_encoded<false, true, 0, 16, false, true>(a, stream);
         case 48: return launch_encoded<false, true, 0, 16>(a, stream);
         // LDS-staged (hdx_encoded_staged.hip): 95 G=7 sorted 10 KiB, 96 G=11 sorted 14 KiB,
         // 97 G=3 sorted 5 KiB, 98 G=4 unsorted 6 KiB, 99 G=15 sorted 20 KiB

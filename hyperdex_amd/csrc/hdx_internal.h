@@ -128,6 +128,10 @@ struct EncodedArgs {
     uint32_t T, lds_tables;  // lds_tables: u64 words of the workgroup's table copies
     SweepTable t[kMaxSweepTables];
     uint8_t codes[HDX_MAX_ATTRS];
+    // numeric walk (launch_hash_encoded fills them): the attributes left to the
+    // hash passes — the key and every STRING value attribute — in order
+    uint8_t p2[HDX_MAX_ATTRS];
+    uint32_t S, s_magic;  // how many; ceil(2^31 / S)
 };
 
 hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream);

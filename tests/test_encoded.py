@@ -167,7 +167,7 @@ def test_oracle_scattered_layout(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [-1, 43, 47, 95, 98, 99])
+@pytest.mark.parametrize("variant", [-1, 43, 47, 95, 98, 99, 170, 171])
 def test_gpu_encoded_scattered_layout(oracle, variant):
     """Objects whose keys and values lie in shuffled order with gaps hash
     exactly as the packed layout does."""
@@ -189,7 +189,7 @@ def test_gpu_encoded_scattered_layout(oracle, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [-1, 33, 43, 47, 48, 95, 96, 97, 98, 99])
+@pytest.mark.parametrize("variant", [-1, 33, 43, 47, 48, 95, 96, 97, 98, 99, 170, 171, 172])
 def test_gpu_encoded_every_variant(oracle, variant):
     """Every stored-object sweep kernel (hdx_encoded.hip; 33 adds the line
     touch) is bit-exact on every config, on corrupt values, on ragged object
@@ -212,6 +212,52 @@ def test_gpu_encoded_every_variant(oracle, variant):
             torch.cuda.synchronize()
             assert np.array_equal(got.cpu().numpy().view(np.uint64), want), (cfg, n)
             assert np.array_equal(versions.cpu().numpy().view(np.uint64), wver), (cfg, n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [-1, 170, 171])
+def test_gpu_encoded_bad_numeric_size(oracle, variant):
+    """A stored int64 / float / timestamp value of neither 0 nor 8 bytes (the
+    reference asserts, datatype_int64.cc:233): its coordinate is 0 and status
+    gets HDX_E_BADSIZE; every other coordinate is the oracle's.  Values with
+    just enough room for the prefix (no speculative 8-byte read past them)."""
+    import struct
+
+    import torch
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import _lib, datatypes as dt
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(variant + 100)
+    types = [dt.HYPERDATATYPE_STRING, dt.HYPERDATATYPE_INT64, dt.HYPERDATATYPE_STRING,
+             dt.HYPERDATATYPE_FLOAT, dt.TIMESTAMPS[2], dt.HYPERDATATYPE_LIST_STRING]
+    n = 300
+    keys, vals, want = [], [], np.zeros((n, len(types)), np.uint64)
+    for i in range(n):
+        key = rng.bytes(int(rng.integers(0, 80)))
+        attrs = [rng.bytes(8) if rng.random() < 0.9 else b"", rng.bytes(int(rng.integers(0, 150))),
+                 rng.bytes(8), rng.bytes(8) if rng.random() < 0.8 else b"", rng.bytes(int(rng.integers(0, 30)))]
+        badk = int(rng.integers(0, 3)) if i % 7 == 3 else -1  # one of the numerics mis-sized
+        if badk >= 0:
+            attrs[(0, 2, 3)[badk]] = rng.bytes(int(rng.choice([1, 4, 7, 9, 16])))
+        keys.append(key)
+        vals.append(struct.pack(">QH", i, len(attrs)) + b"".join(struct.pack(">I", len(x)) + x for x in attrs))
+        want[i, 0] = oracle.hash_value(types[0], key)[0]
+        for k, x in enumerate(attrs):
+            h, err = oracle.hash_value(types[k + 1], x)
+            want[i, k + 1] = 0 if err else h
+    key_len = np.array([len(k) for k in keys], np.uint32)
+    val_len = np.array([len(v) for v in vals], np.uint32)
+    key_off = np.concatenate([[0], np.cumsum(key_len)[:-1]]).astype(np.uint64)
+    val_off = np.concatenate([[0], np.cumsum(val_len)[:-1]]).astype(np.uint64)
+    enc = (np.frombuffer(b"".join(keys) + b"\0", np.uint8), key_off, key_len,
+           np.frombuffer(b"".join(vals), np.uint8), val_off, val_len)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    with _lib.debug_library(variant):
+        got = hdx.hash_encoded(types, *_to_dev(torch, dev, enc), status=status)
+        torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().view(np.uint64), want)
+    assert int(status.item()) == 1 << _lib.HDX_E_BADSIZE
 
 
 @pytest.mark.gpu
