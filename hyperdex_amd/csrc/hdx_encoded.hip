@@ -86,7 +86,14 @@ __host__ __device__ constexpr size_t encoded_lds_per_wave(uint32_t A, uint32_t G
 // issued together, the type is wave-uniform (one schema) — and parks the
 // coordinate; the hash passes then cover only the key and the strings
 // (a.p2), and the wave stores its G * A coordinates from LDS at the end.
-template <bool TOUCH, bool A4 = false, int SHAPE = 0, int G = 64, bool REGIONS = false, bool NW = false>
+// SPEC (with NW): a run of consecutive int64 / float / timestamp attributes is
+// read in one round trip — every prefix and value at the position it has if
+// the run's values are all 8 bytes — then checked in order; from the first
+// prefix that is not 8 on, that lane reads the rest of the run one prefix at
+// a time.  The prefix walk is a chain of dependent loads, and this takes
+// R - 1 links out of it for a run of R fixed-size values.
+template <bool TOUCH, bool A4 = false, int SHAPE = 0, int G = 64, bool REGIONS = false, bool NW = false,
+          bool SPEC = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4, 8)))
 hash_encoded_kernel(const EncodedArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem_raw[];
@@ -146,6 +153,52 @@ hash_encoded_kernel(const EncodedArgs a) {
     for (uint32_t k = 0; k + 1 < A; ++k) {
         uint32_t len = 0;
         const uint32_t cj = a.codes[k + 1];  // wave-uniform (scalar load)
+        if (SPEC && cj >= CODE_INT64) {
+            constexpr uint32_t kRun = 8;
+            uint32_t R = 1;  // wave-uniform run length (scalar loop over the codes)
+            while (R < kRun && k + 1 + R < A && a.codes[k + 1 + R] >= CODE_INT64) ++R;
+            uint32_t hd[kRun];
+            uint64_t bits[kRun];
+#pragma unroll
+            for (uint32_t m = 0; m < kRun; ++m) {
+                const bool room = m < R && ok && vlen - pos >= 12 * (m + 1);
+                hd[m] = room ? load_be32(v + pos + 12 * m) : 0u;
+                bits[m] = room ? *(const __attribute__((address_space(1))) u64_u*)(v + pos + 12 * m + 4) : 0;
+            }
+            bool spec = true;
+#pragma unroll
+            for (uint32_t m = 0; m < kRun; ++m) {
+                if (m >= R) break;
+                const uint32_t cm = a.codes[k + 1 + m];
+                uint64_t h = 0;
+                if (ok) {
+                    if (vlen - pos < 4) {
+                        ok = false;
+                    } else {
+                        uint32_t lm;
+                        uint64_t b;
+                        if (spec && hd[m] == 8 && vlen - pos >= 12) {
+                            lm = 8;
+                            b = bits[m];
+                        } else {  // off the predicted positions: one prefix at a time
+                            spec = false;
+                            lm = load_be32(v + pos);
+                            b = lm == 8 && vlen - pos >= 12 ? *(const __attribute__((address_space(1))) u64_u*)(v + pos + 4)
+                                                            : 0;
+                        }
+                        pos += 4;
+                        if (lm > vlen - pos) ok = false;
+                        else if (lm == 8) h = hash_numeric(cm, b);
+                        else if (lm == 0) h = hash_numeric(cm, 0);
+                        else bad = true;
+                        if (ok) pos += lm;
+                    }
+                }
+                if (valid) parked[lane * A + 1 + k + m] = ok ? h : 0;
+            }
+            k += R - 1;
+            continue;
+        }
         if (NW && cj != CODE_STRING) {
             uint64_t h = 0;
             if (ok) {
@@ -291,7 +344,7 @@ hash_encoded_kernel(const EncodedArgs a) {
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <bool TOUCH, bool A4, int SHAPE = 0, int G = 64, bool REGIONS = false, bool NW = false>
+template <bool TOUCH, bool A4, int SHAPE = 0, int G = 64, bool REGIONS = false, bool NW = false, bool SPEC = false>
 static hipError_t launch_encoded(const EncodedArgs& a, hipStream_t stream) {
     // 4 waves per workgroup while they fit in 64 KiB of LDS (A <= 28 at G = 64), else 1
     const size_t per_wave = encoded_lds_per_wave(a.A, G);
@@ -299,7 +352,7 @@ static hipError_t launch_encoded(const EncodedArgs& a, hipStream_t stream) {
     const uint64_t waves = (a.n + G - 1) / G;
     uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_encoded_kernel<TOUCH, A4, SHAPE, G, REGIONS, NW>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
+    hipLaunchKernelGGL((hash_encoded_kernel<TOUCH, A4, SHAPE, G, REGIONS, NW, SPEC>), dim3((uint32_t)blocks), dim3(64 * waves_per_block),
                        waves_per_block * per_wave + (REGIONS ? (size_t)a.lds_tables * 8 : 0), stream, a);
     return hipGetLastError();
 }
@@ -350,6 +403,9 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
         case 170: return launch_encoded<false, true, 0, 32, false, true>(a, stream);
         case 171: return launch_encoded<false, true, 0, 64, false, true>(a, stream);
         case 172: return launch_encoded<false, true, 0, 16, false, true>(a, stream);
+        // ... plus runs of fixed-size values read in one round trip: 32 / 64 objects per wave
+        case 173: return launch_encoded<false, true, 0, 32, false, true, true>(a, stream);
+        case 174: return launch_encoded<false, true, 0, 64, false, true, true>(a, stream);
         case 48: return launch_encoded<false, true, 0, 16>(a, stream);
         // LDS-staged (hdx_encoded_staged.hip): 95 G=7 sorted 10 KiB, 96 G=11 sorted 14 KiB,
         // 97 G=3 sorted 5 KiB, 98 G=4 unsorted 6 KiB, 99 G=15 sorted 20 KiB

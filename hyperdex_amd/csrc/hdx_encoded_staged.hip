@@ -34,6 +34,8 @@
 
 namespace hdx {
 
+#if HDX_DEBUG_BUILD  // an A/B experiment: not in the product library
+
 namespace {
 
 typedef uint32_t __attribute__((aligned(1))) eu32_u;
@@ -287,5 +289,7 @@ hipError_t launch_hash_encoded_staged(const EncodedArgs& a, int G, uint32_t WB, 
         default: return hipErrorInvalidValue;
     }
 }
+
+#endif  // HDX_DEBUG_BUILD
 
 }  // namespace hdx

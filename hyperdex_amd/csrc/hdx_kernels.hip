@@ -1212,7 +1212,7 @@ static bool known_variant(int v) {
         case 110: case 111:  // fused hash + lookup_region forms (launch_fused_debug)
         case 140: case 141: case 142: case 143: case 144: case 145: case 146: case 147:
         case 150: case 151: case 152: case 153: case 154: case 155: case 160: case 161:
-        case 170: case 171: case 172:  // the sweep's numeric walk (hdx_encoded.hip)
+        case 170: case 171: case 172: case 173: case 174:  // the sweep's numeric walk (hdx_encoded.hip)
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;
