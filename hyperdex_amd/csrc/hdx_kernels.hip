@@ -1007,6 +1007,20 @@ static hipError_t launch_regroup_wpe(const BatchArgs& args, hipStream_t stream) 
 #endif
 
 #if HDX_DEBUG_BUILD
+// Debug: variant 44's kernel with unused dynamic LDS, so that at most
+// wg_per_cu workgroups share a CU (fewer waves contending for the L1).
+static hipError_t launch_44_wg_limit(const BatchArgs& args, hipStream_t stream, uint32_t wg_per_cu) {
+    constexpr int C = 2;
+    const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
+    const uint64_t blocks = (waves + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    const size_t dyn = 160 * 1024 / wg_per_cu - sizeof(RegroupLds<C>) - 1024;
+    hipLaunchKernelGGL((hash_regroup_kernel<C, true, true, true, true, false, true, 1>), dim3((uint32_t)blocks),
+                       dim3(256), dyn, stream, args);
+    return hipGetLastError();
+}
+
 template <int C>
 static hipError_t launch_quad(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
@@ -1103,6 +1117,9 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 145: return launch_regroup_wpe<5, 16, true, false, false>(args, stream);
         case 146: return launch_regroup_wpe<5, 8, true, true, true, false, false, true, 1>(args, stream);
         case 147: return launch_regroup_wpe<6, 8, true, true, true, false, false, true, 1>(args, stream);
+        case 180: return launch_44_wg_limit(args, stream, 2);
+        case 181: return launch_44_wg_limit(args, stream, 3);
+        case 182: return launch_44_wg_limit(args, stream, 4);
         case 160: return launch_quad<2>(args, stream);
         case 161: return launch_quad<4>(args, stream);
         case 154: return launch_regd<4>(args, stream);
@@ -1213,6 +1230,7 @@ static bool known_variant(int v) {
         case 140: case 141: case 142: case 143: case 144: case 145: case 146: case 147:
         case 150: case 151: case 152: case 153: case 154: case 155: case 160: case 161:
         case 170: case 171: case 172: case 173: case 174:  // the sweep's numeric walk (hdx_encoded.hip)
+        case 180: case 181: case 182:
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;
