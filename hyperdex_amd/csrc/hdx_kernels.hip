@@ -163,7 +163,7 @@ struct RegroupLds {
 // lookup_region, hdx_region_lookup.h; tbl = the workgroup's LDS copies) and
 // stores coordinates only when args.coords is set.
 template <int C, bool NT_STORE, bool SORT, bool DIRECT, bool A4, bool PIPE, bool ASORT, int ORDER, bool REG,
-          bool UNI = false, bool REGD = false, bool QUAD = false>
+          bool UNI = false, bool REGD = false, bool QUAD = false, int LATE = 0>
 __device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C>& lds, const uint64_t* tbl,
                                              uint64_t wave = ~0ull) {
     const int lane = threadIdx.x & 63;
@@ -292,7 +292,13 @@ __device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C
         const uint32_t s = uniform ? (uint32_t)(t * 64 + lane) : perm[t * 64 + lane];
         if constexpr (REGD) P.d = dreg[t];
         else P.d = desc[s];
-        P.blk = issue_any<A4>(P.d.code_slot & 0xffu, P.d.p, P.d.n);
+        if constexpr (LATE != 0) {  // LATE 1: > 64-byte strings load their head with their first
+            // block; LATE 2: only the one-block strings (65..128 bytes)
+            const bool g64 = (P.d.code_slot & 0xffu) == CODE_STRING && P.d.n > 64 && (LATE == 1 || P.d.n <= 128);
+            P.blk = issue_any<A4>(g64 ? (uint32_t)CODE_ZERO : P.d.code_slot & 0xffu, P.d.p, g64 ? 0u : P.d.n);
+        } else {
+            P.blk = issue_any<A4>(P.d.code_slot & 0xffu, P.d.p, P.d.n);
+        }
     };
     bool bad = false;
     Pass P0, P1;
@@ -303,7 +309,13 @@ __device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C
         Pass& nxt = (t & 1) ? P0 : P1;
         if (t + 1 < C) load_pass(t + 1, nxt);
         uint64_t h;
-        if constexpr (QUAD) {
+        if constexpr (LATE != 0) {
+            static_assert(A4 && !PIPE, "the late head follows the A4 piece layout");
+            const uint32_t cd = cur.d.code_slot & 0xffu;
+            h = cd == CODE_STRING && cur.d.n > 64 && (LATE == 1 || cur.d.n <= 128) ? city_gt64_late(cur.d.p, cur.d.n)
+                                                   : hash_blk<false, false, true>(cd, cur.d.p, cur.d.n,
+                                                                                 consume_any<true>(cur.blk), bad);
+        } else if constexpr (QUAD) {
             static_assert(A4, "the quad-cooperative loop follows the A4 piece layout");
             h = hash_blk_quad(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n, consume_any<A4>(cur.blk), bad);
         } else {
@@ -406,6 +418,15 @@ __global__ void __launch_bounds__(256)
 hash_regroup_quad_kernel(const BatchArgs args) {
     __shared__ RegroupLds<C> lds;
     regroup_body<C, true, true, true, true, false, true, 1, false, false, false, true>(args, lds, nullptr);
+}
+
+// Debug: variant 44 with each > 64-byte string's head (190), or each one-block
+// string's (191), loaded with its first loop block instead of a pass ahead.
+template <int C, int LATE>
+__global__ void __launch_bounds__(256)
+hash_regroup_late_kernel(const BatchArgs args) {
+    __shared__ RegroupLds<C> lds;
+    regroup_body<C, true, true, true, true, false, true, 1, false, false, false, false, LATE>(args, lds, nullptr);
 }
 
 // Debug: unsorted waves with the descriptors in registers (variants 154/155).
@@ -1021,6 +1042,16 @@ static hipError_t launch_44_wg_limit(const BatchArgs& args, hipStream_t stream, 
     return hipGetLastError();
 }
 
+template <int C, int LATE>
+static hipError_t launch_late(const BatchArgs& args, hipStream_t stream) {
+    const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
+    const uint64_t blocks = (waves + 3) / 4;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((hash_regroup_late_kernel<C, LATE>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    return hipGetLastError();
+}
+
 template <int C>
 static hipError_t launch_quad(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
@@ -1117,6 +1148,8 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 145: return launch_regroup_wpe<5, 16, true, false, false>(args, stream);
         case 146: return launch_regroup_wpe<5, 8, true, true, true, false, false, true, 1>(args, stream);
         case 147: return launch_regroup_wpe<6, 8, true, true, true, false, false, true, 1>(args, stream);
+        case 190: return launch_late<2, 1>(args, stream);
+        case 191: return launch_late<2, 2>(args, stream);
         case 180: return launch_44_wg_limit(args, stream, 2);
         case 181: return launch_44_wg_limit(args, stream, 3);
         case 182: return launch_44_wg_limit(args, stream, 4);
@@ -1230,7 +1263,7 @@ static bool known_variant(int v) {
         case 140: case 141: case 142: case 143: case 144: case 145: case 146: case 147:
         case 150: case 151: case 152: case 153: case 154: case 155: case 160: case 161:
         case 170: case 171: case 172: case 173: case 174:  // the sweep's numeric walk (hdx_encoded.hip)
-        case 180: case 181: case 182:
+        case 180: case 181: case 182: case 190: case 191:
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;

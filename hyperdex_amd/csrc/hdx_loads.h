@@ -435,6 +435,44 @@ __device__ __forceinline__ uint64_t city_gt64_quad(const uint8_t* s, uint32_t n,
     return mix16(mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z, mix16(v1, w1, KMUL) + x, KMUL);
 }
 
+// city_gt64_reg (A4) with the head pieces loaded here, back to back with the
+// first loop block — not a pass ahead — so that the L1 merges their requests
+// for the lines they share (debug variant 190).
+__device__ __forceinline__ uint64_t city_gt64_late(const uint8_t* p, uint32_t n) {
+    const Raw r = issue_block_a4(CODE_STRING, p, n);
+    const Blk64 b0 = ld64<true, false>(p);
+    const Blk t = funnel_raw(r);
+    const u64x2 e0 = t.v0, e1 = t.v1, e2 = t.v2, e3 = t.v3;
+    uint64_t x = e1.y;
+    uint64_t y = e3.x + e0.y;
+    uint64_t z = mix16(e1.x + n, e2.y, KMUL);
+    uint64_t v0, v1, w0, w1;
+    weak32(e0.x, e0.y, e1.x, e1.y, n, z, v0, v1);
+    weak32(e2.x, e2.y, e3.x, e3.y, y + K1, x, w0, w1);
+    const uint32_t sh = (uint32_t)(uintptr_t)p & 3;
+    Blk cur = use64<true>(b0, sh);
+    x = x * K1 + cur.v0.x;
+    const uint32_t blocks = (n - 1) >> 6;
+    const uint8_t* s = p;
+    for (uint32_t k = 0;;) {
+        const u64x2 b_0 = cur.v0, b_1 = cur.v1, b_2 = cur.v2, b_3 = cur.v3;
+        x = ror(x + y + v0 + b_0.y, 37) * K1;
+        y = ror(y + v1 + b_3.x, 42) * K1;
+        x ^= w1;
+        y += v0 + b_2.y;
+        z = ror(z + w0, 33) * K1;
+        uint64_t nv0, nv1, nw0, nw1;
+        weak32(b_0.x, b_0.y, b_1.x, b_1.y, v1 * K1, x + w0, nv0, nv1);
+        weak32(b_2.x, b_2.y, b_3.x, b_3.y, z + w1, y + b_1.x, nw0, nw1);
+        v0 = nv0; v1 = nv1; w0 = nw0; w1 = nw1;
+        const uint64_t tt = z; z = x; x = tt;
+        if (++k == blocks) break;
+        s += 64;
+        cur = use64<true>(ld64<true, false>(s), sh);
+    }
+    return mix16(mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z, mix16(v1, w1, KMUL) + x, KMUL);
+}
+
 // A4: the block comes from issue_block_a4 (16..32-byte, short and numeric
 // pieces in slots 1 and 3).
 template <bool PIPE = false, bool FAKE = false, bool A4 = false>

@@ -289,7 +289,7 @@ def test_full_size_sampled(oracle, torch_dev, cfg):
     torch.cuda.empty_cache()
 
 
-VARIANTS = [12, 18, 19, 20, 21, 25, 26, 30, 31, 35, 37, 38, 39, 44, 45, 46, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 80, 81, 82, 83, 84, 85, 86, 90, 140, 141, 142, 143, 144, 145, 146, 147, 150, 151, 152, 153, 154, 155, 160, 161]
+VARIANTS = [12, 18, 19, 20, 21, 25, 26, 30, 31, 35, 37, 38, 39, 44, 45, 46, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 80, 81, 82, 83, 84, 85, 86, 90, 140, 141, 142, 143, 144, 145, 146, 147, 150, 151, 152, 153, 154, 155, 160, 161, 180, 181, 182, 190, 191]
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
