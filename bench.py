@@ -6,16 +6,26 @@ Metric (BASELINE.json): hashed GiB/s (device-resident) + Mobjects/s on
 synthetic bytes generated in HBM.  A step = one launch hashing the whole
 batch (every attribute of every object -> coords[n, 17]).
 
-Multi-GPU (torchrun, one rank per GPU): each rank owns its own 10M-object
-shard (weak scaling, no collective in the timed region); the RCCL all-gather
-of the coordinates is timed separately and reported as `allgather`.
+Multi-GPU (`--gpus N`, one rank per GPU on RCCL): launched bare, the parent
+starts N fresh rank processes itself (before it touches the GPU) and relays
+rank 0's line; under torchrun/torch.distributed.run (WORLD_SIZE set) each
+process is one rank and WORLD_SIZE must equal --gpus.  Each rank owns its own
+10M-object shard (weak scaling, no collective in the timed region); the RCCL
+all-gather of the coordinates is timed separately and reported as `allgather`.
 
 Config 4 rides along in every line as `config4`: one batch
-of 100M config-3b objects split over the N ranks by payload bytes
-(hyperdex_amd.dist.shard_ranges), each rank hashing its shard straight into
-its rows of the full coordinate matrix (hash phase, max over ranks), then the
-in-place RCCL all-gather of those rows over xGMI (reported apart), so the
-1/2/4/8-GPU runs give config 4's strong-scaling curve.
+of 100M config-3b objects split over the N ranks (hyperdex_amd.dist.
+shard_ranges: equal object counts when that keeps every rank within 0.1 % of
+its byte share, else byte-balanced cuts), each rank hashing its shard
+straight into its rows of the full coordinate matrix (hash phase, max over
+ranks), then ONE all-gather of those rows over xGMI (in place for equal
+counts, padded otherwise; reported apart), so the 1/2/4/8-GPU runs give
+config 4's strong-scaling curve.
+
+HDX_BENCH_DEVICE=cpu (+ HDX_BENCH_BACKEND=gloo) is a CPU rehearsal of the
+multi-rank plumbing only — launch, shard cuts, the config-4 gather and the
+JSON relay — with a stand-in that writes each object's index instead of its
+coordinates (no hashing, no throughput; `value` is null).
 
 Prints ONE JSON line on rank 0.
 """
@@ -37,9 +47,13 @@ ALGO_EXTRA_PER_ATTR = 4 + 8  # u32 length read + u64 coordinate write (SURVEY §
 HBM_PEAK_GBPS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def main():
+CONFIG4_EQUAL_COUNT_TOL = 1e-3  # see shard_ranges(equal_count_tol)
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (GPUs); default WORLD_SIZE under a launcher, else 1")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="cfg3a")
@@ -60,17 +74,82 @@ def main():
                     help="skip timing config 3b (16 mixed attrs) beside the config-3a line")
     ap.add_argument("--traffic", default=latest_traffic_file(),
                     help="HBM bytes/launch measured by scripts/gpu_profile.sh (rocprofv3 PMC)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+def main():
+    args = parse_args()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        if (args.gpus or 1) > 1:
+            # bare `bench.py --gpus N`: start the N ranks here, before anything
+            # in this process initialises HIP
+            sys.exit(spawn_ranks(args.gpus))
+    elif args.gpus is not None and int(env_world) != args.gpus:
+        raise SystemExit("bench.py: WORLD_SIZE=%s but --gpus %d" % (env_world, args.gpus))
+    if os.environ.get("HDX_BENCH_DEVICE", "cuda") == "cpu":
+        return rehearse_cpu(args)
+    return run_rank(args)
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(world, grace_s=30.0):
+    """Run this script as `world` child processes (RANK = LOCAL_RANK = k,
+    WORLD_SIZE, MASTER_ADDR 127.0.0.1, a free MASTER_PORT), relay rank 0's
+    stdout (the JSON line) and return non-zero if any rank failed.  When one
+    rank fails the others get `grace_s` to exit (they may be blocked in a
+    collective) and are then killed by PID."""
+    import subprocess
+    import tempfile
+    port = free_port()
+    out0 = tempfile.TemporaryFile()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
+                   LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=out0 if r == 0 else sys.stderr))
+    failed_at = None
+    while any(p.poll() is None for p in procs):
+        if failed_at is None and any(p.returncode not in (None, 0) for p in procs):
+            failed_at = time.monotonic()
+            log("bench.py: a rank failed (exit codes %s); stopping the others"
+                % [p.returncode for p in procs])
+        if failed_at is not None and time.monotonic() - failed_at > grace_s:
+            for p in procs:
+                if p.poll() is None:
+                    p.kill()
+        time.sleep(0.2)
+    codes = [p.wait() for p in procs]
+    out0.seek(0)
+    for line in out0.read().decode(errors="replace").splitlines():
+        # rank 0's JSON line to stdout; anything else it printed (gloo's
+        # connection banner) to stderr
+        print(line, file=sys.stdout if line.startswith("{") else sys.stderr, flush=True)
+    if any(codes):
+        log("bench.py: rank exit codes %s" % codes)
+        return 1
+    return 0
+
+
+def run_rank(args):
     import torch
     import torch.distributed as dist
 
     import hyperdex_amd as hdx
     from hyperdex_amd import synth
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
     # HDX_BENCH_BACKEND=gloo rehearses the multi-rank flow with every rank on
     # cuda:0 (one-GPU box); the real multi-GPU run is one rank per GPU on RCCL.
     backend = os.environ.get("HDX_BENCH_BACKEND", "nccl")
@@ -82,6 +161,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        world = dist.get_world_size()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -230,6 +310,7 @@ def main():
         else:
             result["cpu_baseline"] = cpu_baseline(types, blob, base, lens, A, args.cpu_seconds,
                                                   coords)
+            result["cpu_per_object"] = cpu_per_object_suite(dev, stream, max(1.5, args.cpu_seconds / 3))
 
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -238,26 +319,20 @@ def main():
 
 
 def time_allgather(coords, world, dev, backend, max_over_ranks, reps=3):
-    """RCCL all-gather of every rank's (n, A) u64 coordinates into (world*n, A)
-    (hyperdex_amd.dist.allgather_coords), timed apart from the hash phase."""
+    """The all-gather of every rank's (n, A) u64 coordinates into (world*n, A)
+    (hyperdex_amd.dist.allgather_coords: one collective), timed apart from the
+    hash phase, and the per-rank D2H of the local shard beside it."""
     import torch
     import torch.distributed as dist
 
-    from hyperdex_amd.dist import allgather_coords
-    src = coords if backend == "nccl" else coords[: min(coords.shape[0], 1_000_000)].cpu()
-    counts = [src.shape[0]] * world
-    out = allgather_coords(src, counts)
-    torch.cuda.synchronize()
-    dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        out = allgather_coords(src, counts)
-    torch.cuda.synchronize()
-    (dt,) = max_over_ranks((time.perf_counter() - t0) / reps)
-    nbytes = out.numel() * 8
+    counts = [coords.shape[0]] * world
+    if backend == "nccl":
+        src = coords
+    else:
+        counts = rehearsal_counts(counts, rows=1_000_000)
+        src = coords[:counts[0]].cpu()
+    res, out = time_gather(src, counts, coords.shape[1], None, max_over_ranks, backend, reps)
     del out
-    res = {"ms": round(dt * 1e3, 3), "bytes": nbytes, "backend": backend,
-           "busbw_GBps": round(nbytes * (world - 1) / world / dt / 1e9, 2)}
     # the cheaper "gather to host" alternative (SURVEY §8e): every rank
     # copies its own shard to pinned host memory at once
     host = torch.empty(coords.shape, dtype=coords.dtype, pin_memory=True)
@@ -276,13 +351,14 @@ def time_allgather(coords, world, dev, backend, max_over_ranks, reps=3):
 
 def time_config4(n_total, world, rank, dev, stream, max_over_ranks, backend, gather=True, steps=5):
     """Config 4: one batch of n_total config-3b objects split
-    over the ranks by payload bytes.  Every rank derives the same cuts from
-    the batch's lengths (dist.shard_ranges on the device), generates its shard
-    in HBM, hashes it straight into its rows of the full (n_total, 17)
-    coordinate matrix (timed with HIP events, max over ranks = the hash
-    phase), then the rows are all-gathered in place (RCCL over xGMI; timed
-    apart), and copied to pinned host memory as the cheaper gather-to-host
-    alternative.  Strong scaling: the batch is the same at every N."""
+    over the ranks (shard_ranges with CONFIG4_EQUAL_COUNT_TOL).  Every rank
+    derives the same cuts from the batch's lengths (computed on the device),
+    generates its shard in HBM, hashes it straight into its rows of the full
+    (n_total, 17) coordinate matrix (timed with HIP events, max over ranks =
+    the hash phase), then ONE all-gather fills the other ranks' rows (RCCL
+    over xGMI; timed apart), and the rows are copied to pinned host memory as
+    the cheaper gather-to-host alternative.  Strong scaling: the batch is the
+    same at every N."""
     import torch
     import torch.distributed as dist
 
@@ -302,7 +378,8 @@ def time_config4(n_total, world, rank, dev, stream, max_over_ranks, backend, gat
         _lib.check(lib.hdx_synth_lengths(cr, A, synth.SEED, f, c, tmp.data_ptr(), stream.cuda_stream))
         sizes[f:f + c] = tmp[:c * A].view(c, A).to(torch.int64).sum(dim=1)
     del tmp
-    ranges = hdist.shard_ranges(n_total, world, sizes)
+    ranges = hdist.shard_ranges(n_total, world, sizes, equal_count_tol=CONFIG4_EQUAL_COUNT_TOL)
+    imbalance = hdist.byte_imbalance(ranges, sizes) if world > 1 else 0.0
     counts = [c for _, c in ranges]
     first, cnt = ranges[rank]
     shard_bytes = int(sizes[first:first + cnt].sum().item())
@@ -330,32 +407,22 @@ def time_config4(n_total, world, rank, dev, stream, max_over_ranks, backend, gat
         dist.all_reduce(t)
         payload_total = float(t.item())
     algo_rank = shard_bytes + cnt * A * ALGO_EXTRA_PER_ATTR
-    res = {"workload": "config 4: %dM config-3b objects sharded over %d GPU(s) by payload bytes"
+    res = {"workload": "config 4: %dM config-3b objects sharded over %d GPU(s)"
                        % (n_total // 1_000_000, world),
-           "objects": n_total, "objects_per_rank": counts, "hash_ms": round(hash_ms, 4),
+           "objects": n_total, "objects_per_rank": counts,
+           "shard_byte_imbalance": round(imbalance, 6), "hash_ms": round(hash_ms, 4),
            "mobjects_per_s": round(n_total / (hash_ms / 1e3) / 1e6, 1),
            "GiB_s": round(payload_total / (hash_ms / 1e3) / 2**30, 2),
            "rank0_roofline_frac": round(algo_rank / (hash_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
            "scaling": "strong"}
     if gather and world > 1:
-        src = mine if backend == "nccl" else mine[: min(cnt, 100_000)].cpu()
-        cnts = counts if backend == "nccl" else [min(c, 100_000) for c in counts]
-        gout = out if backend == "nccl" else None
-        hdist.allgather_coords(src, cnts, out=gout)
-        torch.cuda.synchronize()
-        dist.barrier()
-        reps = 3
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            hdist.allgather_coords(src, cnts, out=gout)
-        torch.cuda.synchronize()
-        (dt,) = max_over_ranks((time.perf_counter() - t0) / reps)
-        nbytes = int(sum(cnts)) * A * 8
-        res["allgather"] = {"ms": round(dt * 1e3, 3), "bytes": nbytes, "backend": backend,
-                            "equal_counts": len(set(cnts)) == 1,
-                            "algbw_GBps": round(nbytes / dt / 1e9, 2),
-                            "busbw_GBps": round(nbytes * (world - 1) / world / dt / 1e9, 2)}
-        res["end_to_end_ms"] = round(hash_ms + dt * 1e3, 3)
+        if backend == "nccl":
+            src, cnts, gout = mine, counts, out
+        else:  # gloo rehearsal on one GPU: host copies, the same counts pattern
+            cnts = rehearsal_counts(counts)
+            src, gout = mine[:cnts[rank]].cpu(), None
+        res["allgather"], _ = time_gather(src, cnts, A, gout, max_over_ranks, backend)
+        res["end_to_end_ms"] = round(hash_ms + res["allgather"]["ms"], 3)
     # gather to host instead: every rank copies its rows to pinned memory at once
     host = torch.empty(mine.shape, dtype=mine.dtype, pin_memory=True)
     host.copy_(mine, non_blocking=True)
@@ -370,6 +437,117 @@ def time_config4(n_total, world, rank, dev, stream, max_over_ranks, backend, gat
     del host, out, mine, blob, base, lens
     torch.cuda.empty_cache()
     return res
+
+
+def rehearsal_counts(counts, rows=100_000):
+    """Per-rank row counts clipped for a host-memory rehearsal, keeping their
+    differences (so equal stays equal and unequal stays unequal)."""
+    cut = max(0, min(counts) - rows)
+    return [int(c) - cut for c in counts]
+
+
+def time_gather(src, counts, A, out, max_over_ranks, backend, reps=3):
+    """hyperdex_amd.dist.allgather_coords of every rank's rows, timed (max
+    over ranks), with the number of collectives each gather issued."""
+    import torch
+    import torch.distributed as dist
+
+    from hyperdex_amd import dist as hdist
+    issued = count_collectives()
+    got = hdist.allgather_coords(src, counts, out=out)
+    if src.is_cuda:
+        torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        got = hdist.allgather_coords(src, counts, out=out)
+    if src.is_cuda:
+        torch.cuda.synchronize()
+    (dt,) = max_over_ranks((time.perf_counter() - t0) / reps)
+    per_gather = issued.stop() / (reps + 1)
+    nbytes = int(sum(counts)) * A * 8
+    return {"ms": round(dt * 1e3, 3), "bytes": nbytes, "backend": backend,
+            "form": hdist.gather_form(counts), "collectives_per_gather": per_gather,
+            "equal_counts": len(set(counts)) == 1,
+            "algbw_GBps": round(nbytes / dt / 1e9, 2),
+            "busbw_GBps": round(nbytes * (len(counts) - 1) / len(counts) / dt / 1e9, 2)}, got
+
+
+class count_collectives:
+    """Counts torch.distributed collective calls until stop() (wraps the
+    module functions allgather_coords may reach)."""
+    NAMES = ("all_gather_into_tensor", "all_gather", "broadcast", "all_to_all_single",
+             "batch_isend_irecv", "send", "recv", "isend", "irecv")
+
+    def __init__(self):
+        import torch.distributed as dist
+        self.n, self.saved = 0, {}
+        for name in self.NAMES:
+            fn = getattr(dist, name)
+            self.saved[name] = fn
+
+            def wrap(*a, _fn=fn, **k):
+                self.n += 1
+                return _fn(*a, **k)
+            setattr(dist, name, wrap)
+
+    def stop(self):
+        import torch.distributed as dist
+        for name, fn in self.saved.items():
+            setattr(dist, name, fn)
+        return self.n
+
+
+def rehearse_cpu(args):
+    """HDX_BENCH_DEVICE=cpu: the multi-rank plumbing on the host (gloo), no
+    hashing.  Same shard cuts and the same single-collective gather as
+    config 4, on a batch of --config4-objects (default 200k here) whose rows
+    are filled with each object's global index by a stand-in, so the gathered
+    matrix can be checked row by row."""
+    import torch
+    import torch.distributed as dist
+
+    from hyperdex_amd import dist as hdist
+    from hyperdex_amd import synth
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_process_group(os.environ.get("HDX_BENCH_BACKEND", "gloo"))
+        world = dist.get_world_size()
+    rank = dist.get_rank() if world > 1 else 0
+
+    def max_over_ranks(*xs):
+        if world == 1:
+            return xs
+        t = torch.tensor(xs, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return tuple(float(v) for v in t.tolist())
+
+    n_total = args.config4_objects if args.config4_objects != 100_000_000 else 200_000
+    rules = synth.CONFIGS["cfg3b"]
+    A = len(rules)
+    sizes = synth.lengths(rules, n_total).reshape(n_total, A).astype(np.int64).sum(axis=1)
+    ranges = hdist.shard_ranges(n_total, world, sizes, equal_count_tol=CONFIG4_EQUAL_COUNT_TOL)
+    counts = [c for _, c in ranges]
+    first, cnt = ranges[rank]
+    out = torch.full((n_total, A), -1, dtype=torch.int64)
+    mine = hdist.rank_rows(out, counts, rank)
+    mine.copy_(torch.arange(first, first + cnt, dtype=torch.int64)[:, None].expand(cnt, A))
+    c4 = {"workload": "config 4 plumbing rehearsal: %d config-3b objects over %d rank(s), no hashing"
+                      % (n_total, world),
+          "objects": n_total, "objects_per_rank": counts,
+          "shard_byte_imbalance": round(hdist.byte_imbalance(ranges, sizes), 6)}
+    if world > 1 and not args.no_allgather:
+        c4["allgather"], got = time_gather(mine, counts, A, out, max_over_ranks, "gloo", reps=1)
+        ok = bool(torch.equal(got, torch.arange(n_total, dtype=torch.int64)[:, None].expand(n_total, A)))
+        (bad,) = max_over_ranks(0.0 if ok else 1.0)
+        c4["allgather"]["verified"] = bad == 0.0
+    result = {"metric": "hashed GiB/s (device-resident) + Mobjects/s, 16-attr×64B batches",
+              "value": None, "unit": "GiB/s", "n_gpus": world, "dry_run": "cpu plumbing rehearsal",
+              "config4": c4}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def key_subspace_tables(A):
@@ -690,6 +868,76 @@ def cpu_baseline(types, blob, base, lens, A, seconds, coords):
             "sample": "%d objects (%.0f MB) of the same batch, %d passes, oracle/hdx_oracle.c -O2 "
                       "pthreads; verified equal to the GPU coords" % (ns, nb / 1e6, reps),
             **host_info(threads, quota)}
+
+
+def cpu_per_object(types, blob, base, lens, coords, seconds, label):
+    """The product's own per-object CPU path (hdx_hash_object / hdx_hash_key,
+    what the C++ drop-in include/hyperdex_amd/hash.h runs for
+    common/hash.cc:48-68) timed the way daemon threads call it: one
+    synchronous call per object (tools/libhdxcpubench.so), single thread and
+    over this host's quota of cores, on a sample of the given batch (host
+    numpy arrays); its output is checked against `coords` (the GPU's)."""
+    import ctypes
+    threads, quota = cpu_threads()
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libhdxcpubench.so"))
+    fn = lib.hdxcpu_time_objects
+    fn.restype = ctypes.c_int
+    vp = ctypes.c_void_p
+    fn.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, ctypes.c_uint64, vp, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_double, vp, vp]
+    A = len(types)
+    n = len(base)
+    t = np.ascontiguousarray(types, np.uint32)
+    out = np.zeros((n, A), np.uint64)
+    key_only = 1 if A == 1 else 0
+    nbytes = int(lens.astype(np.uint64).sum())
+
+    def run(nthreads, budget):
+        passes, secs = ctypes.c_uint64(), ctypes.c_double()
+        rc = fn(t.ctypes.data, A, blob.ctypes.data, base.ctypes.data, lens.ctypes.data, n, out.ctypes.data,
+                nthreads, key_only, budget, ctypes.byref(passes), ctypes.byref(secs))
+        if rc != 0:
+            raise SystemExit("cpu_per_object: hdx status %d" % rc)
+        return passes.value, secs.value
+
+    run(1, 0.0)
+    if not np.array_equal(out, coords.reshape(n, A)):
+        raise SystemExit("cpu_per_object: %s coordinates differ from the GPU's" % label)
+    p1, s1 = run(1, seconds / 3)
+    pm, sm = run(threads, seconds * 2 / 3)
+    return {"workload": label, "objects": n, "bytes": nbytes,
+            "ns_per_object_1thread": round(s1 / (p1 * n) * 1e9, 1),
+            "mobjects_per_s_1thread": round(p1 * n / s1 / 1e6, 3),
+            "GiB_s_1thread": round(p1 * nbytes / s1 / 2**30, 3),
+            "cores": threads, "mobjects_per_s": round(pm * n / sm / 1e6, 3),
+            "GiB_s": round(pm * nbytes / sm / 2**30, 3),
+            "verified_vs_gpu": True}
+
+
+def cpu_per_object_suite(dev, stream, seconds):
+    """cpu_per_object on config 1 (1 M 64-byte keys, BASELINE's CPU-only
+    config) and config 3b (the mixed 16-attribute object); each sample's GPU
+    coordinates come from the product kernel on the same bytes."""
+    import torch
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import synth
+    threads, quota = cpu_threads()
+    res = {"kind": "product per-object CPU path (hdx_hash_object / hdx_hash_key via libhdxcpubench)",
+           **host_info(threads, quota), "configs": {}}
+    samples = [("config 1: 64-byte key, hash(schema, key, &h)", "cfg1", 1_000_000),
+               ("config 3b: key + 16 mixed attrs, hash(schema, key, value, hs)", "cfg3b", 100_000)]
+    for label, cfg, n in samples:
+        types, blob, base, lens = synth.make_batch_host(cfg, n)
+        tb = torch.from_numpy(blob).to(dev)
+        to = torch.from_numpy(base.view(np.int64)).to(dev)
+        tl = torch.from_numpy(lens.view(np.int32)).to(dev)
+        got = hdx.hash_batch(types, tb, to, tl, stream=stream)
+        torch.cuda.synchronize()
+        gpu = got.cpu().numpy().view(np.uint64)
+        res["configs"][cfg] = cpu_per_object(types, blob, base, lens, gpu, seconds, label)
+        del tb, to, tl, got
+    return res
 
 
 def cgroup_cpu_quota():

@@ -118,3 +118,18 @@ def test_reference_assert_paths_return_errors():
         hdx.hash_object([dt.HYPERDATATYPE_STRING, dt.HYPERDATATYPE_INT64], b"k", [b"123"])
     assert e.value.status == _lib.HDX_E_BADSIZE
     assert hdx.hash(dt.HYPERDATATYPE_MAP_STRING_INT64, b"\x01\x02\x03") == 0  # not hashable -> 0
+
+
+def test_cpubench_harness_matches_oracle():
+    """bench.py's cpu_per_object leg (tools/libhdxcpubench.so: one
+    hdx_hash_object / hdx_hash_key call per object, N threads) computes the
+    reference's coordinates; bench.py checks the same against the GPU's."""
+    import bench
+    from hyperdex_amd import synth
+    from oracle import oracle
+    for cfg, n in (("cfg1", 5000), ("cfg3b", 3000), ("mixed", 2000)):
+        types, blob, base, lens = synth.make_batch_host(cfg, n, seed=11)
+        want, err = oracle.hash_batch(types, blob, base, lens)
+        assert err == 0
+        res = bench.cpu_per_object(types, blob, base, lens, want, 0.05, cfg)
+        assert res["verified_vs_gpu"] and res["objects"] == n and res["ns_per_object_1thread"] > 0

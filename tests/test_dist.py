@@ -55,12 +55,57 @@ def _free_port():
     return p
 
 
+def test_shard_ranges_equal_count_tolerance():
+    """Equal counts whenever every rank stays within the tolerance of its byte
+    share (the single in-place all-gather), byte-balanced cuts otherwise."""
+    rng = np.random.default_rng(3)
+    sizes = rng.integers(0, 196, 200_000) + 64
+    for world in (2, 3, 8):
+        even = hdist.shard_ranges(len(sizes), world)
+        got = hdist.shard_ranges(len(sizes), world, sizes, equal_count_tol=1e-2)
+        assert got == even and hdist.byte_imbalance(got, sizes) <= 1e-2
+        assert hdist.shard_ranges(len(sizes), world, torch.from_numpy(sizes), equal_count_tol=1e-2) == even
+    skew = np.concatenate([np.full(1000, 10), np.full(1000, 1000)])
+    got = hdist.shard_ranges(len(skew), 2, skew, equal_count_tol=1e-3)
+    assert got == hdist.shard_ranges(len(skew), 2, skew) and got != hdist.shard_ranges(len(skew), 2)
+    assert hdist.gather_form([5, 5]) == "in_place" and hdist.gather_form([5, 6]) == "padded"
+
+
+class _Count:
+    """Counts torch.distributed collectives issued while active."""
+    NAMES = ("all_gather_into_tensor", "all_gather", "broadcast", "all_to_all_single",
+             "batch_isend_irecv", "send", "recv", "isend", "irecv")
+
+    def __enter__(self):
+        self.n, self.saved = 0, {k: getattr(dist, k) for k in self.NAMES}
+        for k, fn in self.saved.items():
+            def wrap(*a, _fn=fn, **kw):
+                self.n += 1
+                return _fn(*a, **kw)
+            setattr(dist, k, wrap)
+        return self
+
+    def __exit__(self, *exc):
+        for k, fn in self.saved.items():
+            setattr(dist, k, fn)
+
+
 def _worker(rank, world, port, ret):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from oracle import oracle
     ok = True
+    # config 4's gather is ONE collective for equal and for near-equal counts
+    for counts in ([40] * world, [40 + (r % 2) for r in range(world)], [1] + [0] * (world - 1)):
+        out = torch.full((sum(counts), 3), -1, dtype=torch.int64)
+        first = sum(counts[:rank])
+        mine = hdist.rank_rows(out, counts, rank)
+        mine.copy_(torch.arange(first, first + counts[rank])[:, None].expand(counts[rank], 3))
+        with _Count() as c:
+            got = hdist.allgather_coords(mine, counts, out=out)
+        ok &= c.n == 1 and got.data_ptr() == out.data_ptr()
+        ok &= bool(torch.equal(out, torch.arange(sum(counts))[:, None].expand(sum(counts), 3)))
     for n in (301, 64):  # byte-balanced (unequal counts), then an even split
         types, blob, base, lens = synth.make_batch_host("cfg3b", n, seed=42)
         A = len(types)
@@ -76,9 +121,11 @@ def _worker(rank, world, port, ret):
 
         out = torch.full((n, A), -1, dtype=torch.int64)
         mine = hdist.rank_rows(out, counts, rank)
-        full = hdist.hash_sharded(types, blob, torch.from_numpy(base[first:first + cnt].view(np.int64)),
-                                  torch.from_numpy(lens[first * A:(first + cnt) * A].view(np.int32)),
-                                  counts, out=out, hash_fn=oracle_into)
+        with _Count() as c:
+                full = hdist.hash_sharded(types, blob, torch.from_numpy(base[first:first + cnt].view(np.int64)),
+                                      torch.from_numpy(lens[first * A:(first + cnt) * A].view(np.int32)),
+                                      counts, out=out, hash_fn=oracle_into)
+        ok &= c.n == 1
         want, _ = oracle.hash_batch(types, blob, base, lens)
         ok &= full.data_ptr() == out.data_ptr() == mine.data_ptr() - first * A * 8  # in place
         ok &= bool(np.array_equal(full.numpy().view(np.uint64), want))
