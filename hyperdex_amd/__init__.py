@@ -12,9 +12,9 @@ from .datatypes import Attribute, Schema  # noqa: F401
 from .hashing import (hash, hash_batch, hash_batch_host, hash_encoded, hash_encoded_regions, hash_batch_regions,  # noqa: F401
                       hash_key, hash_object, hashable, schema_check)
 from .regions import RegionTable, lookup_region  # noqa: F401
-from .index import index_encode, index_key_size, search_regions  # noqa: F401
+from .index import index_encode, index_key_size, search_regions, search_space  # noqa: F401
 from .batcher import Batcher  # noqa: F401
 
 __all__ = ["HdxError", "Attribute", "Schema", "hash", "hash_key", "hash_object", "hash_batch",
            "hash_batch_host", "hash_encoded", "hash_encoded_regions", "hash_batch_regions", "hashable", "schema_check", "RegionTable",
-           "lookup_region", "index_encode", "index_key_size", "search_regions", "Batcher", "lib"]
+           "lookup_region", "index_encode", "index_key_size", "search_regions", "search_space", "Batcher", "lib"]

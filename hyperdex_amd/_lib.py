@@ -70,6 +70,7 @@ SIGNATURES = [
     ("hdx_index_key_size", ctypes.c_size_t, [_u32]),
     ("hdx_index_encode_device", _i32, [_u32, _vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     ("hdx_search_regions", _i32, [_vp, _vp, _u32, _vp, _vp, _vp]),
+    ("hdx_search_space", _i32, [_vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),
     ("hdx_batcher_create", _i32, [_vp, _u32, _vp, _vp]),
     ("hdx_batcher_destroy", _i32, [_vp]),
     ("hdx_batcher_hash_object", _i32, [_vp, _vp, ctypes.c_size_t, _vp, _vp, _vp, _vp]),

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <vector>
 
 #include "hdx_host.h"
 
@@ -220,5 +221,52 @@ HDX_EXPORT hdx_status hdx_search_regions(hdx_region_table t, const hdx_range* ra
         return HDX_OK;
     }
     std::memcpy(include, g.host + o_incl, t->R);
+    return HDX_OK;
+}
+
+HDX_EXPORT hdx_status hdx_search_space(const hdx_region_table* tables, uint32_t ntables, const hdx_range* ranges,
+                                       uint32_t nranges, const uint8_t* const* has_replicas, int32_t* chosen,
+                                       uint8_t* include, uint32_t* servers, int* cleared) {
+    if (!chosen || !servers || !cleared || (ntables && !tables) || (nranges && !ranges))
+        return fail(HDX_E_INVALID, "NULL pointer");
+    *chosen = -1;
+    *servers = 0;
+    *cleared = 0;
+    uint32_t rmax = 0;
+    for (uint32_t i = 0; i < ntables; ++i) {
+        if (!tables[i]) return fail(HDX_E_INVALID, "table %u is NULL", i);
+        rmax = std::max(rmax, tables[i]->R);
+    }
+    if (rmax && !include) return fail(HDX_E_INVALID, "NULL include");
+    // configuration.cc:771-866: subspaces in order; the first initialises the
+    // choice, a later one replaces it only if its server set is non-empty and
+    // no larger (so the last of equal non-empty sizes wins); a cleared server
+    // list (:766, :811) ends the whole search empty.
+    std::vector<uint8_t> mask(rmax ? rmax : 1);
+    bool initialized = false;
+    uint32_t best = 0;
+    for (uint32_t i = 0; i < ntables; ++i) {
+        int cl = 0;
+        hdx_status st = hdx_search_regions(tables[i], ranges, nranges, has_replicas ? has_replicas[i] : nullptr,
+                                           mask.data(), &cl);
+        if (st != HDX_OK) return st;
+        if (cl) {
+            *chosen = -1;
+            *servers = 0;
+            *cleared = 1;
+            if (rmax) std::memset(include, 0, rmax);
+            return HDX_OK;
+        }
+        uint32_t cnt = 0;
+        for (uint32_t r = 0; r < tables[i]->R; ++r) cnt += mask[r] != 0;
+        if (!initialized || (cnt != 0 && cnt <= best)) {
+            initialized = true;
+            best = cnt;
+            *chosen = (int32_t)i;
+            if (rmax) std::memset(include, 0, rmax);
+            if (tables[i]->R) std::memcpy(include, mask.data(), tables[i]->R);
+        }
+    }
+    *servers = best;
     return HDX_OK;
 }

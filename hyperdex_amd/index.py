@@ -81,3 +81,33 @@ def search_regions(table: RegionTable, ranges: Sequence[tuple],
     check(lib().hdx_search_regions(table.handle, arr, len(ranges), None if rep is None else rep.ctypes.data,
                                    include.ctypes.data, ctypes.byref(cleared)))
     return include[:R], bool(cleared.value)
+
+
+def search_space(tables: Sequence[RegionTable], ranges: Sequence[tuple],
+                 has_replicas=None) -> Tuple[int, np.ndarray, bool]:
+    """configuration::lookup_search over a space's subspaces (tables in the
+    space's order; hdx_search_space).  has_replicas: None or one u8[R] array
+    (or None) per table.  Returns (chosen subspace index or -1, its include
+    mask u8[R], cleared)."""
+    T = len(tables)
+    handles = (ctypes.c_void_p * max(T, 1))(*[t.handle for t in tables])
+    rmax = max([len(t.ids) for t in tables] + [1])
+    include = np.zeros(rmax, np.uint8)
+    reps, keep = None, []
+    if has_replicas is not None:
+        assert len(has_replicas) == T
+        reps = (ctypes.c_void_p * max(T, 1))()
+        for i, r in enumerate(has_replicas):
+            if r is not None:
+                a = np.ascontiguousarray(r, np.uint8)
+                assert a.size == len(tables[i].ids), "has_replicas[%d] must hold one flag per region" % i
+                keep.append(a)
+                reps[i] = a.ctypes.data
+    chosen, servers, cleared = ctypes.c_int32(-1), ctypes.c_uint32(0), ctypes.c_int(0)
+    arr = _ranges(ranges)
+    check(lib().hdx_search_space(handles, T, arr, len(ranges), reps, ctypes.byref(chosen), include.ctypes.data,
+                                 ctypes.byref(servers), ctypes.byref(cleared)))
+    c = chosen.value
+    mask = include[:len(tables[c].ids)] if c >= 0 else include[:0]
+    assert c < 0 or int(mask.sum()) == servers.value
+    return c, mask, bool(cleared.value)

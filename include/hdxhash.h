@@ -262,6 +262,23 @@ typedef struct hdx_range {
 hdx_status hdx_search_regions(hdx_region_table table, const hdx_range* ranges, uint32_t nranges,
                               const uint8_t* has_replicas, uint8_t* include, int* cleared);
 
+/* The whole of configuration::lookup_search (common/configuration.cc:737-868)
+ * over a space's subspaces tables[0..ntables) (in the space's order): each
+ * subspace's server set is its hdx_search_regions include mask (one server per
+ * included region, region.replicas.back(), :853-856); the first subspace
+ * initialises the choice and a later one replaces it only when its set is
+ * non-empty and no larger than the current one (:859-865; so the last of equal
+ * sizes wins, and an empty first subspace is never replaced).  Outputs:
+ * *chosen = the chosen subspace index (-1 when ntables == 0 or cleared),
+ * include[0..max R) = its mask (zero beyond its R), *servers = its set size,
+ * *cleared = 1 when the reference returns an empty list outright (an invalid
+ * range, or an ill-formed box reached in any subspace).  has_replicas may be
+ * NULL, or hold one per-table flag array (entries may be NULL).  Host
+ * pointers; synchronous. */
+hdx_status hdx_search_space(const hdx_region_table* tables, uint32_t ntables, const hdx_range* ranges,
+                            uint32_t nranges, const uint8_t* const* has_replicas, int32_t* chosen,
+                            uint8_t* include, uint32_t* servers, int* cleared);
+
 /* ---- daemon batching shim --------------------------------- */
 
 /* key_state::hash_objects (daemon/key_state.cc:1455-1543) hashes one or two

@@ -530,3 +530,32 @@ int hdxo_search_regions(uint32_t D, uint32_t R, const uint16_t* attrs, const uin
     }
     return 0;
 }
+
+int hdxo_search_space(uint32_t ntables, const uint32_t* D, const uint32_t* R, const uint16_t* const* attrs,
+                      const uint64_t* const* lower, const uint64_t* const* upper,
+                      const uint8_t* const* has_replicas, const hdxo_range* ranges, uint32_t nranges,
+                      uint8_t* include, int* cleared) {
+    int initialized = 0, chosen = -1; /* :771-772 */
+    uint32_t smallest = 0;
+    *cleared = 0;
+    for (uint32_t i = 0; i < ntables; ++i) { /* :774 */
+        uint8_t* mine = (uint8_t*)calloc(R[i] ? R[i] : 1, 1);
+        int rc = hdxo_search_regions(D[i], R[i], attrs[i], lower[i], upper[i],
+                                     has_replicas ? has_replicas[i] : NULL, ranges, nranges, mine);
+        if (rc != 0) { /* servers->clear(); return (:766, :811), or a bad endpoint */
+            free(mine);
+            *cleared = rc == 1;
+            return rc == 1 ? -1 : -2;
+        }
+        uint32_t size = 0; /* one server per included region (:853-856) */
+        for (uint32_t r = 0; r < R[i]; ++r) size += mine[r];
+        if (!initialized || (size != 0 && size <= smallest)) { /* :859-865 */
+            smallest = size;
+            chosen = (int)i;
+            initialized = 1;
+            memcpy(include, mine, R[i]);
+        }
+        free(mine);
+    }
+    return chosen;
+}

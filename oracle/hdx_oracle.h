@@ -101,6 +101,16 @@ int hdxo_search_regions(uint32_t D, uint32_t R, const uint16_t* attrs, const uin
                         const uint64_t* upper, const uint8_t* has_replicas, const hdxo_range* ranges,
                         uint32_t nranges, uint8_t* include);
 
+/* common/configuration.cc:771-868 (lookup_search's choice over subspaces):
+ * subspace i has D[i] attributes attrs[i], R[i] boxes lower[i]/upper[i] and
+ * replica flags has_replicas[i] (may be NULL).  Returns the chosen subspace
+ * (its include mask in include[0..R[chosen])) or -1 (none, or cleared: then
+ * *cleared = 1); -2 on a bad numeric endpoint. */
+int hdxo_search_space(uint32_t ntables, const uint32_t* D, const uint32_t* R, const uint16_t* const* attrs,
+                      const uint64_t* const* lower, const uint64_t* const* upper,
+                      const uint8_t* const* has_replicas, const hdxo_range* ranges, uint32_t nranges,
+                      uint8_t* include, int* cleared);
+
 #ifdef __cplusplus
 }
 #endif

@@ -46,6 +46,8 @@ def lib():
         L.hdxo_hash_encoded.argtypes = [vp, u32, vp, vp, vp, vp, vp, vp, u64, vp, vp, vp]
         L.hdxo_index_encode.restype = sz
         L.hdxo_index_encode.argtypes = [u32, vp, sz, vp, ctypes.POINTER(ctypes.c_int)]
+        L.hdxo_search_space.restype = ctypes.c_int
+        L.hdxo_search_space.argtypes = [u32, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp]
         L.hdxo_search_regions.restype = ctypes.c_int
         L.hdxo_search_regions.argtypes = [u32, u32, vp, vp, vp, vp, vp, u32, vp]
         L.hdxo_hash_encoded.restype = ctypes.c_int64
@@ -193,3 +195,33 @@ def search_regions(attrs, lower, upper, ranges, has_replicas=None):
     if rc < 0:
         raise ValueError("numeric endpoint not 0 or 8 bytes")
     return include[:R], bool(rc)
+
+
+def search_space(subspaces, ranges, has_replicas=None):
+    """lookup_search over subspaces [(attrs, lower, upper), ...] in order ->
+    (chosen index or -1, its include mask, cleared); configuration.cc:771-868."""
+    T = len(subspaces)
+    keep = []
+    D = np.array([len(a) for a, _, _ in subspaces] or [0], np.uint32)
+    R = np.zeros(max(T, 1), np.uint32)
+    P = [(ctypes.c_void_p * max(T, 1))() for _ in range(4)]
+    for i, (a, lo, up) in enumerate(subspaces):
+        a = np.ascontiguousarray(a, np.uint16)
+        lo = np.ascontiguousarray(lo, np.uint64).reshape(-1)
+        up = np.ascontiguousarray(up, np.uint64).reshape(-1)
+        R[i] = lo.size // max(len(a), 1)
+        keep += [a, lo, up]
+        P[0][i], P[1][i], P[2][i] = a.ctypes.data, lo.ctypes.data, up.ctypes.data
+        if has_replicas is not None and has_replicas[i] is not None:
+            r = np.ascontiguousarray(has_replicas[i], np.uint8)
+            keep.append(r)
+            P[3][i] = r.ctypes.data
+    include = np.zeros(max(int(R.max()) if T else 1, 1), np.uint8)
+    cleared = ctypes.c_int(0)
+    arr = make_ranges(ranges)
+    c = lib().hdxo_search_space(T, D.ctypes.data, R.ctypes.data, P[0], P[1], P[2],
+                                None if has_replicas is None else P[3], arr, len(ranges),
+                                include.ctypes.data, ctypes.byref(cleared))
+    if c == -2:
+        raise ValueError("numeric endpoint not 0 or 8 bytes")
+    return c, (include[:R[c]] if c >= 0 else include[:0]), bool(cleared.value)

@@ -214,6 +214,102 @@ def test_oracle_search_random_cases_are_consistent(oracle):
             assert inc[r] == keep
 
 
+# ---- lookup_search's choice over subspaces (configuration.cc:771-868) -----
+
+def _choose(sets):
+    """The reference's rule, restated in Python over per-subspace set sizes:
+    the first initialises; a later one replaces if non-empty and <=."""
+    chosen, best = -1, None
+    for i, n in enumerate(sets):
+        if chosen < 0 or (n != 0 and n <= best):
+            chosen, best = i, n
+    return chosen
+
+
+def _space(oracle, specs):
+    """[(attrs, partitions)] -> [(attrs, lower, upper)] from admin/partition.cc."""
+    out = []
+    for attrs, parts in specs:
+        lo, up = oracle.partition(len(attrs), parts)
+        out.append((list(attrs), lo.copy(), up.copy()))
+    return out
+
+
+def test_oracle_search_space_choice(oracle):
+    i64 = lambda x: struct.pack("<q", x)  # noqa: E731
+    sp = _space(oracle, [([0], 8), ([1], 4), ([2], 4), ([1, 2], 16)])
+    # no range names anything: every subspace keeps all its regions; the
+    # smallest non-empty set wins and the last of equal sizes wins the tie
+    c, inc, cl = oracle.search_space(sp, [])
+    assert (c, int(inc.sum()), cl) == (2, 4, False)
+    # a range on attr 1 narrows subspace 1 (and 3): [2^62..] keeps 2 of 4 regions
+    c, inc, cl = oracle.search_space(sp, [(1, INT64, i64(0), None)])
+    assert c == 1 and list(inc) == [0, 0, 1, 1]
+    # an empty FIRST subspace is never replaced (initialised, later sets are not <= 0)
+    rep = [np.zeros(8, np.uint8), None, None, None]
+    c, inc, cl = oracle.search_space(sp, [], has_replicas=rep)
+    assert c == 0 and not inc.any() and not cl
+    # an empty LATER subspace is never chosen
+    rep = [None, np.zeros(4, np.uint8), None, None]
+    c, inc, cl = oracle.search_space(sp, [], has_replicas=rep)
+    assert c == 2 and inc.sum() == 4
+    # no subspaces at all: nothing chosen, not cleared
+    assert oracle.search_space([], []) [0] == -1
+    # an ill-formed box reached in a LATER subspace clears the whole search
+    sp[3][1][5, 1], sp[3][2][5, 1] = sp[3][2][5, 1], sp[3][1][5, 1]
+    c, inc, cl = oracle.search_space(sp, [(2, INT64, i64(-5), None)])
+    assert c == -1 and cl
+    # an invalid range clears before any subspace
+    c, inc, cl = oracle.search_space(sp[:3], [(0, INT64, i64(0), None, True)])
+    assert c == -1 and cl
+
+
+def _random_space(rng, oracle):
+    T = int(rng.integers(1, 5))
+    specs = [(sorted(rng.choice(8, size=int(rng.integers(1, 4)), replace=False).tolist()),
+              int(rng.choice([2, 4, 8, 64]))) for _ in range(T)]
+    sp = _space(oracle, specs)
+    _, _, _, ranges = _random_search_case(rng, oracle)
+    reps = None
+    if rng.random() < 0.4:
+        reps = [(rng.random(len(lo)) < rng.choice([0.0, 0.5, 1.0])).astype(np.uint8) if rng.random() < 0.7
+                else None for _, lo, _ in sp]
+    if rng.random() < 0.05:
+        k = int(rng.integers(0, T))
+        sp[k][1][0, 0], sp[k][2][0, 0] = sp[k][2][0, 0], sp[k][1][0, 0]
+    return sp, ranges, reps
+
+
+def test_oracle_search_space_random_matches_rule(oracle):
+    rng = np.random.default_rng(21)
+    for _ in range(300):
+        sp, ranges, reps = _random_space(rng, oracle)
+        c, inc, cl = oracle.search_space(sp, ranges, has_replicas=reps)
+        per = [oracle.search_regions(a, lo, up, ranges, has_replicas=None if reps is None else reps[i])
+               for i, (a, lo, up) in enumerate(sp)]
+        if any(x[1] for x in per):
+            assert cl and c == -1
+            continue
+        assert not cl and c == _choose([int(x[0].sum()) for x in per])
+        assert np.array_equal(inc, per[c][0])
+
+
+@pytest.mark.gpu
+def test_gpu_search_space_matches_oracle(oracle):
+    import hyperdex_amd as hdx
+    rng = np.random.default_rng(23)
+    for case in range(150):
+        sp, ranges, reps = _random_space(rng, oracle)
+        want = oracle.search_space(sp, ranges, has_replicas=reps)
+        tables = [hdx.RegionTable(a, lo, up, np.arange(1, len(lo) + 1, dtype=np.uint64)) for a, lo, up in sp]
+        got = hdx.search_space(tables, ranges, has_replicas=reps)
+        for t in tables:
+            t.close()
+        assert got[0] == want[0] and got[2] == want[2], case
+        assert np.array_equal(got[1], want[1]), case
+    assert hdx.search_space([], []) == (-1, hdx.search_space([], [])[1], False)
+
+
 # ---- GPU -----------------------------------------------------------------
 
 def _column(rng, t, n):
