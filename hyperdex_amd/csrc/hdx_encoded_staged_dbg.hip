@@ -1,4 +1,5 @@
-// hdx_encoded_staged.hip — the reindex sweep with each group of stored
+// hdx_encoded_staged_dbg.hip — (debug library only: an A/B experiment)
+// the reindex sweep with each group of stored
 // objects staged in LDS (variants 95-98).
 //
 // Same contract as hash_encoded_kernel (hdx_encoded.hip): every value
@@ -28,13 +29,8 @@
 #include "hdx_lds_hash.h"
 #include "hdx_loads.h"
 
-#ifndef HDX_DEBUG_BUILD
-#define HDX_DEBUG_BUILD 0
-#endif
-
 namespace hdx {
 
-#if HDX_DEBUG_BUILD  // an A/B experiment: not in the product library
 
 namespace {
 
@@ -290,6 +286,5 @@ hipError_t launch_hash_encoded_staged(const EncodedArgs& a, int G, uint32_t WB, 
     }
 }
 
-#endif  // HDX_DEBUG_BUILD
 
 }  // namespace hdx

@@ -60,6 +60,10 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
 // library; libhdxhash_dbg.so (HDX_DEBUG_BUILD) adds a process-wide selection.
 int hash_variant();
 int set_hash_variant(int v);  // debug build only: -2 if unknown, else the previous selection
+// Debug library only (hdx_kernels_dbg.hip): the retired A/B forms of the batch
+// hash and of the fused hash + lookup.
+hipError_t launch_debug_variant(const BatchArgs& args, hipStream_t stream, int variant);
+hipError_t launch_fused_debug(const BatchArgs& args, hipStream_t stream, int variant);
 // The variant launch_hash_batch would run for args, and its kernel's symbol.
 int chosen_variant(const BatchArgs& args);
 const char* variant_kernel_name(int v);

@@ -1,4 +1,5 @@
-// hdx_staged.hip — LDS-staged hashing of packed batches (variants 80-83).
+// hdx_staged_dbg.hip — (debug library only: an A/B experiment)
+// LDS-staged hashing of packed batches (variants 80-83).
 //
 // hdx_hash_batch_device's contract (include/hdxhash.h): coords[i*A + j] =
 // hs[j] of hyperdex::hash(schema, key, value, hs) (common/hash.cc:56-68).
@@ -28,13 +29,8 @@
 #include "hdx_lds_hash.h"
 #include "hdx_loads.h"
 
-#ifndef HDX_DEBUG_BUILD
-#define HDX_DEBUG_BUILD 0
-#endif
-
 namespace hdx {
 
-#if HDX_DEBUG_BUILD  // an A/B experiment: not in the product library
 namespace {
 
 constexpr uint32_t kStagedSlotsMax = 256;  // K * A <= this (descriptor / perm arrays)
@@ -266,6 +262,5 @@ hipError_t launch_hash_staged(const BatchArgs& a, hipStream_t stream, uint32_t s
         default: return launch_staged_nch<4>(args, stream);
     }
 }
-#endif  // HDX_DEBUG_BUILD
 
 }  // namespace hdx

@@ -7,7 +7,7 @@ intervals; a 3-attribute subspace, 4 x 4 x 4 cells).  Every round times, back
 to back: the separate path (hash_batch + one lookup_region per table, the
 automatic kernels), the automatic fused form, and each fused form (debug
 variants 100-111,
-hdx_kernels.hip launch_fused_debug; coordinates not written, as in bench.py's
+hdx_kernels_dbg.hip launch_fused_debug; coordinates not written, as in bench.py's
 fused line).  The first round checks every form's region ids against the
 separate path's.  One JSON line per (config, form): median / min ms.
 """

@@ -54,7 +54,7 @@ def test_product_library_has_no_knobs_or_debug_kernels():
     for knob in (b"HDX_KERNEL_VARIANT", b"HDX_REGION_SCAN", b"HDX_SWEEP_REGION_LDS"):
         assert knob not in raw, knob
     dbg = open(_lib.DEBUG_LIB_PATH, "rb").read()
-    # debug shapes: the chunk kernel with SHAPE 1 / 2 (hdx_kernels.hip)
+    # debug shapes: the chunk kernel with SHAPE 1 / 2 (hdx_regroup.h)
     for shape in (b"hash_chunk_kernelILb1ELb0ELi1ELb0E", b"hash_chunk_kernelILb1ELb0ELi2ELb0E"):
         assert shape not in raw and shape in dbg, shape
 
