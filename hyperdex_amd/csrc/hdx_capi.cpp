@@ -342,8 +342,16 @@ HDX_EXPORT hdx_status hdx_init_mask(uint64_t device_mask) {
 }
 
 HDX_EXPORT hdx_status hdx_shutdown(void) {
-    std::lock_guard<std::mutex> lk(g_scratch_mu);
-    for (Scratch* s : g_scratch) s->release();
+    // each release() binds its scratch's device; the caller's current device
+    // is restored afterwards, so its lazy rebind returns to the same device
+    int dev = -1;
+    const bool had = hipGetDevice(&dev) == hipSuccess;
+    {
+        std::lock_guard<std::mutex> lk(g_scratch_mu);
+        for (Scratch* s : g_scratch) s->release();
+    }
+    if (had && dev >= 0) (void)hipSetDevice(dev);
+    (void)hipGetLastError();
     return HDX_OK;
 }
 

@@ -307,7 +307,8 @@ def test_gpu_search_space_matches_oracle(oracle):
             t.close()
         assert got[0] == want[0] and got[2] == want[2], case
         assert np.array_equal(got[1], want[1]), case
-    assert hdx.search_space([], []) == (-1, hdx.search_space([], [])[1], False)
+    c, inc, cl = hdx.search_space([], [])
+    assert c == -1 and inc.size == 0 and not cl
 
 
 # ---- GPU -----------------------------------------------------------------
