@@ -74,8 +74,9 @@ __global__ void __launch_bounds__(256) k_dma(Args a) {
     const bool valid = s < a.n;
     const uint64_t o = valid ? a.off[s] : a.off[s0];
     const uint32_t L = valid ? a.len[s] : 65u;
-    const uint64_t wbase = __builtin_amdgcn_readfirstlane((uint32_t)a.off[s0]) |
-                           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(a.off[s0] >> 32)) << 32);
+    // (readfirstlane returns int: widen through uint32_t, or offsets >= 2 GiB sign-extend)
+    const uint64_t wbase = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)a.off[s0]) |
+                           ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(a.off[s0] >> 32)) << 32);
     const uint8_t* gb = a.buf + (wbase & ~3ull);
     const uint32_t rel = (uint32_t)(o - (wbase & ~3ull));  // this lane's string, from the wave's dword floor
     const uint32_t nb = (L - 1) >> 6;
