@@ -49,6 +49,9 @@ hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream);
 // LDS-staged hashing of packed batches (hdx_staged.hip): K = slots / A objects
 // per wave, a win_bytes window (multiple of 1 KiB, <= 64 KiB); A <= 64.
 hipError_t launch_hash_staged(const BatchArgs& args, hipStream_t stream, uint32_t slots, uint32_t win_bytes);
+// Wave-staged hash (hdx_wstage.hip): K whole objects per wave copied into an
+// LDS window by DMA and hashed from LDS; form = passes / window size.
+hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int form);
 // hash + lookup_region in one launch (args.T tables in args.t, A <= 128)
 hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream);
 // Fills args.uniform_code from args.codes[0..A), and inv_A / a_magic from A.

@@ -724,6 +724,13 @@ hipError_t launch_debug_variant(const BatchArgs& args, hipStream_t stream, int v
         case 151: return launch_regroup_stride<4, true, false>(args, stream, 8);
         case 152: return launch_regroup_stride<2, true, true, true, true, false, true, 1>(args, stream, 4);
         case 153: return launch_regroup_stride<2, true, true, true, true, false, true, 1>(args, stream, 8);
+        // wave-staged (hdx_wstage.hip): 200 2 passes / 10 KiB, 201 3 / 14 KiB, 202 2 / 8 KiB,
+        // 203 1 / 5 KiB, 204 4 / 18 KiB, 205 2 / 8832 B, 206 = 205 with <= 6 objects
+        case 200: case 201: case 202: case 203: case 204: case 205: case 206: case 207: case 208:
+        case 210: case 211: {
+            const hipError_t e = launch_hash_wstage(args, stream, variant - 200);
+            return e == hipErrorInvalidValue ? launch_hash_batch_variant(args, stream, 44) : e;
+        }
         // debug shapes: WRONG coordinates, debug library only
         case 40: return launch_chunk<true, false, 1>(args, stream);  // loads only
         case 41: return launch_chunk<true, false, 2>(args, stream);  // arithmetic only
@@ -767,6 +774,9 @@ static bool known_variant(int v) {
         case 150: case 151: case 152: case 153: case 154: case 155: case 160: case 161:
         case 170: case 171: case 172: case 173: case 174:  // the sweep's numeric walk (hdx_encoded.hip)
         case 180: case 181: case 182: case 190: case 191:
+        case 200: case 201: case 202: case 203: case 204: case 205: case 206:  // wave-staged (hdx_wstage.hip)
+        case 207: case 208:  // its debug shapes: no hash / no DMA (WRONG coordinates)
+        case 210: case 211:  // wave-staged, sorted over the workgroup
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;

@@ -289,7 +289,36 @@ def test_full_size_sampled(oracle, torch_dev, cfg):
     torch.cuda.empty_cache()
 
 
-VARIANTS = [12, 18, 19, 20, 21, 25, 26, 30, 31, 35, 37, 38, 39, 44, 45, 46, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 80, 81, 82, 83, 84, 85, 86, 90, 140, 141, 142, 143, 144, 145, 146, 147, 150, 151, 152, 153, 154, 155, 160, 161, 180, 181, 182, 190, 191]
+VARIANTS = [12, 18, 19, 20, 21, 25, 26, 30, 31, 35, 37, 38, 39, 44, 45, 46, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 80, 81, 82, 83, 84, 85, 86, 90, 140, 141, 142, 143, 144, 145, 146, 147, 150, 151, 152, 153, 154, 155, 160, 161, 180, 181, 182, 190, 191,
+            200, 201, 202, 203, 204, 205, 206, 210, 211]
+
+
+@pytest.mark.parametrize("variant", [200, 201, 202, 203, 204, 205, 206, 210, 211])
+def test_wave_staged_layouts(oracle, torch_dev, variant):
+    """The wave-staged kernel (hdx_wstage.hip) stages a group's span only when
+    its objects are back to back and fit the window: gaps after some objects
+    (an early DMA that turns out unusable), one oversized object per group,
+    and a batch whose last object ends at the blob's last byte all give the
+    reference's coordinates."""
+    torch, dev = torch_dev
+    rng = np.random.default_rng(variant)
+    with _lib.debug_library(variant):
+        for n in (1, 6, 7, 8, 64, 2001):
+            types, blob, base, lens = synth.make_batch_host("cfg3b", n, seed=n)
+            check_batch(oracle, torch, dev, types, blob, base, lens)
+            # gaps: shift every object after a random cut by a few bytes
+            gap = np.cumsum(rng.integers(0, 2, n) * rng.integers(1, 40, n)).astype(np.uint64)
+            nb = np.zeros(int(base[-1] + gap[-1]) + int(lens.reshape(n, -1)[-1].sum()) + 1, np.uint8)
+            A = len(types)
+            sz = lens.reshape(n, A).astype(np.uint64).sum(axis=1)
+            for i in range(n):
+                nb[int(base[i] + gap[i]):int(base[i] + gap[i] + sz[i])] = blob[int(base[i]):int(base[i] + sz[i])]
+            check_batch(oracle, torch, dev, types, nb[:-1], base + gap, lens)
+        # objects far larger than any window (keys of 200..4000 bytes + attrs)
+        types, blob, base, lens = synth.make_batch_host("keyonly_long", 300, seed=3)
+        check_batch(oracle, torch, dev, types, blob, base, lens)
+        types, blob, base, lens = synth.make_batch_host("mixed", 700, seed=4)
+        check_batch(oracle, torch, dev, types, blob, base, lens)
 
 
 @pytest.mark.parametrize("variant", VARIANTS)

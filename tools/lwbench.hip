@@ -15,7 +15,11 @@
 //          then s_waitcnt vmcnt(0) and 5 ds_read_b128 per lane at an 80-byte
 //          window stride (conflict-free: 5 is odd);
 //   dma2   dma double-buffered: window set t + 1's DMA is issued before set t
-//          is read (vmcnt(5)).
+//          is read (vmcnt(5));
+//   stage  the wave's 64 strings (one contiguous span) copied to LDS by
+//          coalesced DMA, windows read back with ds_read_b32 + v_alignbyte;
+//   stage2 stage over four groups per wave, group g + 1's DMA under group g's
+//          LDS reads (two buffers).
 // Prints one JSON line per (mode, data): GB/s of string bytes.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -139,6 +143,77 @@ __global__ void __launch_bounds__(256) k_dma(Args a) {
     if (valid) a.out[s] = acc;
 }
 
+
+// stage: the wave's 64 consecutive strings are one contiguous span; it is
+// copied into wave-private LDS with coalesced global_load_lds_dwordx4 (1 KiB
+// per instruction, ~8 lines), then each lane reads its windows from LDS with
+// ds_read_b32 + v_alignbyte (17 dwords per window).  GROUPS > 1: the wave
+// takes GROUPS consecutive groups, the next group's DMA in flight while the
+// current one is read (two LDS buffers).
+template <int GROUPS>
+__global__ void __launch_bounds__(256) k_stage(Args a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    constexpr uint32_t WB = 13312;  // per buffer: 64 strings of <= 195 B + alignment (832 units)
+    constexpr uint32_t KI = WB / 1024;  // DMA instructions per group, always all issued
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    uint8_t* win0 = lds + w * (GROUPS > 1 ? 2 : 1) * WB;
+    const uint64_t ngroups = (a.n + 63) / 64;
+    uint64_t g = ((uint64_t)blockIdx.x * 4 + w) * GROUPS;
+    if (g >= ngroups) return;
+    auto span = [&](uint64_t gg, uint64_t& b16, uint32_t& units) {
+        const uint64_t s0 = gg * 64, s1 = min(s0 + 64, a.n) - 1;
+        const uint64_t lo = a.off[s0], hi = a.off[s1] + a.len[s1];
+        b16 = lo & ~15ull;
+        units = (uint32_t)((hi - b16 + 15) >> 4);
+    };
+    auto issue = [&](uint64_t b16, uint32_t units, uint8_t* dst) {
+        const uint8_t* src = a.buf + b16;
+#pragma unroll
+        for (uint32_t i = 0; i < KI; ++i) {  // every lane, every instruction: vmcnt stays countable
+            const uint32_t u = min(i * 64 + (uint32_t)lane, units - 1);
+            __builtin_amdgcn_global_load_lds((const void*)(src + 16ull * u), (lptr)(dst + 1024 * i), 16, 0, 0);
+        }
+    };
+    auto fold = [&](const uint8_t* win, uint32_t o) -> uint32_t {
+        uint32_t x = 0;
+        const __attribute__((address_space(3))) uint32_t* d = (const __attribute__((address_space(3))) uint32_t*)(win + (o & ~3u));
+        uint32_t prev = d[0];
+#pragma unroll
+        for (int k = 1; k <= 16; ++k) {
+            const uint32_t cur = d[k];
+            x ^= __builtin_amdgcn_alignbyte(cur, prev, o & 3);
+            prev = cur;
+        }
+        return x;
+    };
+    uint64_t b16, nb16 = 0;
+    uint32_t units, nunits = 0;
+    span(g, b16, units);
+    issue(b16, units, win0);
+    for (int t = 0; t < GROUPS && g < ngroups; ++t, ++g) {
+        uint8_t* cur = win0 + (t & 1) * WB;
+        const uint64_t s = g * 64 + lane;
+        const bool valid = s < a.n;
+        const uint64_t so = valid ? a.off[s] : 0;
+        const uint32_t L = valid ? a.len[s] : 65u;
+        const bool more = GROUPS > 1 && t + 1 < GROUPS && g + 1 < ngroups;
+        if (more) span(g + 1, nb16, nunits);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this group's DMA (issued a group ago) + metadata
+        if (more) issue(nb16, nunits, win0 + ((t + 1) & 1) * WB);
+        if (valid) {
+            const uint32_t o = (uint32_t)(so - b16);
+            uint32_t acc = fold(cur, o + L - 64);
+            const uint32_t nb = (L - 1) >> 6;
+            for (uint32_t bb = 0; bb < nb; ++bb) acc += fold(cur, o + 64 * bb);
+            a.out[s] = acc;
+        }
+        __builtin_amdgcn_wave_barrier();
+        b16 = nb16;
+        units = nunits;
+    }
+}
+
 static double time_kernel(void (*launch)(const Args&), const Args& a, int reps = 5) {
     launch(a);
     CK(hipDeviceSynchronize());
@@ -157,6 +232,10 @@ static double time_kernel(void (*launch)(const Args&), const Args& a, int reps =
 static uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + 255) / 256); }
 static void launch_lane(const Args& a) { hipLaunchKernelGGL(k_lane, dim3(blocks_for(a.n)), dim3(256), 0, 0, a); }
 static void launch_dma(const Args& a) { hipLaunchKernelGGL(k_dma<false>, dim3(blocks_for(a.n)), dim3(256), 4 * 5120, 0, a); }
+static void launch_stage(const Args& a) { hipLaunchKernelGGL(k_stage<1>, dim3(blocks_for(a.n)), dim3(256), 4 * 13312 + 64, 0, a); }
+static void launch_stage2(const Args& a) {
+    hipLaunchKernelGGL(k_stage<4>, dim3((uint32_t)(((a.n + 63) / 64 + 15) / 16)), dim3(256), 8 * 13312 + 64, 0, a);
+}
 static void launch_dma2(const Args& a) { hipLaunchKernelGGL(k_dma<true>, dim3(blocks_for(a.n)), dim3(256), 8 * 5120, 0, a); }
 
 int main(int argc, char** argv) {
@@ -186,7 +265,8 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(dlen, len.data(), n * 4, hipMemcpyHostToDevice));
         Args a{buf, doff, dlen, n, out};
         struct M { const char* name; void (*fn)(const Args&); };
-        for (M m : {M{"lane", launch_lane}, M{"dma", launch_dma}, M{"dma2", launch_dma2}, M{"lane", launch_lane}}) {
+        for (M m : {M{"lane", launch_lane}, M{"dma", launch_dma}, M{"dma2", launch_dma2}, M{"stage", launch_stage},
+                    M{"stage2", launch_stage2}, M{"lane", launch_lane}}) {
             const double ms = time_kernel(m.fn, a);
             printf("{\"tool\": \"lwbench\", \"mode\": \"%s\", \"data\": \"%s\", \"strings\": %llu, \"bytes\": %llu, "
                    "\"ms\": %.4f, \"GBps\": %.1f, \"GBps_incl_meta\": %.1f}\n",
