@@ -52,6 +52,10 @@ hipError_t launch_hash_staged(const BatchArgs& args, hipStream_t stream, uint32_
 // Wave-staged hash (hdx_wstage.hip): K whole objects per wave copied into an
 // LDS window by DMA and hashed from LDS; form = passes / window size.
 hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int form);
+// Streamed hash (hdx_stream.hip): one persistent workgroup per CU walks its
+// objects in batches staged in LDS by DMA a batch ahead, slots class-sorted
+// over the workgroup; A <= 64 (else hipErrorInvalidValue).
+hipError_t launch_hash_stream(const BatchArgs& args, hipStream_t stream, int form);
 // hash + lookup_region in one launch (args.T tables in args.t, A <= 128)
 hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream);
 // Fills args.uniform_code from args.codes[0..A), and inv_A / a_magic from A.

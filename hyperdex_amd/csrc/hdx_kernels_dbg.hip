@@ -727,8 +727,13 @@ hipError_t launch_debug_variant(const BatchArgs& args, hipStream_t stream, int v
         // wave-staged (hdx_wstage.hip): 200 2 passes / 10 KiB, 201 3 / 14 KiB, 202 2 / 8 KiB,
         // 203 1 / 5 KiB, 204 4 / 18 KiB, 205 2 / 8832 B, 206 = 205 with <= 6 objects
         case 200: case 201: case 202: case 203: case 204: case 205: case 206: case 207: case 208:
-        case 210: case 211: {
+        case 209: case 210: case 211: {
             const hipError_t e = launch_hash_wstage(args, stream, variant - 200);
+            return e == hipErrorInvalidValue ? launch_hash_batch_variant(args, stream, 44) : e;
+        }
+        // streamed (hdx_stream.hip): 220 16 waves / 2 x 63 KiB, 221 8 waves / 2 x 31 KiB, 222 16 / 2 x 60 KiB
+        case 220: case 221: case 222: {
+            const hipError_t e = launch_hash_stream(args, stream, variant - 220);
             return e == hipErrorInvalidValue ? launch_hash_batch_variant(args, stream, 44) : e;
         }
         // debug shapes: WRONG coordinates, debug library only
@@ -776,6 +781,8 @@ static bool known_variant(int v) {
         case 180: case 181: case 182: case 190: case 191:
         case 200: case 201: case 202: case 203: case 204: case 205: case 206:  // wave-staged (hdx_wstage.hip)
         case 207: case 208:  // its debug shapes: no hash / no DMA (WRONG coordinates)
+        case 209:  // <= 3 objects per wave (per-regime VALU on uniform batches)
+        case 220: case 221: case 222:  // streamed (hdx_stream.hip)
         case 210: case 211:  // wave-staged, sorted over the workgroup
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)

@@ -395,6 +395,7 @@ hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int for
         case 6: return launch_wstage_t<2, 8832, 6>(args, stream);
         case 7: return launch_wstage_t<2, 8832, 63, 1>(args, stream);  // debug shape: no hash
         case 8: return launch_wstage_t<2, 8832, 63, 2>(args, stream);  // debug shape: no DMA
+        case 9: return launch_wstage_t<2, 8832, 3>(args, stream);  // <= 3 objects: per-regime costs on uniform batches
         // the slots class-sorted over the workgroup
         case 10: return launch_wgstage_t<2, 8832>(args, stream);
         case 11: return launch_wgstage_t<1, 4352>(args, stream);
