@@ -70,9 +70,9 @@ static bool sweep_region_lds() {
 #endif
 }
 // Wave-private LDS: G object bases {value, key}, the code table, the pass
-// attribute list (numeric walk), descriptors.
-__host__ __device__ constexpr size_t encoded_lds_per_wave(uint32_t A, uint32_t G = 64) {
-    return G * 16 + 512 + (size_t)G * A * sizeof(EncDesc);
+// attribute list (numeric walk only), descriptors.
+__host__ __device__ constexpr size_t encoded_lds_per_wave(uint32_t A, uint32_t G = 64, bool NW = false) {
+    return G * 16 + 256 + (NW ? 256 : 0) + (size_t)G * A * sizeof(EncDesc);
 }
 
 // G objects per wave (lanes G..63 idle in phase 1).  SHAPE (debug variants
@@ -112,11 +112,11 @@ hash_encoded_kernel(const EncodedArgs a) {
         __syncthreads();  // the kernel's only workgroup barrier (before any wave may exit)
     }
     // wave-private LDS: G object bases {value, key}, the code table, descriptors
-    uint8_t* wsmem = smem_raw + (REGIONS ? (size_t)a.lds_tables * 8 : 0) + (size_t)w * encoded_lds_per_wave(A, G);
+    uint8_t* wsmem = smem_raw + (REGIONS ? (size_t)a.lds_tables * 8 : 0) + (size_t)w * encoded_lds_per_wave(A, G, NW);
     uint64_t* bases = reinterpret_cast<uint64_t*>(wsmem);           // [G][2]
     uint8_t* codes = wsmem + G * 16;                                 // [256]
-    uint8_t* p2 = wsmem + G * 16 + 256;                              // [256]
-    EncDesc* desc = reinterpret_cast<EncDesc*>(wsmem + G * 16 + 512);
+    uint8_t* p2 = wsmem + G * 16 + 256;                              // [256] (NW only)
+    EncDesc* desc = reinterpret_cast<EncDesc*>(wsmem + G * 16 + 256 + (NW ? 256 : 0));
     bool bad = false;
     const uint64_t o0 = ((uint64_t)blockIdx.x * (blockDim.x >> 6) + w) * G;
     if (o0 >= a.n) return;  // no barrier after this point: waves are independent
@@ -345,9 +345,16 @@ hash_encoded_kernel(const EncodedArgs a) {
 }
 
 template <bool TOUCH, bool A4, int SHAPE = 0, int G = 64, bool REGIONS = false, bool NW = false, bool SPEC = false>
-static hipError_t launch_encoded(const EncodedArgs& a, hipStream_t stream) {
-    // 4 waves per workgroup while they fit in 64 KiB of LDS (A <= 28 at G = 64), else 1
-    const size_t per_wave = encoded_lds_per_wave(a.A, G);
+static hipError_t launch_encoded(const EncodedArgs& a_in, hipStream_t stream) {
+    EncodedArgs a = a_in;
+    if constexpr (NW) {  // the attributes left to the hash passes: the key and every string
+        a.S = 0;
+        for (uint32_t j = 0; j < a.A; ++j)
+            if (j == 0 || a.codes[j] == CODE_STRING) a.p2[a.S++] = (uint8_t)j;
+        a.s_magic = (uint32_t)(((1ull << 31) + a.S - 1) / a.S);
+    }
+    // 4 waves per workgroup while they fit in 64 KiB of LDS (A <= 61 at G = 32), else 1
+    const size_t per_wave = encoded_lds_per_wave(a.A, G, NW);
     const uint32_t waves_per_block = 4 * per_wave <= 65536 ? 4 : 1;
     const uint64_t waves = (a.n + G - 1) / G;
     uint64_t blocks = (waves + waves_per_block - 1) / waves_per_block;
@@ -361,10 +368,6 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
     if (a_in.n == 0) return hipSuccess;
     EncodedArgs a = a_in;
     a.a_magic = (uint32_t)(((1ull << 31) + a.A - 1) / a.A);
-    a.S = 0;
-    for (uint32_t j = 0; j < a.A; ++j)
-        if (j == 0 || a.codes[j] == CODE_STRING) a.p2[a.S++] = (uint8_t)j;
-    a.s_magic = (uint32_t)(((1ull << 31) + a.S - 1) / a.S);
     // default: dword-aligned loads (5.49 vs 6.14 ms per 10 M config-3b objects,
     // profiles/r1/ab_a4_cfg5.jsonl), 32 objects per wave (5.05 vs 5.31 ms for
     // 64 (variant 47) and 5.88 for 16 (48), ab_cfg5_objects_per_wave.jsonl);

@@ -732,7 +732,7 @@ hipError_t launch_debug_variant(const BatchArgs& args, hipStream_t stream, int v
             return e == hipErrorInvalidValue ? launch_hash_batch_variant(args, stream, 44) : e;
         }
         // streamed (hdx_stream.hip): 220 16 waves / 2 x 63 KiB, 221 8 waves / 2 x 31 KiB, 222 16 / 2 x 60 KiB
-        case 220: case 221: case 222: {
+        case 220: case 221: case 222: case 223: case 224: case 225: {
             const hipError_t e = launch_hash_stream(args, stream, variant - 220);
             return e == hipErrorInvalidValue ? launch_hash_batch_variant(args, stream, 44) : e;
         }
@@ -783,6 +783,7 @@ static bool known_variant(int v) {
         case 207: case 208:  // its debug shapes: no hash / no DMA (WRONG coordinates)
         case 209:  // <= 3 objects per wave (per-regime VALU on uniform batches)
         case 220: case 221: case 222:  // streamed (hdx_stream.hip)
+        case 223: case 224: case 225:  // its debug shapes (WRONG coordinates)
         case 210: case 211:  // wave-staged, sorted over the workgroup
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)

@@ -39,11 +39,12 @@
 //
 // Synchronisation per batch b: three workgroup barriers — B1 (per-wave slot
 // counts per class, the next batch's size), B2 (sorted descriptors written),
-// B3 (coordinates parked).  The DMA of batch b+1 is
-// issued after B1 of batch b and waited for with s_waitcnt vmcnt(1) at the top
-// of batch b+1 (the only younger VMEM operation a wave may still have in
-// flight there is its coordinate store of batch b: loads, stores and LDS DMA
-// complete in issue order, MI355X_MICROARCH.md), before B1 publishes it.
+// B3 (coordinates parked, the next batch's copies landed).  Everything the
+// next batch needs — its span, its slot lengths, the object bases after it —
+// arrives by LDS DMA issued after B1 of batch b, so no register waits on it;
+// each wave drains its own copies (s_waitcnt vmcnt(0)) just before B3.
+// Batch b's coordinates are stored from LDS early in batch b+1, so that drain
+// never waits for a fresh store.
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -60,7 +61,7 @@ typedef __attribute__((address_space(3))) void* lds_void_t;
 
 constexpr uint32_t kInvalid = 0xffffffffu;
 constexpr uint32_t kFront = 32;   // window bytes before the span (tail reads of short strings)
-constexpr uint32_t kBack = 128;   // after it (head reads of short strings, dword over-reads)
+constexpr uint32_t kBack = 256;  // after it (head reads of short strings; the 64-lane tail copy)
 constexpr uint32_t kLenBits = 17, kLenMax = (1u << kLenBits) - 1;
 
 // Sort classes, most expensive first: > 64-byte strings by loop blocks (4+,
@@ -160,132 +161,205 @@ __device__ __forceinline__ uint64_t hash_slot_global(const uint8_t* p, uint32_t 
     return hash_blk<false, false, true>(code, p, n, consume_any<true>(issue_any<true>(code, p, n)), bad);
 }
 
+// Batch x's buffers: span window x % 3, lengths x % 3, bases x % 4 (the bases
+// are copied a batch earlier than the span, whose bounds they give).
 template <int WAVES, uint32_t W>
 struct StreamLds {
-    static constexpr uint32_t S = 64 * WAVES;            // slots per batch at most
-    uint8_t win[2][kFront + W + kBack] __attribute__((aligned(16)));
-    uint64_t sdesc[S];        // class-sorted {offset, slot | code | staged | len}; then the coordinate
-    uint32_t bdelta[2][S];    // per batch parity: base[o0 + t] - base[o0], or kInvalid
-    uint32_t wcls[WAVES][kStreamClasses];  // per wave: slots per class
-    uint32_t kfirst[2];       // per batch parity: the first object that does not fit (atomic min)
+    static constexpr uint32_t S = 64 * WAVES;  // slots per batch at most
+    uint8_t win[3][kFront + W + kBack] __attribute__((aligned(16)));
+    uint32_t lens[3][S];             // slot lengths (LDS DMA; past the batch: garbage)
+    uint32_t bases[4][S];            // object bases o0 .. o0 + S/2 - 1, u64 as dword pairs (LDS DMA)
+    uint64_t sdesc[S];               // class-sorted {offset, slot | code | staged | len}; then the coordinate
+    uint32_t cnt[2][16];             // per batch parity: slots per class (LDS atomics)
+    uint32_t lastpos[2];             // per batch parity: the sorted position of the batch's last slot
+    uint32_t dummy[64];              // the tail copy of waves that have no tail
     uint8_t codes[64];
 };
 
+// A workgroup barrier for LDS traffic only: this wave's LDS reads and writes
+// are complete, then s_barrier.  __syncthreads()' workgroup-scope release
+// fence would also wait for every LDS DMA in flight.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+// s_waitcnt vmcnt(N) (expcnt / lgkmcnt untouched) as the builtin, so that the
+// compiler's wait tracking sees it; N is an immediate, hence the switch.
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0x0f70 | (N & 15) | ((N >> 4) << 14));
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+__device__ __forceinline__ void vm_wait_le(uint32_t n) {
+    switch (n) {
+        case 0: vm_wait<0>(); break;   case 1: vm_wait<1>(); break;   case 2: vm_wait<2>(); break;
+        case 3: vm_wait<3>(); break;   case 4: vm_wait<4>(); break;   case 5: vm_wait<5>(); break;
+        case 6: vm_wait<6>(); break;   case 7: vm_wait<7>(); break;   case 8: vm_wait<8>(); break;
+        case 9: vm_wait<9>(); break;   case 10: vm_wait<10>(); break; case 11: vm_wait<11>(); break;
+        case 12: vm_wait<12>(); break; case 13: vm_wait<13>(); break; case 14: vm_wait<14>(); break;
+        case 15: vm_wait<15>(); break; case 16: vm_wait<16>(); break; case 17: vm_wait<17>(); break;
+        case 18: vm_wait<18>(); break; case 19: vm_wait<19>(); break; case 20: vm_wait<20>(); break;
+        case 21: vm_wait<21>(); break; case 22: vm_wait<22>(); break; case 23: vm_wait<23>(); break;
+        default: vm_wait<24>(); break;
+    }
+}
+// LDS DMA (global_load_lds_dwordx4 / _dword: this lane's 16 / 4 bytes at src
+// to dst + 16 * lane / 4 * lane; dst wave-uniform, through M0) issued from
+// inline assembly: the compiler then neither counts it nor — unable to tell
+// the buffers apart — waits for it before every later LDS read (it would
+// drain the next batches' copies before hashing this one).  Every lane
+// issues (sources clamped to valid bytes), so a wave's count of copies per
+// batch is fixed and the kernel waits for its own with counted vm_wait_le.
+__device__ __forceinline__ void dma_x4(const void* src, const void* dst) {
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t)dst);
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+}
+__device__ __forceinline__ void dma_x1(const void* src, const void* dst) {
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t)dst);
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+}
+
 }  // namespace
 
-// One batch's uniform description (every wave holds a copy in SGPRs).
-struct StreamBatch {
-    uint64_t o0;     // first object
-    uint64_t base0;  // its base
-    uint32_t K;      // objects
-    uint32_t span;   // base[o0 + K] - base0 (the bytes the window holds), or kInvalid
-    uint32_t lead;   // (blob + base0) & 15: the span's offset in its first DMA unit
-};
-
-template <int WAVES, uint32_t W>
+// SHAPE (debug variants only, WRONG coordinates): bit 0 = no hashing (each
+// slot's descriptor is stored), bit 1 = no copy of the span (the window is
+// hashed as it is).
+template <int WAVES, uint32_t W, int SHAPE = 0>
 __global__ void __launch_bounds__(64 * WAVES)
 hash_stream_kernel(const BatchArgs args) {
     typedef StreamLds<WAVES, W> L;
     constexpr uint32_t S_MAX = L::S;
+    constexpr uint32_t NI = W / 1024;  // span copy instructions per batch
+    static_assert(W % 1024 == 0, "whole 1 KiB copy instructions");
     __shared__ L lds;
     const uint32_t tid = threadIdx.x;
     const int lane = tid & 63;
     const uint32_t w = tid >> 6;
     const uint32_t A = args.A;  // 1..64
     const uint64_t n = args.n;
-    const uint32_t kcap = std::min<uint32_t>(S_MAX / A, S_MAX - 1);  // objects per batch at most (lane kcap: its end)
+    // this wave's copies per batch: span instructions + tail + lengths; and one for its bases
+    const uint32_t per_span = (NI + WAVES - 1 - w) / WAVES + 2;
 
-    // this workgroup's objects
+    // this workgroup's objects, in batches of K (fixed, so that every batch's
+    // start is known ahead and the copies run two batches ahead)
     const uint64_t G = gridDim.x;
     const uint64_t r0 = n * blockIdx.x / G, r1 = n * (blockIdx.x + 1) / G;
     if (r0 >= r1) return;  // (uniform: no barrier reached)
+    // K from the range's mean object size: ~90 % of a window per batch
+    const uint32_t kcap = std::min<uint32_t>(S_MAX / A, S_MAX / 2 - 1);  // K + 1 bases per buffer
+    uint32_t K = kcap;
+    {
+        const uint64_t re = r1 < n ? r1 : n - 1;
+        const uint64_t b0 = args.obj_base[r0], b1 = args.obj_base[re];
+        if (re > r0 && b1 > b0) {
+            const uint64_t mean = (b1 - b0) / (re - r0);
+            const uint64_t k = mean ? (uint64_t)(W * 9 / 10) / mean : kcap;
+            K = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(k, kcap));
+        }
+    }
+    const uint32_t nbatch = (uint32_t)((r1 - r0 + K - 1) / K);
 
     if (tid < 64) lds.codes[tid] = tid < A ? args.codes[tid] : (uint8_t)CODE_ZERO;
-    if (tid < 2) lds.kfirst[tid] = kInvalid;
-    __syncthreads();
+    if (tid < 32) (&lds.cnt[0][0])[tid] = 0;
 
-    // ---- the next batch's size from its bases (lane t: base[o1 + t]) --------
-    // fit(t): object o1 + t starts inside the window when the batch starts at
-    // o1, i.e. the batch may end before it; the batch is the objects before
-    // the first t >= 1 that does not fit.
-    auto size_next = [&](uint64_t o1, uint64_t bt, uint32_t par) {
-        const uint64_t b0 = args.obj_base[o1];  // wave-uniform: a scalar load
-        const uint32_t lead = (uint32_t)((uintptr_t)(args.blob + b0) & 15);
-        const uint64_t kmax = std::min<uint64_t>(kcap, r1 - o1);
-        const bool in = tid <= kmax;
-        const bool fit = in && o1 + tid < n && bt >= b0 && bt - b0 + lead <= W;
-        const uint64_t nf = __ballot(tid >= 1 && in && !fit);
-        if (nf != 0 && lane == 0) atomicMin(&lds.kfirst[par], w * 64 + (uint32_t)__builtin_ctzll(nf));
-        if (in) lds.bdelta[par][tid] = fit ? (uint32_t)(bt - b0) : kInvalid;
+    auto batch_o0 = [&](uint32_t x) { return r0 + (uint64_t)x * K; };
+    auto batch_k = [&](uint32_t x) { return (uint32_t)std::min<uint64_t>(K, r1 - batch_o0(x)); };
+    auto base_at = [&](uint32_t x, uint32_t i) { return pack64(lds.bases[x & 3][2 * i], lds.bases[x & 3][2 * i + 1]); };
+    // the span of batch x held in its window: bytes from its first 16-byte
+    // unit (0 for the launch's last batch, whose end is unknown: hashed from
+    // global memory)
+    auto held_bytes = [&](uint32_t x, uint64_t& b0, uint32_t& lead) {
+        const uint64_t o0 = batch_o0(x);
+        const uint32_t k = batch_k(x);
+        b0 = base_at(x, 0);
+        lead = (uint32_t)((uintptr_t)(args.blob + b0) & 15);
+        if (o0 + k >= n) return 0u;
+        const uint64_t be = base_at(x, k);
+        return be > b0 ? (uint32_t)std::min<uint64_t>(lead + (be - b0), W) : 0u;
     };
-    auto read_next = [&](uint64_t o1, uint32_t par) {
-        StreamBatch nb;
-        nb.o0 = o1;
-        nb.base0 = args.obj_base[o1];
-        nb.lead = (uint32_t)((uintptr_t)(args.blob + nb.base0) & 15);
-        const uint64_t kmax = std::min<uint64_t>(kcap, r1 - o1);
-        const uint32_t kf = std::min<uint64_t>(lds.kfirst[par], kmax + 1);
-        nb.K = kf >= 2 ? kf - 1 : 1u;
-        nb.span = kf >= 2 ? lds.bdelta[par][nb.K] : kInvalid;
-        return nb;
+    // batch x's bases: 1 copy per wave (64 dwords each, 512 bases)
+    auto issue_bases = [&](uint32_t x) {
+        dma_x1((const uint32_t*)args.obj_base + std::min<uint64_t>(2 * batch_o0(x) + tid, 2 * n - 1),
+               lds.bases[x & 3] + 64 * w);
     };
-    // the DMA of a batch's span into window par; its lengths (lane t: slot t,
-    // and slot t - 64 for the carry of an object straddling two waves) and
-    // the bases after it — unconditional, clamped loads: they must be a
-    // wave's youngest VMEM operations but for its coordinate store
-    auto issue_next = [&](const StreamBatch& nb, uint32_t par, uint32_t& lnext, uint32_t& pnext, uint64_t& bnext) {
-        if (nb.span != kInvalid) {
-            const uint8_t* s16 = args.blob + nb.base0 - nb.lead;
-            const uint32_t units = (nb.lead + nb.span + 15) >> 4;
-            for (uint32_t k = w; k * 64 < units; k += WAVES) {
-                const uint32_t u = k * 64 + lane;
-                if (u < units)
-                    __builtin_amdgcn_global_load_lds((const void*)(s16 + 16ull * u),
-                                                     (lds_void_t)(lds.win[par] + kFront + 1024 * k), 16, 0, 0);
-            }
+    // batch x's span and lengths: per_span copies per wave (every lane issues,
+    // sources clamped), its bases already in LDS
+    auto issue_span = [&](uint32_t x) {
+        const uint32_t buf = x % 3;
+        uint64_t b0;
+        uint32_t lead;
+        const uint32_t bytes = held_bytes(x, b0, lead);
+        const uint8_t* s16 = args.blob + b0 - lead;
+        const uint32_t units = SHAPE & 2 ? 1u : bytes >> 4;
+        for (uint32_t i = w; i < NI; i += WAVES) {
+            const uint32_t u = std::min<uint32_t>(i * 64 + lane, units ? units - 1 : 0);
+            dma_x4(s16 + 16ull * u, lds.win[buf] + kFront + 1024 * i);
         }
-        const uint64_t q = std::min<uint64_t>(nb.o0 * A + tid, n * A - 1);
-        lnext = args.attr_len[q];
-        pnext = args.attr_len[q >= 64 ? q - 64 : 0];
-        const uint64_t o2 = nb.o0 + nb.K;
-        bnext = args.obj_base[std::min<uint64_t>(o2 + tid, n - 1)];
+        // the last partial unit as dwords (a dword never crosses a page)
+        const uint32_t tdw = ((bytes & 15) + 3) >> 2;
+        const bool tail = w == WAVES - 1 && tdw != 0 && !(SHAPE & 2);
+        dma_x1(tail ? (const void*)(s16 + 16ull * units + 4 * std::min<uint32_t>(lane, tdw - 1)) : (const void*)args.attr_len,
+               tail ? (const void*)(lds.win[buf] + kFront + 16 * units) : (const void*)lds.dummy);
+        dma_x1(args.attr_len + std::min<uint64_t>(batch_o0(x) * A + tid, n * A - 1), lds.lens[buf] + 64 * w);
     };
 
-    // ---- prologue: batch 0's size, DMA, lengths; batch 1's bases ------------
-    uint64_t bn = args.obj_base[std::min<uint64_t>(r0 + tid, n - 1)];
-    size_next(r0, bn, 0);
-    __syncthreads();
-    StreamBatch cur = read_next(r0, 0);
-    uint32_t lc = 0, lp = 0;
-    issue_next(cur, 0, lc, lp, bn);
+    // prologue: bases 0, 1; then span 0, bases 2, span 1
+    issue_bases(0);
+    if (1 < nbatch) issue_bases(1);
+    vm_wait<0>();
+    lds_barrier();
+    issue_span(0);
+    if (2 < nbatch) issue_bases(2);
+    if (1 < nbatch) issue_span(1);
+    vm_wait_le(1 < nbatch ? per_span : 0u);
+    lds_barrier();
+
     bool bad = false;
+    uint64_t prev_o0 = 0;
+    uint32_t prev_S = 0, prev_pos = 0;
+    for (uint32_t b = 0; b < nbatch; ++b) {
+        // here: batch b's span and lengths, and the bases of batches <= b + 2, are in LDS
+        const uint32_t buf = b % 3, par = b & 1;
+        const uint64_t o0 = batch_o0(b);
+        const uint32_t k = batch_k(b);
+        const uint32_t S = k * A;
+        // copies: batch b+3's bases, then batch b+2's span and lengths
+        if (b + 3 < nbatch) issue_bases(b + 3);
+        const bool span2 = b + 2 < nbatch;
+        if (span2) issue_span(b + 2);
+        // batch b-1's coordinates, parked in sdesc, in slot order (every lane
+        // stores — slot min(t, S - 1) — so that the store is always issued)
+        if (prev_S) {
+            const uint32_t t = std::min<uint32_t>(tid, prev_S - 1);
+            const uint32_t pp = tid < prev_S ? prev_pos : lds.lastpos[par ^ 1];
+            __builtin_nontemporal_store(lds.sdesc[pp], args.coords + prev_o0 * A + t);
+        }
+        const uint32_t stores = prev_S ? 1u : 0u;
 
-    for (uint32_t b = 0;; ++b) {
-        const uint32_t par = b & 1;
-        const uint32_t S = cur.K * A;
-        const uint64_t o1 = cur.o0 + cur.K;
-        const bool more = o1 < r1;
-        // batch b's DMA, its lengths and batch b+1's bases have landed
-        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-        // (A) batch b+1's size (lane t holds base[o1 + t])
-        if (more) size_next(o1, bn, par ^ 1);
-
-        // (B) describe batch b: slot t = tid
+        // describe batch b: slot t = tid
         const bool valid = tid < S;
-        const uint32_t len = valid ? lc : 0u;
+        uint64_t base0;
+        uint32_t lead;
+        const uint32_t held = SHAPE & 2 ? W : held_bytes(b, base0, lead);
+        if (SHAPE & 2) {
+            base0 = base_at(b, 0);
+            lead = (uint32_t)((uintptr_t)(args.blob + base0) & 15);
+        }
+        const uint32_t len = valid ? lds.lens[buf][tid] : 0u;
         const uint32_t orel = div_small(tid, args.a_magic);  // object within the batch
         const uint32_t j = tid - orel * A;
         const uint32_t code = valid ? (uint32_t)lds.codes[j] : (uint32_t)CODE_ZERO;
         const uint32_t xex = wave_scan_dpp(len) - len;
         // in-object offset: from this wave's head of the object, or — an
         // object straddling two waves (A <= 64) — the previous wave's slots
-        // from its last head on (lp = length of slot t - 64)
+        // from its last head on
         const int head = lane - (int)j;
         uint32_t inoff;
         if (w == 0) {
             inoff = xex - __shfl(xex, head, 64);
         } else {
             const uint32_t sp = tid - 64;
+            const uint32_t lp = sp < S ? lds.lens[buf][sp] : 0u;
             const uint32_t jp = sp - div_small(sp, args.a_magic) * A;
             const uint64_t heads = __ballot(jp == 0);  // a wave always holds a head (A <= 64)
             const int lasth = 63 - __builtin_clzll(heads);
@@ -294,93 +368,79 @@ hash_stream_kernel(const BatchArgs args) {
                                    (__builtin_amdgcn_readlane(pin, lasth) - __builtin_amdgcn_readlane(lp, lasth));
             inoff = head >= 0 ? xex - __shfl(xex, head, 64) : xex + carry;
         }
-        // staged: the slot's bytes lie inside the batch's window
-        const uint32_t od = lds.bdelta[par][orel];
-        const bool staged = valid && cur.span != kInvalid && od != kInvalid && od + inoff + len <= cur.span;
+        // staged: the slot's bytes lie inside the held part of the window
+        const uint64_t ob = base_at(b, orel < k ? orel : 0);
+        const uint64_t wo = ob - base0 + lead;  // the object's offset in the window (when ob >= base0)
+        const bool staged = valid && ob >= base0 && wo + inoff + len <= held;
         const uint32_t cls = valid ? stream_class(code, len, staged) : kStreamClasses;
         uint32_t rank = 0, mycnt = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < kStreamClasses; ++k) {
-            const uint64_t m = __ballot(cls == k);
-            if (cls == k) rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            if (lane == (int)k) mycnt = (uint32_t)__popcll(m);
+        for (uint32_t c = 0; c < kStreamClasses; ++c) {
+            const uint64_t m = __ballot(cls == c);
+            if (cls == c) rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (lane == (int)c) mycnt = (uint32_t)__popcll(m);
         }
-        if (lane < (int)kStreamClasses) lds.wcls[w][lane] = mycnt;
-        __syncthreads();  // ---------------------------------------------- B1 (class counts, next batch's size)
+        // this wave's slots of class c go after those of the waves that got there first
+        uint32_t before = 0;
+        if (lane < (int)kStreamClasses && mycnt) before = atomicAdd(&lds.cnt[par][lane], mycnt);
+        lds_barrier();  // ------------------------------------------------- B1 (class counts)
 
-        // (C) batch b+1: its size, the DMA of its span, its lengths, batch
-        // b+2's bases
-        StreamBatch nxt{};
-        uint32_t lnext = 0, pnext = 0;
-        uint64_t bnext = 0;
-        if (more) {
-            nxt = read_next(o1, par ^ 1);
-            issue_next(nxt, par ^ 1, lnext, pnext, bnext);
-        }
-        if (tid == 0) lds.kfirst[par] = kInvalid;  // every wave read it before B1; next used for batch b+2
-
-        // (D) class positions: lane k < classes: class k's start over the
-        // workgroup + the slots of class k in waves before this one
-        uint32_t tot = 0, before = 0;
-        if (lane < (int)kStreamClasses) {
-#pragma unroll
-            for (int v = 0; v < WAVES; ++v) {
-                const uint32_t x = lds.wcls[v][lane];
-                tot += x;
-                before += (uint32_t)v < w ? x : 0u;
-            }
-        }
+        // class positions: class c's start over the workgroup + this wave's
+        // offset in it + the slot's rank in this wave
+        const uint32_t tot = lane < (int)kStreamClasses ? lds.cnt[par][lane] : 0u;
         const uint32_t cstart = wave_scan_dpp(tot) - tot + before;
         const uint32_t pos = (uint32_t)__shfl((int)cstart, (int)std::min<uint32_t>(cls, kStreamClasses - 1), 64) + rank;
         if (valid) {
-            const uint32_t off = staged ? kFront + cur.lead + od + inoff : inoff;
+            const uint32_t off = staged ? kFront + (uint32_t)wo + inoff : inoff;
             const uint32_t hi = tid | (code << 10) | ((uint32_t)staged << 14) | (std::min(len, kLenMax) << 15);
             lds.sdesc[pos] = (uint64_t)off | ((uint64_t)hi << 32);
         }
-        __syncthreads();  // ---------------------------------------------- B2 (descriptors)
+        if (tid == S - 1) lds.lastpos[par] = pos;
+        lds_barrier();  // ------------------------------------------------- B2 (descriptors)
+        if (tid < 16) lds.cnt[par][tid] = 0;  // read by every wave before B2; next used by batch b + 2
 
-        // (E) pass w: 64 class-sorted slots
+        // pass w: 64 class-sorted slots
         {
             const uint32_t idx = w * 64 + lane;
-            if (idx < S) {
+            if (idx < S && !(SHAPE & 1)) {
                 const uint64_t e = lds.sdesc[idx];
                 const uint32_t off = (uint32_t)e, hi = (uint32_t)(e >> 32);
                 const uint32_t cd = (hi >> 10) & 15u;
                 uint32_t ln = hi >> 15;
                 uint64_t h;
                 if ((hi >> 14) & 1u) {
-                    h = hash_slot_window(as_ldsw(lds.win[par]), cd, off, ln, bad);
+                    h = hash_slot_window(as_ldsw(lds.win[buf]), cd, off, ln, bad);
                 } else {
                     const uint32_t t = hi & 1023u;
-                    const uint32_t ob = div_small(t, args.a_magic);
-                    if (ln == kLenMax) ln = args.attr_len[cur.o0 * A + t];
-                    const uint8_t* p = args.blob + args.obj_base[cur.o0 + ob] + off;
+                    const uint32_t ot = div_small(t, args.a_magic);
+                    if (ln == kLenMax) ln = args.attr_len[o0 * A + t];
+                    const uint8_t* p = args.blob + args.obj_base[o0 + ot] + off;
                     h = hash_slot_global(p, cd, ln, bad);
                 }
                 lds.sdesc[idx] = h;
             }
         }
-        __syncthreads();  // ---------------------------------------------- B3 (coordinates parked)
-
-        // (F) coordinates in slot order
-        if (valid) __builtin_nontemporal_store(lds.sdesc[pos], args.coords + cur.o0 * A + tid);
-        if (!more) break;
-        cur = nxt;
-        lc = lnext;
-        lp = pnext;
-        bn = bnext;
+        // batch b+1's span and lengths and batch b+3's bases have landed
+        // (this wave's; every wave's after B3): younger are batch b+2's span
+        // copies and the store
+        vm_wait_le((span2 ? per_span : 0u) + stores);
+        lds_barrier();  // ------------------------------------------------- B3 (coordinates parked)
+        prev_o0 = o0;
+        prev_S = S;
+        prev_pos = pos;
     }
+    if (tid < prev_S) __builtin_nontemporal_store(lds.sdesc[prev_pos], args.coords + prev_o0 * A + tid);
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <int WAVES, uint32_t W>
+template <int WAVES, uint32_t W, int SHAPE = 0>
 static hipError_t launch_stream_t(const BatchArgs& args, hipStream_t stream, uint32_t wgs) {
     static_assert(sizeof(StreamLds<WAVES, W>) <= 163840, "one workgroup per CU");
     if (args.A == 0 || args.A > 64) return hipErrorInvalidValue;
     const uint64_t kcap = (64ull * WAVES) / args.A;
     uint64_t g = std::min<uint64_t>(wgs, (args.n + kcap - 1) / kcap);
     if (g == 0) g = 1;
-    hipLaunchKernelGGL((hash_stream_kernel<WAVES, W>), dim3((uint32_t)g), dim3(64 * WAVES), 0, stream, args);
+    hipLaunchKernelGGL((hash_stream_kernel<WAVES, W, SHAPE>), dim3((uint32_t)g), dim3(64 * WAVES), 0, stream, args);
     return hipGetLastError();
 }
 
@@ -391,16 +451,19 @@ static uint32_t device_cus() {
     return (uint32_t)cus;
 }
 
-// form 0: 16 waves, two 64 KiB windows, one workgroup per CU;
-// form 1: 8 waves, two 32 KiB windows, two per CU;
-// form 2: 16 waves, two 60 KiB windows.
+// form 0: 16 waves, 40 KiB windows; form 1: 16 waves, 32 KiB windows;
+// form 2: 8 waves, 16 KiB windows (two workgroups per CU).
 hipError_t launch_hash_stream(const BatchArgs& args, hipStream_t stream, int form) {
     if (args.n == 0) return hipSuccess;
     const uint32_t cus = device_cus();
     switch (form) {
-        case 0: return launch_stream_t<16, 65536 - 1024>(args, stream, cus);
-        case 1: return launch_stream_t<8, 32768 - 1024>(args, stream, 2 * cus);
-        case 2: return launch_stream_t<16, 61440>(args, stream, cus);
+        case 0: return launch_stream_t<16, 40960>(args, stream, cus);
+        case 1: return launch_stream_t<16, 32768>(args, stream, cus);
+        case 2: return launch_stream_t<8, 16384>(args, stream, 2 * cus);
+        // debug shapes of form 0 (WRONG coordinates): no hashing / no span copy / neither
+        case 3: return launch_stream_t<16, 40960, 1>(args, stream, cus);
+        case 4: return launch_stream_t<16, 40960, 2>(args, stream, cus);
+        case 5: return launch_stream_t<16, 40960, 3>(args, stream, cus);
         default: return hipErrorInvalidValue;
     }
 }
