@@ -133,4 +133,80 @@ __device__ __forceinline__ uint64_t hash_numeric_lds(ldsw_t w, uint32_t code, ui
     return hash_numeric(code, bits);
 }
 
+// 32 bytes at window byte offset o (any alignment): q[k] = bytes [o+8k, o+8k+8)
+struct Q32 {
+    uint64_t q0, q1, q2, q3;
+};
+__device__ __forceinline__ Q32 lds_read32(ldsw_t w, uint32_t o) {
+    const ldsw_t d = w + (o >> 2);
+    const uint32_t r = o & 3;
+    uint32_t x[9];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) x[i] = d[i];
+    Q32 q;
+    q.q0 = pack64(__builtin_amdgcn_alignbyte(x[1], x[0], r), __builtin_amdgcn_alignbyte(x[2], x[1], r));
+    q.q1 = pack64(__builtin_amdgcn_alignbyte(x[3], x[2], r), __builtin_amdgcn_alignbyte(x[4], x[3], r));
+    q.q2 = pack64(__builtin_amdgcn_alignbyte(x[5], x[4], r), __builtin_amdgcn_alignbyte(x[6], x[5], r));
+    q.q3 = pack64(__builtin_amdgcn_alignbyte(x[7], x[6], r), __builtin_amdgcn_alignbyte(x[8], x[7], r));
+    return q;
+}
+__device__ __forceinline__ uint64_t lds_read8(ldsw_t w, uint32_t o) {
+    const ldsw_t d = w + (o >> 2);
+    const uint32_t r = o & 3;
+    const uint32_t x0 = d[0], x1 = d[1], x2 = d[2];
+    return pack64(__builtin_amdgcn_alignbyte(x1, x0, r), __builtin_amdgcn_alignbyte(x2, x1, r));
+}
+
+// city.cc:278-301 (HashLen0to16) from s[0,8) and s[n-8,n).
+__device__ __forceinline__ uint64_t city_le16_ht(uint64_t h0, uint64_t t3, uint32_t n) {
+    const uint64_t mul = K2 + 2ull * n;
+    if (n >= 8) {
+        const uint64_t a = h0 + K2;
+        return mix16(ror(t3, 37) * mul + a, (ror(a, 25) + t3) * mul, mul);
+    }
+    if (n >= 4) return mix16(n + ((h0 & 0xffffffffull) << 3), t3 >> 32, mul);
+    if (n > 0) {
+        const uint32_t d0 = (uint32_t)h0;
+        const uint32_t y = (d0 & 0xff) + (((d0 >> (8 * (n >> 1))) & 0xff) << 8);
+        const uint32_t z = n + ((uint32_t)(t3 >> 56) << 2);
+        return shiftmix((uint64_t)y * K2 ^ (uint64_t)z * K0) * K2;
+    }
+    return K2;
+}
+
+// hash(type, slice) of a slot whose bytes start at window byte offset off,
+// from its first and last 32 bytes (two reads that serve every regime:
+// HashLen0to16 / 17to32 / 33to64 / the > 64-byte tail block) and, over 64
+// bytes, the loop blocks.  The window needs 32 readable bytes before off
+// (s[n-32, n) of a short string) and 36 after the value's end.
+__device__ __forceinline__ uint64_t hash_slot_window(ldsw_t w, uint32_t code, uint32_t off, uint32_t n, bool& bad) {
+    if (code == CODE_STRING) {
+        const Q32 t = lds_read32(w, off + n - 32);  // s[n-32, n): the front pad covers n < 32
+        const u64x2 t01 = {t.q0, t.q1}, t23 = {t.q2, t.q3};
+        if (n > 64) {
+            const Q32 u = lds_read32(w, off + n - 64);
+            Blk b;
+            b.v0 = u64x2{u.q0, u.q1};
+            b.v1 = u64x2{u.q2, u.q3};
+            b.v2 = t01;
+            b.v3 = t23;
+            return city_gt64_lds(w, off, n, b);
+        }
+        const Q32 h = lds_read32(w, off);  // s[0, 32): the back pad covers n < 32
+        const u64x2 h01 = {h.q0, h.q1};
+        if (n > 32) return city_33to64(h01, u64x2{h.q2, h.q3}, t01, t23, n);
+        if (n > 16) return city_17to32(h01, t23, n);
+        return city_le16_ht(h.q0, t.q3, n);
+    }
+    if (code == CODE_ZERO) return 0;
+    uint64_t bits = 0;
+    if (n == 8) {
+        bits = lds_read8(w, off);
+    } else if (n != 0) {
+        bad = true;
+        return 0;
+    }
+    return hash_numeric(code, bits);
+}
+
 }  // namespace hdx

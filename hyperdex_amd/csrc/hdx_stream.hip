@@ -84,91 +84,21 @@ __device__ __forceinline__ uint32_t stream_class(uint32_t code, uint32_t n, bool
     return 8;
 }
 
-// 32 bytes at window byte offset o (any alignment): q[k] = bytes [o+8k, o+8k+8)
-struct Q32 {
-    uint64_t q0, q1, q2, q3;
-};
-__device__ __forceinline__ Q32 lds_read32(ldsw_t w, uint32_t o) {
-    const ldsw_t d = w + (o >> 2);
-    const uint32_t r = o & 3;
-    uint32_t x[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) x[i] = d[i];
-    Q32 q;
-    q.q0 = pack64(__builtin_amdgcn_alignbyte(x[1], x[0], r), __builtin_amdgcn_alignbyte(x[2], x[1], r));
-    q.q1 = pack64(__builtin_amdgcn_alignbyte(x[3], x[2], r), __builtin_amdgcn_alignbyte(x[4], x[3], r));
-    q.q2 = pack64(__builtin_amdgcn_alignbyte(x[5], x[4], r), __builtin_amdgcn_alignbyte(x[6], x[5], r));
-    q.q3 = pack64(__builtin_amdgcn_alignbyte(x[7], x[6], r), __builtin_amdgcn_alignbyte(x[8], x[7], r));
-    return q;
-}
-__device__ __forceinline__ uint64_t lds_read8(ldsw_t w, uint32_t o) {
-    const ldsw_t d = w + (o >> 2);
-    const uint32_t r = o & 3;
-    const uint32_t x0 = d[0], x1 = d[1], x2 = d[2];
-    return pack64(__builtin_amdgcn_alignbyte(x1, x0, r), __builtin_amdgcn_alignbyte(x2, x1, r));
-}
-
-// city.cc:278-301 (HashLen0to16) from s[0,8) and s[n-8,n).
-__device__ __forceinline__ uint64_t city_le16_ht(uint64_t h0, uint64_t t3, uint32_t n) {
-    const uint64_t mul = K2 + 2ull * n;
-    if (n >= 8) {
-        const uint64_t a = h0 + K2;
-        return mix16(ror(t3, 37) * mul + a, (ror(a, 25) + t3) * mul, mul);
-    }
-    if (n >= 4) return mix16(n + ((h0 & 0xffffffffull) << 3), t3 >> 32, mul);
-    if (n > 0) {
-        const uint32_t d0 = (uint32_t)h0;
-        const uint32_t y = (d0 & 0xff) + (((d0 >> (8 * (n >> 1))) & 0xff) << 8);
-        const uint32_t z = n + ((uint32_t)(t3 >> 56) << 2);
-        return shiftmix((uint64_t)y * K2 ^ (uint64_t)z * K0) * K2;
-    }
-    return K2;
-}
-
-// hash(type, slice) of a slot whose bytes start at window byte offset off.
-__device__ __forceinline__ uint64_t hash_slot_window(ldsw_t w, uint32_t code, uint32_t off, uint32_t n, bool& bad) {
-    if (code == CODE_STRING) {
-        const Q32 t = lds_read32(w, off + n - 32);  // s[n-32, n): the front pad covers n < 32
-        const u64x2 t01 = {t.q0, t.q1}, t23 = {t.q2, t.q3};
-        if (n > 64) {
-            const Q32 u = lds_read32(w, off + n - 64);
-            Blk b;
-            b.v0 = u64x2{u.q0, u.q1};
-            b.v1 = u64x2{u.q2, u.q3};
-            b.v2 = t01;
-            b.v3 = t23;
-            return city_gt64_lds(w, off, n, b);
-        }
-        const Q32 h = lds_read32(w, off);  // s[0, 32): the back pad covers n < 32
-        const u64x2 h01 = {h.q0, h.q1};
-        if (n > 32) return city_33to64(h01, u64x2{h.q2, h.q3}, t01, t23, n);
-        if (n > 16) return city_17to32(h01, t23, n);
-        return city_le16_ht(h.q0, t.q3, n);
-    }
-    if (code == CODE_ZERO) return 0;
-    uint64_t bits = 0;
-    if (n == 8) {
-        bits = lds_read8(w, off);
-    } else if (n != 0) {
-        bad = true;
-        return 0;
-    }
-    return hash_numeric(code, bits);
-}
-
 // The same from global memory (the gather kernels' dword-aligned loads).
 __device__ __forceinline__ uint64_t hash_slot_global(const uint8_t* p, uint32_t code, uint32_t n, bool& bad) {
     return hash_blk<false, false, true>(code, p, n, consume_any<true>(issue_any<true>(code, p, n)), bad);
 }
 
-// Batch x's buffers: span window x % 3, lengths x % 3, bases x % 4 (the bases
-// are copied a batch earlier than the span, whose bounds they give).
+// Batch x's buffers: span window, lengths and object bases x % 3 (copied two
+// batches ahead); its bounds base[o0], base[o0 + K] come from the bounds
+// ring, copied 256 batches at a time a block ahead.
 template <int WAVES, uint32_t W>
 struct StreamLds {
     static constexpr uint32_t S = 64 * WAVES;  // slots per batch at most
     uint8_t win[3][kFront + W + kBack] __attribute__((aligned(16)));
     uint32_t lens[3][S];             // slot lengths (LDS DMA; past the batch: garbage)
-    uint32_t bases[4][S];            // object bases o0 .. o0 + S/2 - 1, u64 as dword pairs (LDS DMA)
+    uint32_t bases[3][S];            // object bases o0 .. o0 + S/2 - 1, u64 as dword pairs (LDS DMA)
+    uint32_t bnd[2][576];            // per block of 256 batches: base[o0] of its batches and the end, dword pairs
     uint64_t sdesc[S];               // class-sorted {offset, slot | code | staged | len}; then the coordinate
     uint32_t cnt[2][16];             // per batch parity: slots per class (LDS atomics)
     uint32_t lastpos[2];             // per batch parity: the sorted position of the batch's last slot
@@ -237,8 +167,8 @@ hash_stream_kernel(const BatchArgs args) {
     const uint32_t w = tid >> 6;
     const uint32_t A = args.A;  // 1..64
     const uint64_t n = args.n;
-    // this wave's copies per batch: span instructions + tail + lengths; and one for its bases
-    const uint32_t per_span = (NI + WAVES - 1 - w) / WAVES + 2;
+    // this wave's copies per batch: span instructions + tail + lengths + bases
+    const uint32_t per_span = (NI + WAVES - 1 - w) / WAVES + 3;
 
     // this workgroup's objects, in batches of K (fixed, so that every batch's
     // start is known ahead and the copies run two batches ahead)
@@ -264,26 +194,32 @@ hash_stream_kernel(const BatchArgs args) {
 
     auto batch_o0 = [&](uint32_t x) { return r0 + (uint64_t)x * K; };
     auto batch_k = [&](uint32_t x) { return (uint32_t)std::min<uint64_t>(K, r1 - batch_o0(x)); };
-    auto base_at = [&](uint32_t x, uint32_t i) { return pack64(lds.bases[x & 3][2 * i], lds.bases[x & 3][2 * i + 1]); };
+    auto base_at = [&](uint32_t x, uint32_t i) { return pack64(lds.bases[x % 3][2 * i], lds.bases[x % 3][2 * i + 1]); };
+    auto bound = [&](uint32_t x) {  // base[o0] of batch x (x = nbatch: the range's end)
+        const uint32_t* v = lds.bnd[(x >> 8) & 1] + 2 * (x & 255);
+        return pack64(v[0], v[1]);
+    };
     // the span of batch x held in its window: bytes from its first 16-byte
     // unit (0 for the launch's last batch, whose end is unknown: hashed from
     // global memory)
     auto held_bytes = [&](uint32_t x, uint64_t& b0, uint32_t& lead) {
         const uint64_t o0 = batch_o0(x);
         const uint32_t k = batch_k(x);
-        b0 = base_at(x, 0);
+        b0 = bound(x);
         lead = (uint32_t)((uintptr_t)(args.blob + b0) & 15);
         if (o0 + k >= n) return 0u;
-        const uint64_t be = base_at(x, k);
+        const uint64_t be = (x & 255) == 255 ? pack64(lds.bnd[(x >> 8) & 1][512], lds.bnd[(x >> 8) & 1][513]) : bound(x + 1);
         return be > b0 ? (uint32_t)std::min<uint64_t>(lead + (be - b0), W) : 0u;
     };
-    // batch x's bases: 1 copy per wave (64 dwords each, 512 bases)
-    auto issue_bases = [&](uint32_t x) {
-        dma_x1((const uint32_t*)args.obj_base + std::min<uint64_t>(2 * batch_o0(x) + tid, 2 * n - 1),
-               lds.bases[x & 3] + 64 * w);
+    // the bounds of block q's batches 256q .. 256q + 255 and the end of the
+    // last: one copy per wave (a lane a dword of base[o0 of batch 256q + v])
+    auto issue_bounds = [&](uint32_t q) {
+        const uint32_t v = tid >> 1;
+        const uint64_t o = std::min<uint64_t>(batch_o0(256 * q + std::min(v, 256u)), n - 1);
+        dma_x1((const uint32_t*)args.obj_base + 2 * o + (tid & 1), w < 9 ? lds.bnd[q & 1] + 64 * w : lds.dummy);
     };
-    // batch x's span and lengths: per_span copies per wave (every lane issues,
-    // sources clamped), its bases already in LDS
+    // batch x's span, lengths and bases: per_span copies per wave (every lane
+    // issues, sources clamped)
     auto issue_span = [&](uint32_t x) {
         const uint32_t buf = x % 3;
         uint64_t b0;
@@ -295,21 +231,24 @@ hash_stream_kernel(const BatchArgs args) {
             const uint32_t u = std::min<uint32_t>(i * 64 + lane, units ? units - 1 : 0);
             dma_x4(s16 + 16ull * u, lds.win[buf] + kFront + 1024 * i);
         }
-        // the last partial unit as dwords (a dword never crosses a page)
+        // the last partial unit as dwords (a dword never crosses a page), by
+        // the wave whose 16-byte copy wrote a clamped lane's bytes there just
+        // before (a wave's LDS DMA lands in issue order)
         const uint32_t tdw = ((bytes & 15) + 3) >> 2;
-        const bool tail = w == WAVES - 1 && tdw != 0 && !(SHAPE & 2);
+        const bool tail = w == (units >> 6) % WAVES && tdw != 0 && !(SHAPE & 2);
         dma_x1(tail ? (const void*)(s16 + 16ull * units + 4 * std::min<uint32_t>(lane, tdw - 1)) : (const void*)args.attr_len,
                tail ? (const void*)(lds.win[buf] + kFront + 16 * units) : (const void*)lds.dummy);
         dma_x1(args.attr_len + std::min<uint64_t>(batch_o0(x) * A + tid, n * A - 1), lds.lens[buf] + 64 * w);
+        dma_x1((const uint32_t*)args.obj_base + std::min<uint64_t>(2 * batch_o0(x) + tid, 2 * n - 1),
+               lds.bases[buf] + 64 * w);
     };
 
-    // prologue: bases 0, 1; then span 0, bases 2, span 1
-    issue_bases(0);
-    if (1 < nbatch) issue_bases(1);
+    // prologue: the bounds of blocks 0 and 1; spans 0 and 1
+    issue_bounds(0);
+    issue_bounds(1);
     vm_wait<0>();
     lds_barrier();
     issue_span(0);
-    if (2 < nbatch) issue_bases(2);
     if (1 < nbatch) issue_span(1);
     vm_wait_le(1 < nbatch ? per_span : 0u);
     lds_barrier();
@@ -317,16 +256,28 @@ hash_stream_kernel(const BatchArgs args) {
     bool bad = false;
     uint64_t prev_o0 = 0;
     uint32_t prev_S = 0, prev_pos = 0;
+    uint64_t tph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // SHAPE & 4: shader cycles per phase (wave 0 of workgroup 0)
+    uint64_t tlast = 0;
+    auto stamp = [&](int ph) {
+        if constexpr ((SHAPE & 4) != 0) {
+            const uint64_t t = __builtin_amdgcn_s_memtime();
+            tph[ph] += t - tlast;
+            tlast = t;
+        }
+    };
     for (uint32_t b = 0; b < nbatch; ++b) {
+        stamp(0);
         // here: batch b's span and lengths, and the bases of batches <= b + 2, are in LDS
         const uint32_t buf = b % 3, par = b & 1;
         const uint64_t o0 = batch_o0(b);
         const uint32_t k = batch_k(b);
         const uint32_t S = k * A;
-        // copies: batch b+3's bases, then batch b+2's span and lengths
-        if (b + 3 < nbatch) issue_bases(b + 3);
+        // copies: at a block's start, the bounds of the block after the next;
+        // then batch b+2's span, lengths and bases
+        if ((b & 255) == 0 && b > 0 && b + 256 < nbatch) issue_bounds((b >> 8) + 1);
         const bool span2 = b + 2 < nbatch;
         if (span2) issue_span(b + 2);
+        stamp(1);
         // batch b-1's coordinates, parked in sdesc, in slot order (every lane
         // stores — slot min(t, S - 1) — so that the store is always issued)
         if (prev_S) {
@@ -335,6 +286,7 @@ hash_stream_kernel(const BatchArgs args) {
             __builtin_nontemporal_store(lds.sdesc[pp], args.coords + prev_o0 * A + t);
         }
         const uint32_t stores = prev_S ? 1u : 0u;
+        stamp(2);
 
         // describe batch b: slot t = tid
         const bool valid = tid < S;
@@ -383,7 +335,9 @@ hash_stream_kernel(const BatchArgs args) {
         // this wave's slots of class c go after those of the waves that got there first
         uint32_t before = 0;
         if (lane < (int)kStreamClasses && mycnt) before = atomicAdd(&lds.cnt[par][lane], mycnt);
+        stamp(3);
         lds_barrier();  // ------------------------------------------------- B1 (class counts)
+        stamp(4);
 
         // class positions: class c's start over the workgroup + this wave's
         // offset in it + the slot's rank in this wave
@@ -396,7 +350,9 @@ hash_stream_kernel(const BatchArgs args) {
             lds.sdesc[pos] = (uint64_t)off | ((uint64_t)hi << 32);
         }
         if (tid == S - 1) lds.lastpos[par] = pos;
+        stamp(5);
         lds_barrier();  // ------------------------------------------------- B2 (descriptors)
+        stamp(6);
         if (tid < 16) lds.cnt[par][tid] = 0;  // read by every wave before B2; next used by batch b + 2
 
         // pass w: 64 class-sorted slots
@@ -420,17 +376,26 @@ hash_stream_kernel(const BatchArgs args) {
                 lds.sdesc[idx] = h;
             }
         }
-        // batch b+1's span and lengths and batch b+3's bases have landed
-        // (this wave's; every wave's after B3): younger are batch b+2's span
-        // copies and the store
+        // batch b+1's copies (and a new block's bounds) have landed (this
+        // wave's; every wave's after B3): younger are batch b+2's copies and
+        // the store
+        stamp(7);
         vm_wait_le((span2 ? per_span : 0u) + stores);
+        stamp(8);
         lds_barrier();  // ------------------------------------------------- B3 (coordinates parked)
+        stamp(9);
         prev_o0 = o0;
         prev_S = S;
         prev_pos = pos;
     }
     if (tid < prev_S) __builtin_nontemporal_store(lds.sdesc[prev_pos], args.coords + prev_o0 * A + tid);
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
+    if constexpr ((SHAPE & 4) != 0) {
+        if (blockIdx.x == 0 && tid == 0) {
+            tph[0] = nbatch;  // (phase 0 is the loop's own overhead: report the batch count instead)
+            for (int i = 0; i < 10; ++i) args.coords[i] = tph[i];
+        }
+    }
 }
 
 template <int WAVES, uint32_t W, int SHAPE = 0>
@@ -464,6 +429,9 @@ hipError_t launch_hash_stream(const BatchArgs& args, hipStream_t stream, int for
         case 3: return launch_stream_t<16, 40960, 1>(args, stream, cus);
         case 4: return launch_stream_t<16, 40960, 2>(args, stream, cus);
         case 5: return launch_stream_t<16, 40960, 3>(args, stream, cus);
+        // form 0 with per-phase shader-cycle counters of workgroup 0, wave 0, in coords[0..9]
+        case 6: return launch_stream_t<16, 40960, 4>(args, stream, cus);
+        case 7: return launch_stream_t<16, 40960, 7>(args, stream, cus);
         default: return hipErrorInvalidValue;
     }
 }

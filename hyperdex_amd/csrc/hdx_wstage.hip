@@ -166,11 +166,16 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
 // One slot: staged from the LDS window lw (desc offset), else from global
 // memory at its object's base (lane o of mybase).  SHAPE 1 (debug): one LDS
 // dword instead of the hash.
-template <int SHAPE>
+// HT: staged slots hashed by hash_slot_window (first / last 32 bytes, every
+// regime from the same two reads; lw then points kFrontHT bytes before the
+// window).
+constexpr uint32_t kFrontHT = 32;
+template <int SHAPE, bool HT = false>
 __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, bool staged, uint64_t mybase,
                                               uint32_t s, uint32_t cd, uint64_t d, bool& bad) {
     const uint32_t doff = (uint32_t)d, dn = (uint32_t)(d >> 32);
     if (SHAPE == 1) return lw[doff >> 2] ^ dn;
+    if (staged && HT) return hash_slot_window(lw, cd, doff + kFrontHT, dn, bad);
     if (staged) return cd == CODE_STRING ? hash_string_lds(lw, doff, dn) : hash_numeric_lds(lw, cd, doff, dn, bad);
     const uint32_t o = div_small(s, args.a_magic);
     const uint64_t ob = shfl64(mybase, (int)(o & 63));
@@ -182,19 +187,21 @@ __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, 
 // wave; WB-byte windows.  SHAPE (debug variants 207/208 only, WRONG
 // coordinates): 1 = everything but the hash (one LDS dword per slot instead);
 // 2 = no DMA (the hash runs on whatever the window holds).
-template <int NCH, uint32_t WB, int SHAPE = 0>
+template <int NCH, uint32_t WB, int SHAPE = 0, bool HT = false>
 __global__ void __launch_bounds__(256)
 hash_wstage_kernel(const BatchArgs args) {
     static_assert(NCH >= 1 && NCH <= 4 && WB % 16 == 0, "slot indices are 8 bits; windows whole DMA units");
-    __shared__ __attribute__((aligned(16))) uint8_t win_all[4][WB + 64];  // +64: dword over-reads past the span
+    constexpr uint32_t FRONT = HT ? kFrontHT : 0;
+    // +64: dword over-reads past the span; HT: 32 bytes before it (short strings' tail reads)
+    __shared__ __attribute__((aligned(16))) uint8_t win_all[4][FRONT + WB + 64];
     __shared__ WStageMeta<NCH> meta;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
-    uint8_t* win = win_all[w];
+    uint8_t* win = win_all[w] + FRONT;
     uint64_t* desc = meta.desc[w];
     uint16_t* perm = meta.perm[w];
     uint32_t* cnt = meta.cnt[w];
-    const ldsw_t lw = as_ldsw(win);
+    const ldsw_t lw = as_ldsw(win_all[w]);
 
     const uint64_t o0 = ((uint64_t)blockIdx.x * 4 + w) * args.K;
     if (o0 >= args.n) return;  // no barrier anywhere: waves are independent
@@ -228,7 +235,7 @@ hash_wstage_kernel(const BatchArgs args) {
     for (int t = 0; t < NCH; ++t) {
         const uint32_t e = perm[t * 64 + lane];
         const uint32_t s = e & 0xffu;
-        desc[s] = hash_slot<SHAPE>(args, lw, g.staged, g.mybase, s, e >> 8, desc[s], bad);
+        desc[s] = hash_slot<SHAPE, HT>(args, lw, g.staged, g.mybase, s, e >> 8, desc[s], bad);
     }
     wave_lds_fence();
 
@@ -354,7 +361,7 @@ hash_wgstage_kernel(const BatchArgs args) {
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0>
+template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, bool HT = false>
 static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     // lane o holds object o's base and lane K the next group's first: K <= 63
     args.K = std::min<uint32_t>(std::min<uint32_t>((uint32_t)(64 * NCH) / args.A, KCAP), 63u);
@@ -363,7 +370,7 @@ static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
     return hipGetLastError();
 }
 
@@ -396,6 +403,10 @@ hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int for
         case 7: return launch_wstage_t<2, 8832, 63, 1>(args, stream);  // debug shape: no hash
         case 8: return launch_wstage_t<2, 8832, 63, 2>(args, stream);  // debug shape: no DMA
         case 9: return launch_wstage_t<2, 8832, 3>(args, stream);  // <= 3 objects: per-regime costs on uniform batches
+        // head/tail window hashing (hash_slot_window)
+        case 12: return launch_wstage_t<2, 8832, 63, 0, true>(args, stream);
+        case 13: return launch_wstage_t<2, 8832, 3, 0, true>(args, stream);  // <= 3 objects (per-regime costs)
+        case 14: return launch_wstage_t<3, 14336, 63, 0, true>(args, stream);
         // the slots class-sorted over the workgroup
         case 10: return launch_wgstage_t<2, 8832>(args, stream);
         case 11: return launch_wgstage_t<1, 4352>(args, stream);
