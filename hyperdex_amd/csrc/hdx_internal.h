@@ -51,7 +51,10 @@ hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream);
 hipError_t launch_hash_staged(const BatchArgs& args, hipStream_t stream, uint32_t slots, uint32_t win_bytes);
 // Wave-staged hash (hdx_wstage.hip): K whole objects per wave copied into an
 // LDS window by DMA and hashed from LDS; form = passes / window size.
-hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int form);
+hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int form);  // debug library
+// Its product form (hdx_wstage.hip): two passes per wave, head/tail hashing;
+// A <= 128 (else hipErrorInvalidValue).
+hipError_t launch_hash_wstage_product(const BatchArgs& args, hipStream_t stream);
 // Streamed hash (hdx_stream.hip): one persistent workgroup per CU walks its
 // objects in batches staged in LDS by DMA a batch ahead, slots class-sorted
 // over the workgroup; A <= 64 (else hipErrorInvalidValue).

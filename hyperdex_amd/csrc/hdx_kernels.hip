@@ -38,7 +38,9 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 21: return launch_regroup<4, true, false>(args, stream);
         case 25: return launch_regroup<16, true, false, false>(args, stream);
         case 44: return launch_regroup<2, true, true, true, true, false, true, 1>(args, stream);
-        case 46: return launch_regroup<8, true, true, true, false, false, true, 1>(args, stream);        default:
+        case 46: return launch_regroup<8, true, true, true, false, false, true, 1>(args, stream);
+        case 212: return launch_hash_wstage_product(args, stream);  // hdx_wstage.hip
+        default:
 #if HDX_DEBUG_BUILD
             return launch_debug_variant(args, stream, variant);  // hdx_kernels_dbg.hip
 #else
@@ -85,11 +87,15 @@ hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream) 
 //    and burst stores (25) when the grid keeps >= 64 K waves, 8 chunks (20) from
 //    32 M slots (config 3a: 2.24 vs 2.38 ms), else the one-chunk kernel (12)
 //    (config 1);
-//  * otherwise (strings + int64/float, config 3b): regroup with the class sort
-//    over 2 chunks (LDS fetch-add counting sort, classes in ORDER 1) and
-//    dword-aligned loads (44): 3.37 vs 3.43 ms in ORDER 0 (38) and 4.22 for
-//    the chunk kernel — byte-misaligned 16-byte loads had made the
-//    texture-address unit the bound.
+//  * otherwise (strings + int64/float, config 3b): the wave-staged kernel
+//    (212, hdx_wstage.hip): each wave copies its 7 objects' span into LDS by
+//    coalesced DMA, class-sorts the 119 slots and hashes them from LDS with
+//    head/tail reads — 2.92 vs 3.32 ms for the gather kernel 44 (round 3,
+//    profiles/r3/ab_wstage_ht.jsonl).  Up to round 2 this case ran 44: the
+//    class sort over 2 chunks with dword-aligned loads (3.37 vs 3.43 ms in
+//    ORDER 0 (38) and 4.22 for the chunk kernel — byte-misaligned 16-byte
+//    loads had made the texture-address unit the bound).
+//    Schemas of more than 128 attributes keep 44.
 static int auto_variant(const BatchArgs& args) {
     uint32_t numeric = 0;
     bool complex_types = false;
@@ -106,7 +112,7 @@ static int auto_variant(const BatchArgs& args) {
         if (slots >= (32ull << 20)) return 20;
         return 12;
     }
-    return 44;
+    return args.A <= 128 ? 212 : 44;
 }
 
 #if !HDX_DEBUG_BUILD
@@ -152,6 +158,7 @@ const char* variant_kernel_name(int v) {
         case 44: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true, 1>(hdx::BatchArgs)";
         case 45: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true, 2>(hdx::BatchArgs)";
         case 46: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, true, 1>(hdx::BatchArgs)";
+        case 212: return "void hdx::hash_wstage_kernel<2, 8832u, 0, true, 1>(hdx::BatchArgs)";
         default: return "";
     }
 }

@@ -114,6 +114,18 @@ __device__ __forceinline__ uint32_t work_class(uint32_t code, uint32_t n, bool v
         return n <= 16 ? 1u : n <= 32 ? 2u : 3u;
     }
 }
+// ORDER 3 (the wave-staged kernel's head/tail hashing): strings of <= 64
+// bytes first (33..64, <= 16, 17..32), then numerics / non-hashable / unused
+// slots, then > 64 B by blocks: a 2-pass wave's second pass holds the long
+// strings beside the cheapest regime.
+__device__ __forceinline__ uint32_t work_class3(uint32_t code, uint32_t n, bool valid) {
+    if (!valid || code != CODE_STRING) return 3;
+    if (n > 64) {
+        const uint32_t b = (n - 1) >> 6;
+        return b >= 4 ? 7u : 3u + b;
+    }
+    return n > 32 ? 0u : n <= 16 ? 1u : 2u;
+}
 
 
 // ===========================================================================

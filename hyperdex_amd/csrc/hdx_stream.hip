@@ -59,7 +59,6 @@ namespace {
 
 typedef __attribute__((address_space(3))) void* lds_void_t;
 
-constexpr uint32_t kInvalid = 0xffffffffu;
 constexpr uint32_t kFront = 32;   // window bytes before the span (tail reads of short strings)
 constexpr uint32_t kBack = 256;  // after it (head reads of short strings; the 64-lane tail copy)
 constexpr uint32_t kLenBits = 17, kLenMax = (1u << kLenBits) - 1;

@@ -1,417 +1,17 @@
-// hdx_wstage.hip — wave-staged batch hash for mixed variable-length schemas
-// (config 3b's shape: strings of every CityHash regime beside int64/float).
-//
-// hdx_hash_batch_device's contract (include/hdxhash.h): coords[i*A + j] =
-// hs[j] of hyperdex::hash(schema, key, value, hs) (common/hash.cc:56-68).
-//
-// Why this shape.  The gather kernels load every
-// slot's bytes with per-lane 16-byte loads, one value per lane: each load
-// instruction touches ~64 cache lines, and strings over 64 bytes (the CityHash
-// loop) stream at ~4 TB/s even with no hash arithmetic (tools/lwbench.hip,
-// profiles/r3/lwbench.jsonl: 4.05 TB/s lane-per-string on 65..195-byte
-// strings).  Here one wave owns K whole objects, which a packed batch stores
-// back to back: their bytes are one span, copied into a wave-private LDS window
-// by coalesced LDS DMA (global_load_lds_dwordx4, 1 KiB per instruction), which
-// streams at ~5.4 TB/s in the same probe.  Per wave:
-//   1. the K object bases (+ the next group's first, so the DMA of
-//      [base[o0], base[o0 + K]) goes out before the lengths are back) and the
-//      K*A lengths, coalesced;
-//   2. per-slot in-object offsets by a DPP prefix scan, object sizes, a check
-//      that the objects are back to back and fit the window;
-//   3. a wave-local counting sort of the slots by work class (ORDER 1 of
-//      hdx_regroup.h: numerics, 33..64 B, <= 16 B, 17..32 B, > 64 B by loop
-//      blocks), so a pass of 64 lanes runs few CityHash regimes;
-//   4. s_waitcnt vmcnt(0) (the compiler does not order ds_read behind an LDS
-//      DMA), then NCH passes hashing from LDS (hdx_lds_hash.h: dword reads +
-//      v_alignbyte, the A4 arithmetic), each coordinate parked over its
-//      consumed descriptor;
-//   5. one coalesced non-temporal store of the K*A coordinates.
-// A group whose objects are not back to back or do not fit the window is
-// hashed from global memory instead (the A4 loads of hdx_loads.h), so every
-// layout gives the reference's coordinates.  Four waves per workgroup, each
-// with its own window: no workgroup barrier.
-#include <hip/hip_runtime.h>
-
-#include <stdint.h>
-
-#include <algorithm>
-
-#include "hdx_lds_hash.h"
-#include "hdx_regroup.h"
+// hdx_wstage.hip — the product instantiation of the wave-staged batch hash
+// (hdx_wstage.h): two class-sorted passes per wave, 8832-byte windows (four
+// workgroups of four waves per CU), slots hashed from the window with the
+// head/tail reads of hash_slot_window (hdx_lds_hash.h).  The automatic policy
+// runs it for mixed string / int64 / float schemas (config 3b: 2.92 vs 3.32 ms
+// for variant 44, profiles/r3/ab_wstage_ht.jsonl).  The A/B forms are in
+// hdx_wstage_dbg.hip (debug library only).
+#include "hdx_wstage.h"
 
 namespace hdx {
-namespace {
 
-typedef __attribute__((address_space(3))) void* lds_void_t;
-
-template <int NCH>
-struct WStageMeta {
-    uint64_t desc[4][NCH * 64];  // {offset u32, length u32}; then the slot's parked coordinate
-    uint16_t perm[4][NCH * 64];  // slot | code << 8, in class order
-    uint32_t cnt[4][kClasses];
-};
-
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-    return pack64(__builtin_amdgcn_readlane((uint32_t)v, l), __builtin_amdgcn_readlane((uint32_t)(v >> 32), l));
-}
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int l) {
-    return pack64((uint32_t)__shfl((int)(uint32_t)v, l, 64), (uint32_t)__shfl((int)(uint32_t)(v >> 32), l, 64));
-}
-__device__ __forceinline__ void wave_lds_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-}  // namespace
-
-// One wave's group: K = args.K consecutive objects from o0, their bases,
-// lengths, codes and work classes, and (staged) their span in `win`.
-template <int NCH>
-struct Group {
-    uint64_t q0, mybase;
-    uint32_t nobj, ns;
-    bool staged;
-    uint32_t L[NCH], code[NCH], cls[NCH];
-};
-
-// Phases 1-3a: bases and lengths, the span's DMA into win (early when the
-// next group's first object bounds it), in-object offsets, object sizes, the
-// staged decision, and every slot's descriptor desc[s] = {offset, length}:
-// the offset in `win` + win_off when staged, else in the object.  SHAPE 2
-// (debug) skips the DMA.
-template <int NCH, uint32_t WB, int SHAPE>
-__device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint64_t o0, uint8_t* win, uint32_t win_off,
-                                                     uint64_t* desc) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t A = args.A, K = args.K;
-    Group<NCH> g;
-    g.nobj = (uint32_t)min<uint64_t>(K, args.n - o0);
-    g.ns = g.nobj * A;
-    g.q0 = o0 * A;
-
-    // ---- bases (lane nobj: the next group's first object) and lengths ------
-    const bool has_next = o0 + K < args.n;
-    const uint32_t nbase = g.nobj + (has_next ? 1u : 0u);
-    const uint64_t mybase = (uint32_t)lane < nbase ? args.obj_base[o0 + lane] : 0;
-    g.mybase = mybase;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const uint32_t s = (uint32_t)(c * 64 + lane);
-        g.L[c] = s < g.ns ? args.attr_len[g.q0 + s] : 0u;
-    }
-    const uint64_t b0 = readlane64(mybase, 0);
-    const uint64_t bnext = has_next ? readlane64(mybase, (int)g.nobj) : 0;
-    const uint32_t lead = (uint32_t)((uintptr_t)(args.blob + b0) & 15);
-    const uint8_t* s16 = args.blob + b0 - lead;
-    auto dma = [&](uint32_t units) {  // units 16-byte units from s16 -> win (units <= WB / 16)
-        for (uint32_t u0 = 0; u0 < units; u0 += 64) {
-            const uint32_t u = u0 + (uint32_t)lane;
-            if (u < units)  // lanes past the span write nothing: the window need not be whole KiB
-                __builtin_amdgcn_global_load_lds((const void*)(s16 + 16ull * u), (lds_void_t)(win + 16 * u0), 16, 0, 0);
-        }
-    };
-    // the span up to the next group's first object, before the lengths are back
-    const bool early = has_next && bnext > b0 && lead + (bnext - b0) <= WB;
-    if (early && SHAPE != 2) dma((lead + (uint32_t)(bnext - b0) + 15) >> 4);
-
-    // ---- in-object offsets, codes, object sizes ----------------------------
-    const uint32_t packed_codes = reinterpret_cast<const uint32_t*>(args.codes)[lane];
-    uint32_t off[NCH], endv[NCH];
-    uint32_t carry = 0;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const uint32_t s = (uint32_t)(c * 64 + lane);
-        const uint32_t o = div_small(s, args.a_magic);
-        const uint32_t j = s - o * A;
-        const uint32_t Sx = wave_scan_dpp(g.L[c]) - g.L[c];
-        const int head = lane - (int)j;
-        const uint32_t head_sx = __shfl(Sx, head < 0 ? 0 : head, 64);
-        off[c] = head >= 0 ? Sx - head_sx : carry + Sx;
-        carry = __builtin_amdgcn_readlane(off[c] + g.L[c], 63);
-        const uint32_t cd = args.uniform_code != 0xffu
-                                ? args.uniform_code
-                                : (__shfl(packed_codes, (int)(j >> 2), 64) >> (8 * (j & 3))) & 0xffu;
-        g.code[c] = s < g.ns ? cd : (uint32_t)CODE_ZERO;
-        endv[c] = off[c] + g.L[c];
-    }
-    // lane o < nobj: its object's size = the end of its last attribute
-    const uint32_t last_slot = (uint32_t)lane * A + A - 1;
-    uint32_t mysize = 0;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const uint32_t v = (uint32_t)__shfl((int)endv[c], (int)(last_slot & 63), 64);
-        if ((last_slot >> 6) == (uint32_t)c) mysize = v;
-    }
-    const uint64_t nextb = shfl64(mybase, (lane + 1) & 63);
-    const bool runs = __all((uint32_t)lane >= g.nobj || (uint32_t)lane + 1 >= nbase || mybase + mysize == nextb);
-    const uint64_t bend = readlane64(mybase + mysize, (int)g.nobj - 1);
-    g.staged = runs && bend >= b0 && lead + (bend - b0) <= WB;
-    if (g.staged && !early && SHAPE != 2) dma((lead + (uint32_t)(bend - b0) + 15) >> 4);  // the batch's last group
-    const uint32_t rel = (uint32_t)(mybase - b0) + lead + win_off;  // lane o: its object's window offset (staged)
-
-    // ---- descriptors and work classes ----------------------------------------
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const uint32_t s = (uint32_t)(c * 64 + lane);
-        const uint32_t o = div_small(s, args.a_magic);
-        const uint32_t orel = (uint32_t)__shfl((int)rel, (int)(o & 63), 64);
-        const uint32_t doff = g.staged ? orel + off[c] : off[c];
-        desc[s] = (uint64_t)doff | ((uint64_t)g.L[c] << 32);
-        g.cls[c] = work_class<1>(g.code[c], g.L[c], s < g.ns);
-    }
-    return g;
-}
-
-// One slot: staged from the LDS window lw (desc offset), else from global
-// memory at its object's base (lane o of mybase).  SHAPE 1 (debug): one LDS
-// dword instead of the hash.
-// HT: staged slots hashed by hash_slot_window (first / last 32 bytes, every
-// regime from the same two reads; lw then points kFrontHT bytes before the
-// window).
-constexpr uint32_t kFrontHT = 32;
-template <int SHAPE, bool HT = false>
-__device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, bool staged, uint64_t mybase,
-                                              uint32_t s, uint32_t cd, uint64_t d, bool& bad) {
-    const uint32_t doff = (uint32_t)d, dn = (uint32_t)(d >> 32);
-    if (SHAPE == 1) return lw[doff >> 2] ^ dn;
-    if (staged && HT) return hash_slot_window(lw, cd, doff + kFrontHT, dn, bad);
-    if (staged) return cd == CODE_STRING ? hash_string_lds(lw, doff, dn) : hash_numeric_lds(lw, cd, doff, dn, bad);
-    const uint32_t o = div_small(s, args.a_magic);
-    const uint64_t ob = shfl64(mybase, (int)(o & 63));
-    const uint8_t* p = args.blob + ob + doff;
-    return hash_blk<false, false, true>(cd, p, dn, consume_any<true>(issue_any<true>(cd, p, dn)), bad);
-}
-
-// NCH passes of 64 slots: K = min(floor(64 * NCH / A), KCAP, 63) objects per
-// wave; WB-byte windows.  SHAPE (debug variants 207/208 only, WRONG
-// coordinates): 1 = everything but the hash (one LDS dword per slot instead);
-// 2 = no DMA (the hash runs on whatever the window holds).
-template <int NCH, uint32_t WB, int SHAPE = 0, bool HT = false>
-__global__ void __launch_bounds__(256)
-hash_wstage_kernel(const BatchArgs args) {
-    static_assert(NCH >= 1 && NCH <= 4 && WB % 16 == 0, "slot indices are 8 bits; windows whole DMA units");
-    constexpr uint32_t FRONT = HT ? kFrontHT : 0;
-    // +64: dword over-reads past the span; HT: 32 bytes before it (short strings' tail reads)
-    __shared__ __attribute__((aligned(16))) uint8_t win_all[4][FRONT + WB + 64];
-    __shared__ WStageMeta<NCH> meta;
-    const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
-    uint8_t* win = win_all[w] + FRONT;
-    uint64_t* desc = meta.desc[w];
-    uint16_t* perm = meta.perm[w];
-    uint32_t* cnt = meta.cnt[w];
-    const ldsw_t lw = as_ldsw(win_all[w]);
-
-    const uint64_t o0 = ((uint64_t)blockIdx.x * 4 + w) * args.K;
-    if (o0 >= args.n) return;  // no barrier anywhere: waves are independent
-    const Group<NCH> g = describe_group<NCH, WB, SHAPE>(args, o0, win, 0, desc);
-
-    // ---- counting sort by work class (wave-local) --------------------------
-    if (lane < kClasses) cnt[lane] = 0;
-    wave_lds_fence();
-#pragma unroll
-    for (int c = 0; c < NCH; ++c)
-        __hip_atomic_fetch_add(&cnt[g.cls[c]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    wave_lds_fence();
-    {
-        const uint32_t k = lane < kClasses ? cnt[lane] : 0u;
-        const uint32_t start = wave_scan_dpp(k) - k;
-        if (lane < kClasses) cnt[lane] = start;
-    }
-    wave_lds_fence();
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const uint32_t pos = __hip_atomic_fetch_add(&cnt[g.cls[c]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        perm[pos] = (uint16_t)((uint32_t)(c * 64 + lane) | (g.code[c] << 8));
-    }
-    wave_lds_fence();
-    // every LDS-DMA of this wave must have landed before the window is read
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-    // ---- NCH class-sorted passes, coordinates parked over their descriptors ---
-    bool bad = false;
-#pragma unroll
-    for (int t = 0; t < NCH; ++t) {
-        const uint32_t e = perm[t * 64 + lane];
-        const uint32_t s = e & 0xffu;
-        desc[s] = hash_slot<SHAPE, HT>(args, lw, g.staged, g.mybase, s, e >> 8, desc[s], bad);
-    }
-    wave_lds_fence();
-
-    // ---- coalesced stores in slot order ------------------------------------
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const uint32_t s = (uint32_t)(c * 64 + lane);
-        if (s < g.ns) __builtin_nontemporal_store(desc[s], args.coords + g.q0 + s);
-    }
-    if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
-}
-
-// The same groups, the slots class-sorted over the whole workgroup (4 waves,
-// 4 * NCH * 64 slots) instead of one wave: a pass then runs one or two
-// CityHash regimes instead of three to five.  Every byte is already in the
-// workgroup's LDS, so a wave may hash any wave's slot; three barriers per
-// workgroup (counts published; permutation and every window landed; parked
-// coordinates complete).  A wave whose group is not staged hashes its own
-// slots from global memory before the first barrier and takes no part in the
-// sort.
-template <int NCH, uint32_t WB>
-__global__ void __launch_bounds__(256)
-hash_wgstage_kernel(const BatchArgs args) {
-    static_assert(NCH >= 1 && NCH <= 2 && WB % 16 == 0, "slot ids are 9 bits");
-    constexpr uint32_t SL = NCH * 64;  // slots per wave
-    __shared__ __attribute__((aligned(16))) uint8_t win_all[4][WB + 64];
-    __shared__ uint64_t desc_all[4 * SL];  // {absolute window offset, length}; then the parked coordinate
-    __shared__ uint16_t perm[4 * SL];      // workgroup slot | code << 9, in class order
-    __shared__ uint32_t wcnt[4][kClasses]; // per wave: staged slots per class
-    const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
-    uint64_t* desc = desc_all + w * SL;
-    const ldsw_t lw_all = as_ldsw(&win_all[0][0]);
-    const uint32_t win_off = (uint32_t)w * (WB + 64);
-
-    const uint64_t o0 = ((uint64_t)blockIdx.x * 4 + w) * args.K;
-    const bool live = o0 < args.n;  // (every wave reaches every barrier)
-    Group<NCH> g{};
-    if (live) g = describe_group<NCH, WB, 0>(args, o0, win_all[w], win_off, desc);
-    const bool sorted = live && g.staged;
-    bool bad = false;
-    if (live && !g.staged) {  // hashed here, from global memory, in slot order
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            const uint32_t s = (uint32_t)(c * 64 + lane);
-            desc[s] = hash_slot<0>(args, lw_all, false, g.mybase, s, g.code[c], desc[s], bad);
-        }
-    }
-    // per-class counts of this wave's staged slots
-    uint32_t mine[kClasses];
-#pragma unroll
-    for (int k = 0; k < kClasses; ++k) {
-        uint32_t n = 0;
-#pragma unroll
-        for (int c = 0; c < NCH; ++c)
-            n += (uint32_t)__popcll(__ballot(sorted && (uint32_t)(c * 64 + lane) < g.ns && g.cls[c] == (uint32_t)k));
-        mine[k] = n;
-    }
-    if (lane < kClasses) {
-        uint32_t v = 0;
-#pragma unroll
-        for (int k = 0; k < kClasses; ++k) v = lane == k ? mine[k] : v;
-        wcnt[w][lane] = v;
-    }
-    __syncthreads();  // (1) counts published, descriptors written
-
-    // class bases over the workgroup, and this wave's offset inside each class
-    uint32_t tot = 0, before = 0;  // lane k < kClasses: class k's total, waves < w's share
-    if (lane < kClasses) {
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-            const uint32_t x = wcnt[v][lane];
-            tot += x;
-            before += v < w ? x : 0u;
-        }
-    }
-    const uint32_t cbase = wave_scan_dpp(tot) - tot;  // lanes >= kClasses add 0
-    const uint32_t T = __builtin_amdgcn_readlane(cbase + tot, kClasses - 1);
-    const uint32_t start = cbase + before;  // lane k: this wave's first position in class k
-    uint32_t seen[kClasses];  // per class: this wave's next position (read with every lane active:
-#pragma unroll                // a ds_bpermute from an inactive lane returns 0)
-    for (int k = 0; k < kClasses; ++k) seen[k] = (uint32_t)__shfl((int)start, k, 64);
-    if (sorted) {
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            const uint32_t s = (uint32_t)(c * 64 + lane);
-            const bool in = s < g.ns;
-#pragma unroll
-            for (int k = 0; k < kClasses; ++k) {
-                const uint64_t m = __ballot(in && g.cls[c] == (uint32_t)k);
-                if (in && g.cls[c] == (uint32_t)k) {
-                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    const uint32_t pos = seen[k] + rank;
-                    perm[pos] = (uint16_t)((uint32_t)(w * SL + s) | (g.code[c] << 9));
-                }
-                seen[k] += (uint32_t)__popcll(m);
-            }
-        }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's window has landed
-    __syncthreads();  // (2) permutation complete, every window landed
-
-    // passes of 64 class-sorted slots of the workgroup: wave w takes w, w+4, ...
-    const uint32_t passes = (T + 63) / 64;
-    for (uint32_t p = (uint32_t)w; p < passes; p += 4) {
-        const uint32_t idx = p * 64 + (uint32_t)lane;
-        if (idx < T) {
-            const uint32_t e = perm[idx];
-            const uint32_t gs = e & 0x1ffu, cd = e >> 9;
-            desc_all[gs] = hash_slot<0>(args, lw_all, true, 0, gs, cd, desc_all[gs], bad);
-        }
-    }
-    __syncthreads();  // (3) every parked coordinate written
-
-    if (live) {
-#pragma unroll
-        for (int c = 0; c < NCH; ++c) {
-            const uint32_t s = (uint32_t)(c * 64 + lane);
-            if (s < g.ns) __builtin_nontemporal_store(desc[s], args.coords + g.q0 + s);
-        }
-    }
-    if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
-}
-
-template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, bool HT = false>
-static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
-    // lane o holds object o's base and lane K the next group's first: K <= 63
-    args.K = std::min<uint32_t>(std::min<uint32_t>((uint32_t)(64 * NCH) / args.A, KCAP), 63u);
-    if (args.K == 0) return hipErrorInvalidValue;
-    const uint64_t waves = (args.n + args.K - 1) / args.K;
-    const uint64_t blocks = (waves + 3) / 4;
-    if (blocks == 0) return hipSuccess;
-    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
-    return hipGetLastError();
-}
-
-template <int NCH, uint32_t WB>
-static hipError_t launch_wgstage_t(BatchArgs args, hipStream_t stream) {
-    args.K = std::min<uint32_t>((uint32_t)(64 * NCH) / args.A, 63u);
-    if (args.K == 0) return hipErrorInvalidValue;
-    const uint64_t waves = (args.n + args.K - 1) / args.K;
-    const uint64_t blocks = (waves + 3) / 4;
-    if (blocks == 0) return hipSuccess;
-    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_wgstage_kernel<NCH, WB>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
-    return hipGetLastError();
-}
-
-// form: 0 = 2 passes / 10 KiB windows; 1 = 3 / 14 KiB; 2 = 2 / 8 KiB;
-// 3 = 1 / 5 KiB; 4 = 4 / 18 KiB; 5 = 2 / 8832 B (four workgroups per CU);
-// 6 = form 5 with at most 6 objects per wave.  A wider schema than the form's
-// passes hold (K = 0) returns hipErrorInvalidValue.
-hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int form) {
+hipError_t launch_hash_wstage_product(const BatchArgs& args, hipStream_t stream) {
     if (args.n == 0) return hipSuccess;
-    switch (form) {
-        case 0: return launch_wstage_t<2, 10240>(args, stream);
-        case 1: return launch_wstage_t<3, 14336>(args, stream);
-        case 2: return launch_wstage_t<2, 8192>(args, stream);
-        case 3: return launch_wstage_t<1, 5120>(args, stream);
-        case 4: return launch_wstage_t<4, 18432>(args, stream);
-        case 5: return launch_wstage_t<2, 8832>(args, stream);
-        case 6: return launch_wstage_t<2, 8832, 6>(args, stream);
-        case 7: return launch_wstage_t<2, 8832, 63, 1>(args, stream);  // debug shape: no hash
-        case 8: return launch_wstage_t<2, 8832, 63, 2>(args, stream);  // debug shape: no DMA
-        case 9: return launch_wstage_t<2, 8832, 3>(args, stream);  // <= 3 objects: per-regime costs on uniform batches
-        // head/tail window hashing (hash_slot_window)
-        case 12: return launch_wstage_t<2, 8832, 63, 0, true>(args, stream);
-        case 13: return launch_wstage_t<2, 8832, 3, 0, true>(args, stream);  // <= 3 objects (per-regime costs)
-        case 14: return launch_wstage_t<3, 14336, 63, 0, true>(args, stream);
-        // the slots class-sorted over the workgroup
-        case 10: return launch_wgstage_t<2, 8832>(args, stream);
-        case 11: return launch_wgstage_t<1, 4352>(args, stream);
-        default: return hipErrorInvalidValue;
-    }
+    return launch_wstage_t<2, 8832, 63, 0, true, 1>(args, stream);
 }
 
 }  // namespace hdx

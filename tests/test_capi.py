@@ -131,7 +131,7 @@ def test_kernel_for_reports_the_auto_policy():
     schema, with no device needed."""
     from hyperdex_amd import synth
     from hyperdex_amd.hashing import kernel_for
-    want = {"cfg1": 12, "cfg2": 21, "cfg3a": 25, "cfg3b": 44, "mixed": 46}
+    want = {"cfg1": 12, "cfg2": 21, "cfg3a": 25, "cfg3b": 212, "mixed": 46}
     for cfg, v in want.items():
         got, name = kernel_for([r.type for r in synth.CONFIGS[cfg]], 10_000_000)
         assert got == v and name.startswith("void hdx::hash_"), (cfg, got, name)
