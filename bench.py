@@ -56,6 +56,10 @@ def parse_args(argv=None):
                     help="ranks (GPUs); default WORLD_SIZE under a launcher, else 1")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup-ms", type=float, default=150.0,
+                    help="after the --warmup launches, keep launching untimed until this much "
+                         "back-to-back device time has passed (the device's clocks settle over "
+                         "the first ~15-40 ms of sustained load, profiles/r3/drift_cfg2.jsonl)")
     ap.add_argument("--config", default="cfg3a")
     ap.add_argument("--objects", type=int, default=0,
                     help="objects per GPU (default 10M; 50M for cfg5, BASELINE config 5)")
@@ -205,7 +209,7 @@ def run_rank(args):
           if cfg != "cfg5" and not args.no_stream_probe else None)
     for _ in range(args.warmup):
         launch()
-    torch.cuda.synchronize()
+    sustained_ms = sustain(launch, stream, args.warmup_ms)
 
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
@@ -244,6 +248,7 @@ def run_rank(args):
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "warmup_sustained_ms": round(sustained_ms, 1),
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
         "scaling": "weak",
@@ -270,8 +275,7 @@ def run_rank(args):
         result["roofline"]["frac_of_probe"] = round(
             achieved / sp.get("read_write_mix_GBps", sp["read_write_1to8_GBps"]), 4)
     if cfg == "cfg5":
-        result["roofline"]["kernel"] = ("void hdx::hash_encoded_kernel<false, true, 0, 32, false, false, false>"
-                                        "(hdx::EncodedArgs)")
+        result["roofline"]["kernel"] = "void hdx::hash_sweep_wstage_kernel<2, 8704u, 6u>(hdx::EncodedArgs)"
     if world > 1 and not args.no_allgather:
         result["allgather"] = time_allgather(coords, world, dev, backend, max_over_ranks)
         # hash phase then the coordinate exchange, back to back
@@ -662,7 +666,33 @@ def write_mix(payload, n, A):
     return max(1, min(4, round(64 * (8 * n * A) / reads / 8))) if reads else 1
 
 
-def time_config(cfg, n, dev, stream, steps=10, warmup=2):
+def sustain(launch, stream, min_ms):
+    """Untimed back-to-back launches until min_ms of device time has passed
+    (returns it).  After idle time the device needs tens of milliseconds of
+    sustained load before its clocks settle: config 2's 0.31-ms launches drift
+    to 0.36-0.44 ms and back over the first ~40 launches, with the kernel or
+    with an unrelated 512 MiB fill between launches alike
+    (scripts/drift_probe.py, profiles/r3/drift_cfg2.jsonl)."""
+    import torch
+    if min_ms <= 0:
+        torch.cuda.synchronize()
+        return 0.0
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record(stream)
+    launch()
+    e.record(stream)
+    torch.cuda.synchronize()
+    one = max(s.elapsed_time(e), 1e-3)
+    reps = max(0, int(np.ceil(min_ms / one)) - 1)
+    s.record(stream)
+    for _ in range(reps):
+        launch()
+    e.record(stream)
+    torch.cuda.synchronize()
+    return one + (s.elapsed_time(e) if reps else 0.0)
+
+
+def time_config(cfg, n, dev, stream, steps=10, warmup=2, warmup_ms=150.0):
     """Device-resident throughput of another config at the same object count:
     HIP events around each launch on the launch stream, as for the main line."""
     import torch
@@ -674,6 +704,7 @@ def time_config(cfg, n, dev, stream, steps=10, warmup=2):
     coords = torch.empty((n, A), dtype=torch.int64, device=dev)
     for _ in range(warmup):
         hdx.hash_batch(types, blob, base, lens, coords=coords, stream=stream)
+    sustain(lambda: hdx.hash_batch(types, blob, base, lens, coords=coords, stream=stream), stream, warmup_ms)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
     torch.cuda.synchronize()
     for s, e in ev:

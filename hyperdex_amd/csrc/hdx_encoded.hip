@@ -417,9 +417,23 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
         case 97: if (a.A <= 32) return launch_hash_encoded_staged(a, 3, 5120, true, stream); break;
         case 98: if (a.A <= 32) return launch_hash_encoded_staged(a, 4, 6144, false, stream); break;
         case 99: if (a.A <= 32) return launch_hash_encoded_staged(a, 15, 20480, true, stream); break;
+        // wave-staged (hdx_wsweep.hip): 230 6 objects / 2 passes, 231 7 objects, 232 11 objects / 3 passes
+        case 230: case 231: case 232: {
+            const hipError_t e = launch_hash_wsweep(a, stream, hash_variant() - 230);
+            if (e != hipErrorInvalidValue) return e;
+            break;
+        }
         default: break;
     }
+    // 49: the gather sweep (the product's sweep up to round 2), for A/B runs
+    if (hash_variant() == 49) return launch_encoded<false, true, 0, 32>(a, stream);
 #endif
+    // the wave-staged sweep (hdx_wsweep.hip): 4.65 vs 5.10 ms per 10 M
+    // config-3b objects, 24.2 vs 25.1 ms at 50 M (profiles/r3/ab_wsweep.jsonl)
+    if (a.coords) {
+        const hipError_t e = launch_hash_wsweep_product(a, stream);
+        if (e != hipErrorInvalidValue) return e;
+    }
     return launch_encoded<false, true, 0, 32>(a, stream);
 }
 

@@ -152,6 +152,12 @@ hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream);
 // The sweep with each group of G objects staged in LDS (hdx_encoded_staged.hip):
 // G objects per wave, A <= 32, an LDS window of WB bytes, class-sorted passes.
 hipError_t launch_hash_encoded_staged(const EncodedArgs& a, int G, uint32_t WB, bool sort, hipStream_t stream);
+// The wave-staged sweep (hdx_wsweep.hip): K objects per wave, keys and values
+// copied into LDS by DMA, the walk and the hashing from LDS; coords != NULL,
+// A <= 64 * passes (else hipErrorInvalidValue).  The product form, and (debug
+// library) its A/B forms.
+hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream);
+hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form);
 // HBM streaming probe (hdx_synth.hip): read `bytes` (write = 1: plus one
 // 8-byte store per 64 bytes read into sink[bytes / 64]).
 hipError_t launch_stream_probe(const uint8_t* src, uint64_t bytes, uint64_t* sink, int write, hipStream_t s);

@@ -784,10 +784,11 @@ static bool known_variant(int v) {
         case 209:  // <= 3 objects per wave (per-regime VALU on uniform batches)
         case 212: case 213: case 214: case 215:  // wave-staged, head/tail window hashing
         case 220: case 221: case 222:  // streamed (hdx_stream.hip)
+        case 230: case 231: case 232:  // wave-staged sweep (hdx_wsweep.hip)
         case 223: case 224: case 225: case 226: case 227:  // its debug shapes (WRONG coordinates)
         case 210: case 211:  // wave-staged, sorted over the workgroup
         case 40: case 41:
-        case 33: case 43: case 47: case 48: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
+        case 33: case 43: case 47: case 48: case 49: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)
             return true;
         default:
             return false;

@@ -1,0 +1,341 @@
+// hdx_wsweep.hip — the wave-staged reindex sweep.
+//
+// hdx_hash_encoded_device's contract (include/hdxhash.h): value i is
+// [u64 BE version][u16 BE count]{[u32 BE len][bytes]}*count
+// (daemon/datalayer_encodings.cc:139-166), decoded as decode_value does
+// (:168-217) and re-hashed with its key (common/hash.cc:56-68).
+//
+// Why this shape.  The gather sweep (hdx_encoded.hip)
+// walks every value's length prefixes from global memory — a chain of
+// dependent loads that touches nearly every line of the value — and then
+// gathers the attributes per lane, so the values cross the fabric twice
+// (raw FETCH 1.2-1.4x the bytes) and every load instruction touches ~64
+// lines.  Here one wave owns K consecutive stored objects, as the wave-staged
+// batch kernel (hdx_wstage.h) does:
+//   1. the K key and value offsets and lengths (+ the next object's offsets,
+//      which bound the spans), coalesced;
+//   2. the objects' keys and values — two spans for a packed store — copied
+//      into the wave's LDS window by coalesced LDS DMA (keys first, values
+//      after; a value span longer than the window is held in part);
+//   3. the prefix walk, lane = object, from LDS (from global memory for a
+//      value the window does not hold), writing a {window offset, length}
+//      descriptor per attribute — the walk costs LDS latency, not HBM round
+//      trips;
+//   4. the wave's K*A slots counting-sorted by CityHash regime, hashed from
+//      the window with head/tail reads (hash_slot_window, hdx_lds_hash.h) in
+//      NCH passes, coordinates parked over their descriptors, one coalesced
+//      store.
+// A slot whose bytes are not in the window (unpacked layouts, the launch's
+// last group, an oversized object) is hashed from global memory, sorted into a
+// class of its own.  Each byte crosses HBM once.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "hdx_lds_hash.h"
+#include "hdx_regroup.h"
+
+namespace hdx {
+namespace {
+
+typedef __attribute__((address_space(3))) void* lds_void_t;
+typedef uint32_t __attribute__((aligned(1))) u32_u;
+typedef uint64_t __attribute__((aligned(1))) u64_u;
+typedef uint16_t __attribute__((aligned(1))) u16_u;
+
+constexpr uint32_t kZero = 0xffffffffu;   // descriptor offset of a slot hashed as 0
+constexpr uint32_t kGlobal = 0x80000000u; // descriptor length bit: hashed from global memory
+constexpr uint32_t kFrontS = 32, kBackS = 64;
+
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int l) {
+    return pack64(__builtin_amdgcn_readlane((uint32_t)v, l), __builtin_amdgcn_readlane((uint32_t)(v >> 32), l));
+}
+__device__ __forceinline__ uint64_t sh64(uint64_t v, int l) {
+    return pack64((uint32_t)__shfl((int)(uint32_t)v, l, 64), (uint32_t)__shfl((int)(uint32_t)(v >> 32), l, 64));
+}
+__device__ __forceinline__ void wave_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// big-endian fields at byte p of global memory / at byte offset o of the window
+__device__ __forceinline__ uint32_t g_be32(const uint8_t* p) {
+    return __builtin_bswap32(*(const __attribute__((address_space(1))) u32_u*)p);
+}
+__device__ __forceinline__ uint64_t g_be64(const uint8_t* p) {
+    return __builtin_bswap64(*(const __attribute__((address_space(1))) u64_u*)p);
+}
+__device__ __forceinline__ uint32_t g_be16(const uint8_t* p) {
+    const uint16_t v = *(const __attribute__((address_space(1))) u16_u*)p;
+    return (uint32_t)(uint16_t)((v >> 8) | (v << 8));
+}
+__device__ __forceinline__ uint32_t w_be32(ldsw_t w, uint32_t o) { return lds_be32(w, o); }
+__device__ __forceinline__ uint64_t w_be64(ldsw_t w, uint32_t o) {
+    return ((uint64_t)lds_be32(w, o) << 32) | lds_be32(w, o + 4);
+}
+__device__ __forceinline__ uint32_t w_be16(ldsw_t w, uint32_t o) { return lds_be32(w, o) >> 16; }
+
+// Sort classes: class 7 = hashed from global memory; > 64-byte strings with
+// 3+ blocks share class 6; otherwise work_class<1>'s order (numerics and
+// zero slots first).
+__device__ __forceinline__ uint32_t sweep_class(uint32_t code, uint32_t n, bool zero, bool global) {
+    if (zero) return 0;
+    if (global) return 7;
+    return std::min<uint32_t>(work_class<1>(code, n, true), 6u);
+}
+
+__device__ __forceinline__ uint64_t hash_global(const uint8_t* p, uint32_t code, uint32_t n, bool& bad) {
+    return hash_blk<false, false, true>(code, p, n, consume_any<true>(issue_any<true>(code, p, n)), bad);
+}
+
+// copy [src, src + bytes) (src 16-byte aligned) to LDS dst: whole 16-byte
+// units by LDS DMA, the last partial unit as dwords (a dword never crosses a
+// page, so nothing past the span's last dword is read)
+__device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint32_t bytes, int lane) {
+    const uint32_t units = bytes >> 4;
+    for (uint32_t u0 = 0; u0 < units; u0 += 64) {
+        const uint32_t u = u0 + (uint32_t)lane;
+        if (u < units) __builtin_amdgcn_global_load_lds((const void*)(src + 16ull * u), (lds_void_t)(dst + 16 * u0), 16, 0, 0);
+    }
+    const uint32_t tdw = ((bytes & 15) + 3) >> 2;
+    if ((uint32_t)lane < tdw)
+        __builtin_amdgcn_global_load_lds((const void*)(src + 16ull * units + 4 * lane), (lds_void_t)(dst + 16 * units), 4, 0, 0);
+}
+
+}  // namespace
+
+// NCH passes of 64 slots; K = min(64 * NCH / A, KCAP) objects per wave; a
+// WB-byte window per wave, four waves per workgroup, no workgroup barrier.
+template <int NCH, uint32_t WB, uint32_t KCAP>
+__global__ void __launch_bounds__(256)
+hash_sweep_wstage_kernel(const EncodedArgs a) {
+    constexpr uint32_t SL = NCH * 64;
+    __shared__ __attribute__((aligned(16))) uint8_t win_all[4][kFrontS + WB + kBackS];
+    __shared__ uint64_t desc_all[4][SL];   // {offset, length | kGlobal}; then the parked coordinate
+    __shared__ uint16_t perm_all[4][SL];   // slot | code << 8, in class order
+    __shared__ uint32_t cnt_all[4][kClasses];
+    __shared__ __attribute__((aligned(4))) uint8_t codes_all[4][SL];
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    uint8_t* win = win_all[w];
+    const ldsw_t lw = as_ldsw(win);
+    uint64_t* desc = desc_all[w];
+    uint16_t* perm = perm_all[w];
+    uint32_t* cnt = cnt_all[w];
+    uint8_t* codes = codes_all[w];
+    const uint32_t A = a.A;
+    const uint32_t K = std::min<uint32_t>(SL / A, KCAP);
+    const uint64_t o0 = ((uint64_t)blockIdx.x * 4 + w) * K;
+    if (o0 >= a.n) return;
+    const uint32_t nobj = (uint32_t)std::min<uint64_t>(K, a.n - o0);
+    const uint32_t ns = nobj * A;
+    const bool has_next = o0 + nobj < a.n;
+
+    // ---- offsets and lengths (lane nobj: the next object's offsets) ---------
+    const bool lv = (uint32_t)lane < nobj || ((uint32_t)lane == nobj && has_next);
+    const uint64_t koff = lv ? a.key_off[o0 + lane] : 0, voff = lv ? a.val_off[o0 + lane] : 0;
+    const uint32_t klen = (uint32_t)lane < nobj ? a.key_len[o0 + lane] : 0u;
+    const uint32_t vlen = (uint32_t)lane < nobj ? a.val_len[o0 + lane] : 0u;
+    // the code table (4 bytes a lane: a per-lane index into the kernel
+    // arguments would become serialized scalar loads)
+    if ((uint32_t)lane * 4 < A && (uint32_t)lane * 4 < SL)
+        reinterpret_cast<uint32_t*>(codes)[lane] = reinterpret_cast<const uint32_t*>(a.codes)[lane];
+
+    // ---- the keys, gathered dword by dword (a store keeps each key in its
+    // own place), then the value span (whatever of it fits) --------------------
+    // lane o < nobj: its key's dwords [kd, kd + kdw) from the key's dword floor
+    const uint64_t kd = (uint64_t)(uintptr_t)(a.keys + koff) >> 2;
+    const uint32_t kdw = (uint32_t)lane < nobj ? ((uint32_t)((uintptr_t)(a.keys + koff) & 3) + klen + 3) >> 2 : 0u;
+    const uint32_t kdx = wave_scan_dpp(kdw) - kdw;  // its first dword in the key region
+    const uint32_t td = __builtin_amdgcn_readlane(kdx + kdw, 63);
+    const bool keys_in = 4 * td <= WB / 4;
+    const uint32_t kreg = keys_in ? (4 * td + 15) & ~15u : 0u;  // the values' region starts 16-byte aligned
+    if (keys_in) {
+        for (uint32_t u0 = 0; u0 < td; u0 += 64) {
+            const uint32_t u = u0 + (uint32_t)lane;
+            // the object whose key holds region dword u (a wave-uniform walk over <= 63 objects)
+            uint64_t src = 0;
+            for (uint32_t o = 0; o < nobj; ++o) {
+                const uint32_t x0 = __builtin_amdgcn_readlane(kdx, (int)o), xn = __builtin_amdgcn_readlane(kdw, (int)o);
+                if (u >= x0 && u < x0 + xn) src = 4 * (rl64(kd, (int)o) + (u - x0));
+            }
+            if (u < td)
+                __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)src, (lds_void_t)(win + kFrontS + 4 * u0), 4, 0, 0);
+        }
+    }
+    const uint64_t v0 = rl64(voff, 0);
+    const uint64_t vend = has_next ? rl64(voff, (int)nobj) : 0;
+    const uint32_t vlead = (uint32_t)((uintptr_t)(a.vals + v0) & 15);
+    const uint32_t vheld = has_next && vend >= v0 ? (uint32_t)std::min<uint64_t>(vlead + (vend - v0), WB - kreg) : 0u;
+    if (vheld) copy_span(a.vals + v0 - vlead, win + kFrontS + kreg, vheld, lane);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the compiler does not order ds_read after LDS DMA
+    wave_fence();
+
+    // ---- decode_value (datalayer_encodings.cc:168-217), lane = object --------
+    bool bad = false, ok = false;
+    if ((uint32_t)lane < nobj) {
+        const uint32_t kw = kFrontS + 4 * kdx + (uint32_t)((uintptr_t)(a.keys + koff) & 3);
+        desc[lane * A] = keys_in ? ((uint64_t)kw | ((uint64_t)klen << 32)) : ((uint64_t)0 | ((uint64_t)(klen | kGlobal) << 32));
+        const uint64_t vrel = voff - v0;
+        const bool vin = voff >= v0 && vlead + vrel + vlen <= vheld;
+        const uint32_t vw = kFrontS + kreg + vlead + (uint32_t)vrel;  // the value's window offset (vin)
+        const uint8_t* vp = a.vals + voff;
+        // the walk, reading the value from the window (vin) or global memory
+        auto walk = [&](auto be16, auto be32, auto be64, uint32_t base, uint32_t gbit) {
+            ok = vlen >= 10;
+            uint64_t version = 0;
+            if (ok) {
+                version = be64(0);
+                ok = be16(8) == A - 1;
+            }
+            uint32_t pos = 10;
+            for (uint32_t k = 0; k + 1 < A; ++k) {
+                uint32_t len = 0;
+                if (ok) {
+                    if (vlen - pos < 4) {
+                        ok = false;
+                    } else {
+                        len = be32(pos);
+                        pos += 4;
+                        if (len > vlen - pos) ok = false;  // the reference does not check this (:201-213)
+                    }
+                }
+                desc[lane * A + 1 + k] = ok ? ((uint64_t)(base + pos) | ((uint64_t)(len | gbit) << 32)) : (uint64_t)kZero;
+                if (ok) pos += len;
+            }
+            return version;
+        };
+        uint64_t version;
+        if (vin) {
+            // branch-free from the window: every step reads inside the value
+            // (pos <= vlen: the window holds the value and 64 bytes after it)
+            ok = vlen >= 10;
+            version = w_be64(lw, vw);
+            ok = ok && w_be16(lw, vw + 8) == A - 1;
+            uint32_t pos = 10;
+            uint64_t* dp = desc + lane * A + 1;
+#pragma unroll 4
+            for (uint32_t k = 0; k + 1 < A; ++k) {
+                const uint32_t len = w_be32(lw, vw + pos);
+                const uint32_t room = vlen - pos;  // >= 0 while ok
+                ok = ok && room >= 4 && len <= room - 4;
+                dp[k] = ok ? ((uint64_t)(vw + pos + 4) | ((uint64_t)len << 32)) : (uint64_t)kZero;
+                pos = ok ? pos + 4 + len : pos;
+            }
+        } else
+            version = walk([&](uint32_t o) { return g_be16(vp + o); }, [&](uint32_t o) { return g_be32(vp + o); },
+                           [&](uint32_t o) { return g_be64(vp + o); }, 0u, kGlobal);
+        if (!ok)  // undecodable: every coordinate of the object is 0
+            for (uint32_t j = 0; j < A; ++j) desc[lane * A + j] = (uint64_t)kZero;
+        if (a.versions) a.versions[o0 + lane] = ok ? version : 0;
+    }
+    const bool any_bad = __any((uint32_t)lane < nobj && !ok);
+    wave_fence();
+
+    // ---- counting sort of the slots by class (wave-local) -------------------
+    uint32_t cls[NCH], cd[NCH];
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const uint32_t s = (uint32_t)(c * 64 + lane);
+        const bool valid = s < ns;
+        const uint64_t d = valid ? desc[s] : (uint64_t)kZero;
+        const uint32_t j = s - div_small(s, a.a_magic) * A;
+        const bool zero = (uint32_t)d == kZero;
+        const uint32_t ln = (uint32_t)(d >> 32);
+        cd[c] = valid && !zero ? (uint32_t)codes[j] : (uint32_t)CODE_ZERO;
+        cls[c] = sweep_class(cd[c], ln & ~kGlobal, !valid || zero, (ln & kGlobal) != 0);
+    }
+    if (lane < kClasses) cnt[lane] = 0;
+    wave_fence();
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) __hip_atomic_fetch_add(&cnt[cls[c]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    wave_fence();
+    {
+        const uint32_t k = lane < kClasses ? cnt[lane] : 0u;
+        const uint32_t start = wave_scan_dpp(k) - k;
+        if (lane < kClasses) cnt[lane] = start;
+    }
+    wave_fence();
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const uint32_t p = __hip_atomic_fetch_add(&cnt[cls[c]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        perm[p] = (uint16_t)((uint32_t)(c * 64 + lane) | (cd[c] << 8));
+    }
+    wave_fence();
+
+    // ---- NCH class-sorted passes, coordinates parked over their descriptors ---
+#pragma unroll
+    for (int t = 0; t < NCH; ++t) {
+        const uint32_t e = perm[t * 64 + lane];
+        const uint32_t s = e & 0xffu, code = e >> 8;
+        const uint64_t d = desc[s];
+        const uint32_t obj = div_small(s, a.a_magic);
+        const uint32_t j = s - obj * A;
+        const uint32_t off = (uint32_t)d, ln = (uint32_t)(d >> 32);
+        // the object bases of slots hashed from global memory, by shuffle with
+        // every lane active (a ds_bpermute from an inactive lane reads 0):
+        // both, before any branch, and only when the pass has such a slot
+        uint64_t ob = 0;
+        if (__any(s < ns && off != kZero && (ln & kGlobal) != 0)) {
+            const uint64_t kb = sh64(koff, (int)(obj & 63)), vb = sh64(voff, (int)(obj & 63));
+            asm volatile("" ::"v"(kb), "v"(vb));
+            ob = j == 0 ? kb : vb;
+        }
+        uint64_t h = 0;
+        if (s < ns && off != kZero) {
+            if (ln & kGlobal) h = hash_global((j == 0 ? a.keys : a.vals) + ob + off, code, ln & ~kGlobal, bad);
+            else h = hash_slot_window(lw, code, off, ln, bad);
+        }
+        desc[s] = h;
+    }
+    wave_fence();
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const uint32_t s = (uint32_t)(c * 64 + lane);
+        if (s < ns) __builtin_nontemporal_store(desc[s], a.coords + o0 * A + s);
+    }
+    if (a.status && lane == 0 && any_bad) atomicOr(a.status, 1u << 6 /* HDX_E_BADENC */);
+    if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
+}
+
+template <int NCH, uint32_t WB, uint32_t KCAP>
+static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
+    const uint32_t K = std::min<uint32_t>(64 * NCH / a.A, KCAP);
+    if (K == 0) return hipErrorInvalidValue;
+    const uint64_t waves = (a.n + K - 1) / K;
+    const uint64_t blocks = (waves + 3) / 4;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+    return hipGetLastError();
+}
+
+// The product form: 2 passes, 6 objects per wave, 8.5 KiB windows (four
+// workgroups of four waves per CU).  coords must be set (the fused region
+// form stays on hdx_encoded.hip); A <= 128.
+hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream) {
+    if (a.n == 0) return hipSuccess;
+    if (!a.coords) return hipErrorInvalidValue;
+    return launch_wsweep_t<2, 8704, 6>(a, stream);
+}
+
+#ifndef HDX_DEBUG_BUILD
+#define HDX_DEBUG_BUILD 0
+#endif
+#if HDX_DEBUG_BUILD
+// A/B forms (debug library): 0 = the product's, 1 = 7 objects, 2 = 3 passes / 11 objects / 14 KiB
+hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form) {
+    if (a.n == 0) return hipSuccess;
+    if (!a.coords) return hipErrorInvalidValue;
+    switch (form) {
+        case 0: return launch_wsweep_t<2, 8704, 6>(a, stream);
+        case 1: return launch_wsweep_t<2, 8704, 7>(a, stream);
+        case 2: return launch_wsweep_t<3, 14336, 11>(a, stream);
+        default: return hipErrorInvalidValue;
+    }
+}
+#endif
+
+}  // namespace hdx
