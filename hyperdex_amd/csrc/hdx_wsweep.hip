@@ -35,6 +35,7 @@
 #include <algorithm>
 
 #include "hdx_lds_hash.h"
+#include "hdx_region_lookup.h"
 #include "hdx_regroup.h"
 
 namespace hdx {
@@ -109,7 +110,11 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
 
 // NCH passes of 64 slots; K = min(64 * NCH / A, KCAP) objects per wave; a
 // WB-byte window per wave, four waves per workgroup, no workgroup barrier.
-template <int NCH, uint32_t WB, uint32_t KCAP>
+// REGIONS (hdx_hash_encoded_regions_device): every object is then looked up
+// in the a.T region tables (configuration::lookup_region, hdx_region_lookup.h:
+// the interval index, or the scan), lane = object, from the coordinates
+// parked in LDS; coordinates are stored only when a.coords is set.
+template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false>
 __global__ void __launch_bounds__(256)
 hash_sweep_wstage_kernel(const EncodedArgs a) {
     constexpr uint32_t SL = NCH * 64;
@@ -292,31 +297,54 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         desc[s] = h;
     }
     wave_fence();
+    if (!REGIONS || a.coords) {
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const uint32_t s = (uint32_t)(c * 64 + lane);
-        if (s < ns) __builtin_nontemporal_store(desc[s], a.coords + o0 * A + s);
+        for (int c = 0; c < NCH; ++c) {
+            const uint32_t s = (uint32_t)(c * 64 + lane);
+            if (s < ns) __builtin_nontemporal_store(desc[s], a.coords + o0 * A + s);
+        }
+    }
+    if constexpr (REGIONS) {
+        // the tables in a wave-uniform loop (a table's fields are scalar loads)
+        for (uint32_t t = 0; t < a.T; ++t) {
+            const SweepTable& tb = a.t[t];
+            if ((uint32_t)lane < nobj) {
+                const uint64_t* po = desc + lane * A;
+                uint64_t r;
+                if (tb.index) {
+                    r = lookup_indexed_fn(tb.index, tb.W, tb.D, [&](uint32_t d) { return po[tb.attrs[d]]; }, tb.ids);
+                } else {
+                    uint64_t h[kMaxLookupDims];
+#pragma unroll
+                    for (uint32_t d = 0; d < kMaxLookupDims; ++d)
+                        if (d < tb.D) h[d] = po[tb.attrs[d]];
+                    r = lookup_scan(tb.lower, tb.upper, tb.ids, tb.R, tb.D, h);
+                }
+                tb.out[o0 + lane] = r;
+            }
+        }
     }
     if (a.status && lane == 0 && any_bad) atomicOr(a.status, 1u << 6 /* HDX_E_BADENC */);
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <int NCH, uint32_t WB, uint32_t KCAP>
+template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false>
 static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
     const uint32_t K = std::min<uint32_t>(64 * NCH / a.A, KCAP);
     if (K == 0) return hipErrorInvalidValue;
     const uint64_t waves = (a.n + K - 1) / K;
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
 // The product form: 2 passes, 6 objects per wave, 8.5 KiB windows (four
-// workgroups of four waves per CU).  coords must be set (the fused region
-// form stays on hdx_encoded.hip); A <= 128.
+// workgroups of four waves per CU); with a.T tables the fused region lookup
+// (coords may then be NULL).  A <= 128.
 hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
+    if (a.T) return launch_wsweep_t<2, 8704, 6, true>(a, stream);
     if (!a.coords) return hipErrorInvalidValue;
     return launch_wsweep_t<2, 8704, 6>(a, stream);
 }

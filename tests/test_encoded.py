@@ -261,11 +261,21 @@ def test_gpu_encoded_bad_numeric_size(oracle, variant):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("variant", [-1, 49])
 @pytest.mark.parametrize("with_coords", [False, True])
-def test_gpu_encoded_regions_fused(oracle, with_coords):
+def test_gpu_encoded_regions_fused(oracle, with_coords, variant):
     """hdx_hash_encoded_regions_device = the sweep's coordinates looked up in
     every table (an indexed 64-region key grid, an indexed 3-attribute grid,
-    and a 300-region table that is scanned), corrupt values included."""
+    and a 300-region table that is scanned), corrupt values included; the
+    product's wave-staged form and (49) the gather sweep's fused form."""
+    if variant >= 0:
+        with _lib.debug_library(variant):
+            _encoded_regions_fused(oracle, with_coords)
+    else:
+        _encoded_regions_fused(oracle, with_coords)
+
+
+def _encoded_regions_fused(oracle, with_coords):
     import torch
 
     import hyperdex_amd as hdx
