@@ -377,13 +377,13 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
     // wave or over groups of 2 / 4 passes, 16 / 32 objects per wave, and a
     // lane-per-object walk-and-hash kernel — all slower
     if (a.T) {
-        // the wave-staged sweep with the lookup fused (hdx_wsweep.hip); the
-        // gather sweep's fused form below stays for A/B runs (47, 49) and for
-        // schemas of more than 128 attributes
-        if (!(HDX_DEBUG_BUILD && (hash_variant() == 47 || hash_variant() == 49))) {
-            const hipError_t e = launch_hash_wsweep_product(a, stream);
-            if (e != hipErrorInvalidValue) return e;
-        }
+        // the gather sweep's fused form: 27.3 ms at 50 M objects and the two
+        // tables of bench.py vs 28.5 for the wave-staged sweep with the lookup
+        // fused (debug 233: its 6 objects per wave make the lookups' L2 round
+        // trips the wave's tail; profiles/r3/ab_fused_sweep.jsonl)
+#if HDX_DEBUG_BUILD
+        if (hash_variant() == 233) return launch_hash_wsweep_product(a, stream);
+#endif
         // stage each indexed table (index + ids) in LDS while they fit in 16 KiB together
         uint32_t words = 0;
         for (uint32_t t = 0; t < a.T; ++t) {

@@ -26,6 +26,13 @@ typedef __attribute__((address_space(3))) uint32_t* ldsw_mut_t;
 
 __device__ __forceinline__ ldsw_t as_ldsw(const void* p) { return (ldsw_t)p; }
 
+// 16 bytes at a dword-aligned LDS address as one ds_read_b128 (gfx950 serves
+// dword-aligned b128 reads; the compiler emits them for 4-byte-aligned
+// vectors).  W128 forms below read 4 dwords per instruction instead of 2.
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef u32x4_t __attribute__((aligned(4))) u32x4_a4;
+__device__ __forceinline__ u32x4_t lds_q(ldsw_t d) { return *(const __attribute__((address_space(3))) u32x4_a4*)d; }
+
 // little-endian u32 at byte offset b of the window (any alignment)
 __device__ __forceinline__ uint32_t lds_u32(ldsw_t w, uint32_t b) {
     const ldsw_t d = w + (b >> 2);
@@ -76,8 +83,25 @@ __device__ __forceinline__ Blk lds_block64(ldsw_t w, uint32_t s) {
     return use64<true>(b, s & 3);
 }
 
+__device__ __forceinline__ Blk lds_block64_w128(ldsw_t w, uint32_t s) {
+    const ldsw_t d = w + (s >> 2);
+    const u32x4_t q0 = lds_q(d), q1 = lds_q(d + 4), q2 = lds_q(d + 8), q3 = lds_q(d + 12);
+    Blk64 b;
+    b.b.v0.x = pack64(q0.x, q0.y);
+    b.b.v0.y = pack64(q0.z, q0.w);
+    b.b.v1.x = pack64(q1.x, q1.y);
+    b.b.v1.y = pack64(q1.z, q1.w);
+    b.b.v2.x = pack64(q2.x, q2.y);
+    b.b.v2.y = pack64(q2.z, q2.w);
+    b.b.v3.x = pack64(q3.x, q3.y);
+    b.b.v3.y = pack64(q3.z, q3.w);
+    b.e = d[16];
+    return use64<true>(b, s & 3);
+}
+
 // city.cc:361-397 for n > 64: the tail block t in registers, the loop blocks
 // read from the window (city_gt64_reg's arithmetic).
+template <bool W128 = false>
 __device__ __forceinline__ uint64_t city_gt64_lds(ldsw_t w, uint32_t off, uint32_t n, const Blk& t) {
     const u64x2 e0 = t.v0, e1 = t.v1, e2 = t.v2, e3 = t.v3;
     uint64_t x = e1.y;
@@ -87,7 +111,7 @@ __device__ __forceinline__ uint64_t city_gt64_lds(ldsw_t w, uint32_t off, uint32
     weak32(e0.x, e0.y, e1.x, e1.y, n, z, v0, v1);
     weak32(e2.x, e2.y, e3.x, e3.y, y + K1, x, w0, w1);
     const uint32_t blocks = (n - 1) >> 6;
-    Blk b = lds_block64(w, off);
+    Blk b = W128 ? lds_block64_w128(w, off) : lds_block64(w, off);
     x = x * K1 + b.v0.x;
     for (uint32_t k = 0;;) {
         x = ror(x + y + v0 + b.v0.y, 37) * K1;
@@ -101,7 +125,7 @@ __device__ __forceinline__ uint64_t city_gt64_lds(ldsw_t w, uint32_t off, uint32
         v0 = nv0; v1 = nv1; w0 = nw0; w1 = nw1;
         const uint64_t tt = z; z = x; x = tt;
         if (++k == blocks) break;
-        b = lds_block64(w, off + 64 * k);
+        b = W128 ? lds_block64_w128(w, off + 64 * k) : lds_block64(w, off + 64 * k);
     }
     return mix16(mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z, mix16(v1, w1, KMUL) + x, KMUL);
 }
@@ -137,12 +161,20 @@ __device__ __forceinline__ uint64_t hash_numeric_lds(ldsw_t w, uint32_t code, ui
 struct Q32 {
     uint64_t q0, q1, q2, q3;
 };
+template <bool W128 = false>
 __device__ __forceinline__ Q32 lds_read32(ldsw_t w, uint32_t o) {
     const ldsw_t d = w + (o >> 2);
     const uint32_t r = o & 3;
     uint32_t x[9];
+    if constexpr (W128) {
+        const u32x4_t a = lds_q(d), b = lds_q(d + 4);
+        x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
+        x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+        x[8] = d[8];
+    } else {
 #pragma unroll
-    for (int i = 0; i < 9; ++i) x[i] = d[i];
+        for (int i = 0; i < 9; ++i) x[i] = d[i];
+    }
     Q32 q;
     q.q0 = pack64(__builtin_amdgcn_alignbyte(x[1], x[0], r), __builtin_amdgcn_alignbyte(x[2], x[1], r));
     q.q1 = pack64(__builtin_amdgcn_alignbyte(x[3], x[2], r), __builtin_amdgcn_alignbyte(x[4], x[3], r));
@@ -179,20 +211,21 @@ __device__ __forceinline__ uint64_t city_le16_ht(uint64_t h0, uint64_t t3, uint3
 // HashLen0to16 / 17to32 / 33to64 / the > 64-byte tail block) and, over 64
 // bytes, the loop blocks.  The window needs 32 readable bytes before off
 // (s[n-32, n) of a short string) and 36 after the value's end.
+template <bool W128 = false>
 __device__ __forceinline__ uint64_t hash_slot_window(ldsw_t w, uint32_t code, uint32_t off, uint32_t n, bool& bad) {
     if (code == CODE_STRING) {
-        const Q32 t = lds_read32(w, off + n - 32);  // s[n-32, n): the front pad covers n < 32
+        const Q32 t = lds_read32<W128>(w, off + n - 32);  // s[n-32, n): the front pad covers n < 32
         const u64x2 t01 = {t.q0, t.q1}, t23 = {t.q2, t.q3};
         if (n > 64) {
-            const Q32 u = lds_read32(w, off + n - 64);
+            const Q32 u = lds_read32<W128>(w, off + n - 64);
             Blk b;
             b.v0 = u64x2{u.q0, u.q1};
             b.v1 = u64x2{u.q2, u.q3};
             b.v2 = t01;
             b.v3 = t23;
-            return city_gt64_lds(w, off, n, b);
+            return city_gt64_lds<W128>(w, off, n, b);
         }
-        const Q32 h = lds_read32(w, off);  // s[0, 32): the back pad covers n < 32
+        const Q32 h = lds_read32<W128>(w, off);  // s[0, 32): the back pad covers n < 32
         const u64x2 h01 = {h.q0, h.q1};
         if (n > 32) return city_33to64(h01, u64x2{h.q2, h.q3}, t01, t23, n);
         if (n > 16) return city_17to32(h01, t23, n);

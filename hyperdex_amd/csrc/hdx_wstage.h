@@ -172,12 +172,12 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
 // regime from the same two reads; lw then points kFrontHT bytes before the
 // window).
 constexpr uint32_t kFrontHT = 32;
-template <int SHAPE, bool HT = false>
+template <int SHAPE, bool HT = false, bool W128 = false>
 __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, bool staged, uint64_t mybase,
                                               uint32_t s, uint32_t cd, uint64_t d, bool& bad) {
     const uint32_t doff = (uint32_t)d, dn = (uint32_t)(d >> 32);
     if (SHAPE == 1) return lw[doff >> 2] ^ dn;
-    if (staged && HT) return hash_slot_window(lw, cd, doff + kFrontHT, dn, bad);
+    if (staged && HT) return hash_slot_window<W128>(lw, cd, doff + kFrontHT, dn, bad);
     if (staged) return cd == CODE_STRING ? hash_string_lds(lw, doff, dn) : hash_numeric_lds(lw, cd, doff, dn, bad);
     const uint32_t o = div_small(s, args.a_magic);
     const uint64_t ob = shfl64(mybase, (int)(o & 63));
@@ -189,7 +189,7 @@ __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, 
 // wave; WB-byte windows.  SHAPE (debug variants 207/208 only, WRONG
 // coordinates): 1 = everything but the hash (one LDS dword per slot instead);
 // 2 = no DMA (the hash runs on whatever the window holds).
-template <int NCH, uint32_t WB, int SHAPE = 0, bool HT = false, int ORDER = 1>
+template <int NCH, uint32_t WB, int SHAPE = 0, bool HT = false, int ORDER = 1, bool W128 = false>
 __global__ void __launch_bounds__(256)
 hash_wstage_kernel(const BatchArgs args) {
     static_assert(NCH >= 1 && NCH <= 4 && WB % 16 == 0, "slot indices are 8 bits; windows whole DMA units");
@@ -237,7 +237,7 @@ hash_wstage_kernel(const BatchArgs args) {
     for (int t = 0; t < NCH; ++t) {
         const uint32_t e = perm[t * 64 + lane];
         const uint32_t s = e & 0xffu;
-        desc[s] = hash_slot<SHAPE, HT>(args, lw, g.staged, g.mybase, s, e >> 8, desc[s], bad);
+        desc[s] = hash_slot<SHAPE, HT, W128>(args, lw, g.staged, g.mybase, s, e >> 8, desc[s], bad);
     }
     wave_lds_fence();
 
@@ -259,7 +259,7 @@ hash_wstage_kernel(const BatchArgs args) {
 // slots from global memory before the first barrier and takes no part in the
 // sort.
 
-template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, bool HT = false, int ORDER = 1>
+template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, bool HT = false, int ORDER = 1, bool W128 = false>
 static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     // lane o holds object o's base and lane K the next group's first: K <= 63
     args.K = std::min<uint32_t>(std::min<uint32_t>((uint32_t)(64 * NCH) / args.A, KCAP), 63u);
@@ -268,7 +268,7 @@ static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
     return hipGetLastError();
 }
 

@@ -261,7 +261,7 @@ def test_gpu_encoded_bad_numeric_size(oracle, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [-1, 49])
+@pytest.mark.parametrize("variant", [-1, 233])
 @pytest.mark.parametrize("with_coords", [False, True])
 def test_gpu_encoded_regions_fused(oracle, with_coords, variant):
     """hdx_hash_encoded_regions_device = the sweep's coordinates looked up in
