@@ -55,6 +55,7 @@ hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int for
 // Its product form (hdx_wstage.hip): two passes per wave, head/tail hashing;
 // A <= 128 (else hipErrorInvalidValue).
 hipError_t launch_hash_wstage_product(const BatchArgs& args, hipStream_t stream);
+hipError_t launch_hash_wstage_regions(const BatchArgs& args, hipStream_t stream);  // + args.T tables
 // Streamed hash (hdx_stream.hip): one persistent workgroup per CU walks its
 // objects in batches staged in LDS by DMA a batch ahead, slots class-sorted
 // over the workgroup; A <= 64 (else hipErrorInvalidValue).

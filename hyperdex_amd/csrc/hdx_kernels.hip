@@ -57,7 +57,8 @@ static int auto_variant(const BatchArgs& args);
 // unsorted chunks (the tables then fit in LDS beside the descriptors: 1.97 vs
 // 2.66 ms with 16 chunks and the tables in global memory, config 3a), 2 below
 // 32 M slots (config 1: 0.158 vs 0.178 ms with 8); numeric-heavy 4 unsorted;
-// complex types 8 sorted; mixed strings 3 sorted with A4 loads (config 3b:
+// complex types 8 sorted; mixed strings (round 3) the wave-staged kernel with
+// the lookup fused, before that 3 sorted chunks with A4 loads (config 3b:
 // 3.83 vs 4.26 ms with 2; profiles/r1/fused_batch_regions.jsonl,
 // profiles/r2/ab_fused.jsonl).  A <= 128 (checked by the caller).
 hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream) {
@@ -65,12 +66,17 @@ hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream) 
 #if HDX_DEBUG_BUILD
     const int v = hash_variant();
     if (v >= 100 && v < 120) return launch_fused_debug(args, stream, v);  // hdx_kernels_dbg.hip
+    if (v == 217) return launch_hash_wstage_regions(args, stream);
 #endif
     switch (auto_variant(args)) {
         case 25: case 20: return launch_regroup_regions<8, false, false, false, 0, true>(args, stream);
         case 12: return launch_regroup_regions<2, false, false, false, 0, true>(args, stream);
         case 21: return launch_regroup_regions<4, false, false, false, 0, true>(args, stream);
         case 46: return launch_regroup_regions<8, true, false, true, 1, true>(args, stream);
+        // mixed strings: the wave-staged kernel with the lookup fused (3.68 vs
+        // 3.81 ms, config 3b, 10 M objects, bench.py's two tables;
+        // profiles/r3/ab_fused_batch.jsonl)
+        case 212: return launch_hash_wstage_regions(args, stream);
         default: return launch_regroup_regions<3, true, true, true, 1, true>(args, stream);
     }
 }
@@ -158,7 +164,7 @@ const char* variant_kernel_name(int v) {
         case 44: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true, 1>(hdx::BatchArgs)";
         case 45: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true, 2>(hdx::BatchArgs)";
         case 46: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, true, 1>(hdx::BatchArgs)";
-        case 212: return "void hdx::hash_wstage_kernel<2, 8832u, 0, true, 1>(hdx::BatchArgs)";
+        case 212: return "void hdx::hash_wstage_kernel<2, 8832u, 0, true, 1, false, false>(hdx::BatchArgs)";
         default: return "";
     }
 }

@@ -783,6 +783,7 @@ static bool known_variant(int v) {
         case 207: case 208:  // its debug shapes: no hash / no DMA (WRONG coordinates)
         case 209:  // <= 3 objects per wave (per-regime VALU on uniform batches)
         case 212: case 213: case 214: case 215: case 216:  // wave-staged, head/tail window hashing
+        case 217:  // wave-staged with the fused region lookup (hdx_hash_batch_regions_device)
         case 220: case 221: case 222:  // streamed (hdx_stream.hip)
         case 230: case 231: case 232: case 233:  // wave-staged sweep (hdx_wsweep.hip; 233: fused regions)
         case 223: case 224: case 225: case 226: case 227:  // its debug shapes (WRONG coordinates)

@@ -39,6 +39,7 @@
 #include <algorithm>
 
 #include "hdx_lds_hash.h"
+#include "hdx_region_lookup.h"
 #include "hdx_regroup.h"
 
 namespace hdx {
@@ -189,7 +190,10 @@ __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, 
 // wave; WB-byte windows.  SHAPE (debug variants 207/208 only, WRONG
 // coordinates): 1 = everything but the hash (one LDS dword per slot instead);
 // 2 = no DMA (the hash runs on whatever the window holds).
-template <int NCH, uint32_t WB, int SHAPE = 0, bool HT = false, int ORDER = 1, bool W128 = false>
+// REGIONS (hdx_hash_batch_regions_device): the wave's objects are then looked
+// up in the args.T region tables from their coordinates parked in LDS
+// (lookup_tables_wave), coordinates stored only when args.coords is set.
+template <int NCH, uint32_t WB, int SHAPE = 0, bool HT = false, int ORDER = 1, bool W128 = false, bool REGIONS = false>
 __global__ void __launch_bounds__(256)
 hash_wstage_kernel(const BatchArgs args) {
     static_assert(NCH >= 1 && NCH <= 4 && WB % 16 == 0, "slot indices are 8 bits; windows whole DMA units");
@@ -242,11 +246,15 @@ hash_wstage_kernel(const BatchArgs args) {
     wave_lds_fence();
 
     // ---- coalesced stores in slot order ------------------------------------
+    if (!REGIONS || args.coords) {
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const uint32_t s = (uint32_t)(c * 64 + lane);
-        if (s < g.ns) __builtin_nontemporal_store(desc[s], args.coords + g.q0 + s);
+        for (int c = 0; c < NCH; ++c) {
+            const uint32_t s = (uint32_t)(c * 64 + lane);
+            if (s < g.ns) __builtin_nontemporal_store(desc[s], args.coords + g.q0 + s);
+        }
     }
+    if constexpr (REGIONS)  // the window is free now: the lookups' scratch
+        lookup_tables_wave(args.t, args.T, desc, args.A, g.nobj, o0, reinterpret_cast<uint64_t*>(win), wave_lds_fence);
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
@@ -259,7 +267,8 @@ hash_wstage_kernel(const BatchArgs args) {
 // slots from global memory before the first barrier and takes no part in the
 // sort.
 
-template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, bool HT = false, int ORDER = 1, bool W128 = false>
+template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, bool HT = false, int ORDER = 1, bool W128 = false,
+          bool REGIONS = false>
 static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     // lane o holds object o's base and lane K the next group's first: K <= 63
     args.K = std::min<uint32_t>(std::min<uint32_t>((uint32_t)(64 * NCH) / args.A, KCAP), 63u);
@@ -268,7 +277,7 @@ static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
     return hipGetLastError();
 }
 

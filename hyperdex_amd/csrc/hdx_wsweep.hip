@@ -304,79 +304,8 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
             if (s < ns) __builtin_nontemporal_store(desc[s], a.coords + o0 * A + s);
         }
     }
-    if constexpr (REGIONS) {
-        // configuration::lookup_region per table.  Indexed tables: one lane per
-        // (object, table dimension) searches that dimension's interval and
-        // parks its mask words in the (now free) window; then one lane per
-        // (object, table) ANDs them — a few dependent round trips for all the
-        // tables instead of ~3 per dimension one after another on 6 lanes.
-        // Scanned tables (or more than 64 searches): lane = object, in turn.
-        uint32_t P = 0;
-        bool all_indexed = true;
-        for (uint32_t t = 0; t < a.T; ++t) {
-            P += a.t[t].D;
-            all_indexed &= a.t[t].index != nullptr;
-        }
-        uint64_t* mk = reinterpret_cast<uint64_t*>(win);  // [nobj][P][4]
-        if (all_indexed && nobj * P <= 64) {
-            if ((uint32_t)lane < nobj * P) {
-                const uint32_t o = (uint32_t)lane / P, p = (uint32_t)lane - o * P;
-                uint32_t t = 0, d = p;
-                while (d >= a.t[t].D) d -= a.t[t++].D;
-                const SweepTable& tb = a.t[t];
-                const uint64_t hv = desc[o * A + tb.attrs[d]];
-                const uint64_t hdr = tb.index[d];
-                const uint64_t* B = tb.index + ((hdr >> 16) & 0xffffff);
-                const uint16_t* start = reinterpret_cast<const uint16_t*>(B - kIndexBucketWords);
-                const uint32_t b = (uint32_t)(hv >> 56);
-                uint32_t pos = start[b], cnt = start[b + 1] - pos;
-                while (cnt) {
-                    const uint32_t half = cnt >> 1;
-                    if (B[pos + half] <= hv) {
-                        pos += half + 1;
-                        cnt -= half + 1;
-                    } else {
-                        cnt = half;
-                    }
-                }
-                const uint64_t* mask = tb.index + (hdr >> 40) + (size_t)pos * tb.W;
-#pragma unroll
-                for (uint32_t w = 0; w < 4; ++w) mk[(o * P + p) * 4 + w] = w < tb.W ? mask[w] : 0;
-            }
-            wave_fence();
-            if ((uint32_t)lane < nobj * a.T) {
-                const uint32_t o = (uint32_t)lane / a.T, t = (uint32_t)lane - o * a.T;
-                uint32_t p0 = 0;
-                for (uint32_t u = 0; u < t; ++u) p0 += a.t[u].D;
-                const SweepTable& tb = a.t[t];
-                uint64_t acc[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-                for (uint32_t d = 0; d < tb.D; ++d)
-#pragma unroll
-                    for (uint32_t w = 0; w < 4; ++w) acc[w] &= mk[(o * P + p0 + d) * 4 + w];
-                uint64_t r = 0;
-#pragma unroll
-                for (int w = 3; w >= 0; --w)
-                    if ((uint32_t)w < tb.W && acc[w]) r = tb.ids[64 * w + __builtin_ctzll(acc[w])];
-                tb.out[o0 + o] = r;
-            }
-        } else if ((uint32_t)lane < nobj) {
-            const uint64_t* po = desc + lane * A;
-            for (uint32_t t = 0; t < a.T; ++t) {
-                const SweepTable& tb = a.t[t];
-                uint64_t r;
-                if (tb.index) {
-                    r = lookup_indexed_fn(tb.index, tb.W, tb.D, [&](uint32_t d) { return po[tb.attrs[d]]; }, tb.ids);
-                } else {
-                    uint64_t h[kMaxLookupDims];
-#pragma unroll
-                    for (uint32_t d = 0; d < kMaxLookupDims; ++d)
-                        if (d < tb.D) h[d] = po[tb.attrs[d]];
-                    r = lookup_scan(tb.lower, tb.upper, tb.ids, tb.R, tb.D, h);
-                }
-                tb.out[o0 + lane] = r;
-            }
-        }
-    }
+    if constexpr (REGIONS)  // the window is free now: the lookups' scratch
+        lookup_tables_wave(a.t, a.T, desc, A, nobj, o0, reinterpret_cast<uint64_t*>(win), wave_fence);
     if (a.status && lane == 0 && any_bad) atomicOr(a.status, 1u << 6 /* HDX_E_BADENC */);
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }

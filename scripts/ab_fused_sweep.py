@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--objects", type=int, default=50_000_000)
     ap.add_argument("--variants", default="-1,49")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--batch", default="", help="a batch config (cfg3b, ...): time hdx_hash_batch_regions_device instead")
     a = ap.parse_args()
     import torch
 
@@ -24,7 +25,12 @@ def main():
     import hyperdex_amd as hdx
     from hyperdex_amd import _lib, synth
     dev = torch.device("cuda", 0)
-    types, *enc = synth.make_encoded_device("cfg3b", a.objects, device=dev)
+    if a.batch:
+        types, *enc = synth.make_batch_device(a.batch, a.objects, device=dev)
+        run = lambda tables: hdx.hash_batch_regions(types, *enc, tables)  # noqa: E731
+    else:
+        types, *enc = synth.make_encoded_device("cfg3b", a.objects, device=dev)
+        run = lambda tables: hdx.hash_encoded_regions(types, *enc, tables, coords=False)  # noqa: E731
     A = len(types)
     tables = bench.key_subspace_tables(A)
     variants = [int(v) for v in a.variants.split(",")]
@@ -37,7 +43,7 @@ def main():
                 ctx.__enter__()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
-            ids = hdx.hash_encoded_regions(types, *enc, tables, coords=False)
+            ids = run(tables)
             e.record()
             torch.cuda.synchronize()
             if ctx:
@@ -51,7 +57,7 @@ def main():
             times[v].append(s.elapsed_time(e))
     for v in variants:
         t = np.array(times[v])
-        print(json.dumps({"fused_sweep_variant": v, "objects": a.objects, "ms_median": round(float(np.median(t)), 3),
+        print(json.dumps({"fused": a.batch or "cfg5 sweep", "variant": v, "objects": a.objects, "ms_median": round(float(np.median(t)), 3),
                           "ms_min": round(float(t.min()), 3)}), flush=True)
 
 

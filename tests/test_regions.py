@@ -217,7 +217,7 @@ def test_gpu_batch_regions_fused(oracle, cfg, n, with_coords):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("form", list(range(100, 112)))
+@pytest.mark.parametrize("form", list(range(100, 112)) + [217])
 def test_gpu_batch_regions_every_fused_form(oracle, form):
     """The debug library's fused forms (hdx_kernels_dbg.hip launch_fused_debug:
     chunks per wave, sorted or not, tables in LDS or global memory, the
