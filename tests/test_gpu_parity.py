@@ -118,6 +118,20 @@ def test_attribute_counts(oracle, torch_dev, A):
     check_batch(oracle, torch, dev, types, blob, base, lens)
 
 
+@pytest.mark.parametrize("A", [2, 3, 17, 63, 64, 65, 100, 128, 129, 200])
+def test_mixed_attribute_counts(oracle, torch_dev, A):
+    """Mixed string / int64 / float schemas go through the product's
+    wave-staged kernel up to 128 attributes (one object per wave at 65..128:
+    objects straddle its passes), the gather kernel above."""
+    torch, dev = torch_dev
+    kinds = [synth.Rule(dt.HYPERDATATYPE_STRING, synth.UNIFORM, 0, 150),
+             synth.Rule(dt.HYPERDATATYPE_INT64, synth.NUMERIC, 8, 8),
+             synth.Rule(dt.HYPERDATATYPE_FLOAT, synth.NUMERIC, 8, 8)]
+    rules = [kinds[j % 3] for j in range(A)]
+    types, blob, base, lens = synth.make_batch_host(rules, 301, seed=555 + A)
+    check_batch(oracle, torch, dev, types, blob, base, lens)
+
+
 def test_every_string_length_and_alignment(oracle, torch_dev):
     """Lengths 0..520 at every byte alignment 0..15 (all CityHash regimes and
     1..8 iterations of the 64-byte loop)."""
