@@ -71,6 +71,20 @@ __global__ void __launch_bounds__(256) k_lds(uint32_t* out, uint32_t seed) {
                 asm volatile("ds_read_b64 %0, %2\n\tds_read_b64 %1, %2 offset:8\n\ts_waitcnt lgkmcnt(0)"
                              : "=v"(p), "=v"(q) : "v"(ak));
                 acc ^= p.x ^ p.y ^ q.x ^ q.y;
+            } else if constexpr (V == 6) {  // b128 at the dword floor (4-byte aligned, not 16)
+                uint4 v;
+                asm volatile("ds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(ak & ~3u));
+                acc ^= v.x ^ v.y ^ v.z ^ v.w;
+            } else if constexpr (V == 7) {  // 2 x b64 at the dword floor
+                uint2 p, q;
+                asm volatile("ds_read_b64 %0, %2\n\tds_read_b64 %1, %2 offset:8\n\ts_waitcnt lgkmcnt(0)"
+                             : "=v"(p), "=v"(q) : "v"(ak & ~3u));
+                acc ^= p.x ^ p.y ^ q.x ^ q.y;
+            } else if constexpr (V == 8) {  // b64 at the 8-byte floor
+                uint2 p, q;
+                asm volatile("ds_read_b64 %0, %2\n\tds_read_b64 %1, %2 offset:8\n\ts_waitcnt lgkmcnt(0)"
+                             : "=v"(p), "=v"(q) : "v"(ak & ~7u));
+                acc ^= p.x ^ p.y ^ q.x ^ q.y;
             }
         }
         off = (off + 61 * (acc & 7) + 64) & (kWin - 1);
@@ -114,6 +128,9 @@ int main() {
     run<2>("r2b32u", out, blocks, cus);
     run<4>("b32a+alignbyte", out, blocks, cus);
     run<5>("b64u", out, blocks, cus);
+    run<6>("b128 dword-aligned", out, blocks, cus);
+    run<7>("2 x b64 dword-aligned", out, blocks, cus);
+    run<8>("2 x b64 8-byte-aligned", out, blocks, cus);
     CK(hipFree(out));
     return 0;
 }
