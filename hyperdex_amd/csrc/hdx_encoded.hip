@@ -377,13 +377,34 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
     // wave or over groups of 2 / 4 passes, 16 / 32 objects per wave, and a
     // lane-per-object walk-and-hash kernel — all slower
     if (a.T) {
-        // the gather sweep's fused form: 27.3 ms at 50 M objects and the two
-        // tables of bench.py vs 28.5 for the wave-staged sweep with the lookup
-        // fused (debug 233: its 6 objects per wave make the lookups' L2 round
-        // trips the wave's tail; profiles/r3/ab_fused_sweep.jsonl)
+        // the wave-staged sweep, then one lookup launch per table (chunked
+        // through scratch when the caller wants no coordinates): 25.8 ms at
+        // 50 M objects and the two tables of bench.py vs 27.3 for the gather
+        // sweep's fused form (debug 234, and below kRegionLookupMinObjects)
+        // and 28.5 for the wave-staged sweep with the lookup fused (debug 233:
+        // its 6 objects per wave make the lookups' L2 round trips the wave's
+        // tail; profiles/r3/ab_fused_sweep.jsonl, ab_regions_by_lookup.jsonl)
+        if (a.A <= kWsweepMaxAttrs && regions_by_lookup_pays(a.n)) {
 #if HDX_DEBUG_BUILD
-        if (hash_variant() == 233) return launch_hash_wsweep_product(a, stream);
+            if (hash_variant() == 233) return launch_hash_wsweep_product(a, stream);
+            if (hash_variant() != 234)
 #endif
+            {
+                const RegionHashFn hash = [&](uint64_t first, uint64_t count, uint64_t* c) {
+                    EncodedArgs b = a;
+                    b.key_off += first;
+                    b.key_len += first;
+                    b.val_off += first;
+                    b.val_len += first;
+                    if (b.versions) b.versions += first;
+                    b.n = count;
+                    b.coords = c;
+                    b.T = 0;
+                    return launch_hash_wsweep_product(b, stream);
+                };
+                return regions_by_lookup(a.n, a.A, a.t, a.T, a.coords, hash, stream);
+            }
+        }
         // stage each indexed table (index + ids) in LDS while they fit in 16 KiB together
         uint32_t words = 0;
         for (uint32_t t = 0; t < a.T; ++t) {

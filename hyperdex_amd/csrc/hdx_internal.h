@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <functional>
 #include <vector>
 
 #include "../../include/hdxhash.h"
@@ -98,6 +99,25 @@ struct RegionArgs {
 
 hipError_t launch_lookup_region(const RegionArgs& a, hipStream_t stream);
 
+// Region ids by hash + one lookup launch per table instead of a fused kernel
+// (hdx_regions.hip), for the VALU-bound hash kernels whose fused epilogue
+// costs more than the coordinates' round trip through HBM — from
+// kRegionLookupMinObjects objects (below, the one launch of the fused form
+// wins: the daemon shim's batches).  hash(first, count, c) hashes objects
+// [first, first + count) into c.  With coords, all n objects are hashed there
+// first; without, chunks of at most kRegionChunkBytes of coordinates go
+// through a stream-ordered scratch buffer (hipMallocAsync; each chunk pays a
+// launch tail: config 3b 4.59 / 3.72 / 3.52 ms with 16 / 64 / 256 MiB chunks,
+// 3.47 unchunked, profiles/r3/ab_regions_by_lookup.jsonl).
+// Debug variant 235: by lookup at any n, 64 MiB chunks (tests).
+using RegionHashFn = std::function<hipError_t(uint64_t first, uint64_t count, uint64_t* coords)>;
+constexpr uint64_t kRegionChunkBytes = 4ull << 30;
+constexpr uint64_t kRegionLookupMinObjects = 1ull << 20;
+bool regions_by_lookup_pays(uint64_t n);
+uint64_t regions_chunk_objects(uint64_t n, uint32_t A);
+hipError_t regions_by_lookup(uint64_t n, uint32_t A, const SweepTable* t, uint32_t T, uint64_t* coords,
+                             const RegionHashFn& hash, hipStream_t stream);
+
 // Several subspaces at once (the batcher's prev/this/next lookups): table t's
 // region ids for object i go to out[t * out_stride + i].
 constexpr uint32_t kMaxMultiTables = 16;
@@ -157,6 +177,7 @@ hipError_t launch_hash_encoded_staged(const EncodedArgs& a, int G, uint32_t WB, 
 // copied into LDS by DMA, the walk and the hashing from LDS; coords != NULL,
 // A <= 64 * passes (else hipErrorInvalidValue).  The product form, and (debug
 // library) its A/B forms.
+constexpr uint32_t kWsweepMaxAttrs = 128;
 hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream);
 hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form);
 // HBM streaming probe (hdx_synth.hip): read `bytes` (write = 1: plus one

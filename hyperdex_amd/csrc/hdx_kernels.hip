@@ -57,8 +57,8 @@ static int auto_variant(const BatchArgs& args);
 // unsorted chunks (the tables then fit in LDS beside the descriptors: 1.97 vs
 // 2.66 ms with 16 chunks and the tables in global memory, config 3a), 2 below
 // 32 M slots (config 1: 0.158 vs 0.178 ms with 8); numeric-heavy 4 unsorted;
-// complex types 8 sorted; mixed strings (round 3) the wave-staged kernel with
-// the lookup fused, before that 3 sorted chunks with A4 loads (config 3b:
+// complex types 8 sorted; mixed strings (round 3) the wave-staged kernel and
+// separate lookups, before that 3 sorted chunks with A4 loads (config 3b:
 // 3.83 vs 4.26 ms with 2; profiles/r1/fused_batch_regions.jsonl,
 // profiles/r2/ab_fused.jsonl).  A <= 128 (checked by the caller).
 hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream) {
@@ -73,10 +73,26 @@ hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream) 
         case 12: return launch_regroup_regions<2, false, false, false, 0, true>(args, stream);
         case 21: return launch_regroup_regions<4, false, false, false, 0, true>(args, stream);
         case 46: return launch_regroup_regions<8, true, false, true, 1, true>(args, stream);
-        // mixed strings: the wave-staged kernel with the lookup fused (3.68 vs
-        // 3.81 ms, config 3b, 10 M objects, bench.py's two tables;
-        // profiles/r3/ab_fused_batch.jsonl)
-        case 212: return launch_hash_wstage_regions(args, stream);
+        // mixed strings: the wave-staged kernel is VALU-bound, so a fused
+        // epilogue costs more than the coordinates' round trip (config 3b,
+        // 10 M objects, bench.py's two tables: fused 3.66 ms (debug 217),
+        // hash + separate lookups 3.47; profiles/r3/ab_fused_batch.jsonl):
+        // hash, then one lookup launch per table (chunked through scratch when
+        // the caller wants no coordinates); small batches keep the one fused
+        // launch (debug 217's kernel)
+        case 212: {
+            if (!regions_by_lookup_pays(args.n)) return launch_hash_wstage_regions(args, stream);
+            const RegionHashFn hash = [&](uint64_t first, uint64_t count, uint64_t* c) {
+                BatchArgs b = args;
+                b.obj_base += first;
+                b.attr_len += first * args.A;
+                b.n = count;
+                b.coords = c;
+                b.T = 0;
+                return launch_hash_wstage_product(b, stream);
+            };
+            return regions_by_lookup(args.n, args.A, args.t, args.T, args.coords, hash, stream);
+        }
         default: return launch_regroup_regions<3, true, true, true, 1, true>(args, stream);
     }
 }

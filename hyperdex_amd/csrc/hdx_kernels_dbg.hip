@@ -786,7 +786,8 @@ static bool known_variant(int v) {
         case 217:  // wave-staged with the fused region lookup (hdx_hash_batch_regions_device)
         case 218:  // debug shape of 212: no hash (WRONG coordinates)
         case 220: case 221: case 222:  // streamed (hdx_stream.hip)
-        case 230: case 231: case 232: case 233:  // wave-staged sweep (hdx_wsweep.hip; 233: fused regions)
+        case 230: case 231: case 232: case 233: case 234:  // wave-staged sweep (hdx_wsweep.hip; 233: fused regions; 234: the gather sweep's fused regions)
+        case 235:  // regions by hash + separate lookups at any n, 64 MiB chunks (hdx_regions.hip)
         case 223: case 224: case 225: case 226: case 227:  // its debug shapes (WRONG coordinates)
         case 210: case 211:  // wave-staged, sorted over the workgroup
         case 40: case 41:

@@ -18,6 +18,10 @@
 #include "hdx_internal.h"
 #include "hdx_region_lookup.h"
 
+#ifndef HDX_DEBUG_BUILD
+#define HDX_DEBUG_BUILD 0
+#endif
+
 namespace hdx {
 
 // ---------------------------------------------------------------------------
@@ -153,6 +157,57 @@ hipError_t launch_lookup_region(const RegionArgs& a, hipStream_t stream) {
         hipLaunchKernelGGL(lookup_region_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0, stream, a);
     }
     return hipGetLastError();
+}
+
+bool regions_by_lookup_pays(uint64_t n) {
+#if HDX_DEBUG_BUILD
+    if (hash_variant() == 235) return true;
+#endif
+    return n >= kRegionLookupMinObjects;
+}
+
+uint64_t regions_chunk_objects(uint64_t n, uint32_t A) {
+    uint64_t bytes = kRegionChunkBytes;
+#if HDX_DEBUG_BUILD
+    if (hash_variant() == 235) bytes = 64ull << 20;  // tests: several chunks at small n
+#endif
+    return std::min<uint64_t>(n, std::max<uint64_t>(1, bytes / (8ull * A)));
+}
+
+hipError_t regions_by_lookup(uint64_t n, uint32_t A, const SweepTable* t, uint32_t T, uint64_t* coords,
+                             const RegionHashFn& hash, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint64_t chunk = coords ? n : regions_chunk_objects(n, A);
+    uint64_t* scratch = nullptr;
+    hipError_t e = hipSuccess;
+    if (!coords && (e = hipMallocAsync((void**)&scratch, chunk * A * 8, stream)) != hipSuccess) return e;
+    for (uint64_t first = 0; first < n && e == hipSuccess; first += chunk) {
+        const uint64_t count = std::min(chunk, n - first);
+        uint64_t* c = coords ? coords + first * A : scratch;
+        if ((e = hash(first, count, c)) != hipSuccess) break;
+        for (uint32_t k = 0; k < T && e == hipSuccess; ++k) {
+            RegionArgs r{};
+            r.lower = t[k].lower;
+            r.upper = t[k].upper;
+            r.ids = t[k].ids;
+            r.index = t[k].index;
+            r.W = t[k].W;
+            r.index_words = t[k].index_words;
+            r.coords = c;
+            r.out = t[k].out + first;
+            r.n = count;
+            r.A = A;
+            r.D = t[k].D;
+            r.R = t[k].R;
+            std::memcpy(r.attrs, t[k].attrs, sizeof r.attrs);
+            e = launch_lookup_region(r, stream);
+        }
+    }
+    if (scratch) {
+        const hipError_t f = hipFreeAsync(scratch, stream);
+        if (e == hipSuccess) e = f;
+    }
+    return e;
 }
 
 // One lane per (table, object): small batches from the daemon shim, where a

@@ -323,8 +323,8 @@ static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
 
 // The product form: 2 passes, 6 objects per wave, 8.5 KiB windows (four
 // workgroups of four waves per CU).  With a.T tables, the fused region lookup
-// (coords may then be NULL): debug variant 233 only — the gather sweep's fused
-// form is faster (hdx_encoded.hip).  A <= 128.
+// (coords may then be NULL): debug variant 233 only — the sweep + separate
+// lookups is faster (hdx_encoded.hip).  A <= kWsweepMaxAttrs.
 hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
     if (a.T) return launch_wsweep_t<2, 8704, 6, true>(a, stream);

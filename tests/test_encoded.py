@@ -261,13 +261,14 @@ def test_gpu_encoded_bad_numeric_size(oracle, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [-1, 233])
+@pytest.mark.parametrize("variant", [-1, 233, 234])
 @pytest.mark.parametrize("with_coords", [False, True])
 def test_gpu_encoded_regions_fused(oracle, with_coords, variant):
     """hdx_hash_encoded_regions_device = the sweep's coordinates looked up in
     every table (an indexed 64-region key grid, an indexed 3-attribute grid,
     and a 300-region table that is scanned), corrupt values included; the
-    product's wave-staged form and (49) the gather sweep's fused form."""
+    product (the wave-staged sweep + separate lookups), the wave-staged sweep
+    with the lookup fused (233) and the gather sweep's fused form (234)."""
     if variant >= 0:
         with _lib.debug_library(variant):
             _encoded_regions_fused(oracle, with_coords)
@@ -300,5 +301,52 @@ def _encoded_regions_fused(oracle, with_coords):
         assert np.array_equal(ids[k].cpu().numpy().view(np.uint64), want), k
     if with_coords:
         assert np.array_equal(coords.cpu().numpy().view(np.uint64), want_coords)
+    for t in tables:
+        t.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["chunks", "product"])
+@pytest.mark.parametrize("with_coords", [False, True])
+def test_gpu_encoded_regions_by_lookup(oracle, case, with_coords):
+    """The product's regions sweep from 2^20 objects on is the wave-staged
+    sweep + separate lookups (hdx_regions.hip regions_by_lookup).  "chunks":
+    debug variant 235 (by lookup at any n, 64 MiB of scratch per chunk when no
+    coordinates are wanted): 100 attributes -> 83 886 objects per chunk, so
+    200 003 stored objects are 3 chunks, the last one ragged.  "product": the
+    product library past its threshold.  Versions and the status word follow
+    the chunks."""
+    import contextlib
+
+    import torch
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import RegionTable
+    dev = torch.device("cuda", 0)
+    rules = [synth.Rule(synth.dt.HYPERDATATYPE_STRING, synth.UNIFORM, 0, 40),
+             synth.Rule(synth.dt.HYPERDATATYPE_INT64, synth.NUMERIC, 8, 8)] * 50
+    if case == "chunks":
+        n, attrs3 = 200_003, [1, 2, 99]
+    else:
+        rules, n, attrs3 = rules[:2] + rules[:1], (1 << 20) + 4097, [1, 2, 0]
+    types, blob, base, lens = synth.make_batch_host(rules, n, seed=78)
+    enc = synth.encode_values_host(types, blob, base, lens, first_version=3)
+    want_coords, want_versions, _ = oracle.hash_encoded(types, *enc)
+    specs = [([0],) + tuple(oracle.partition(1, 64)), (attrs3,) + tuple(oracle.partition(3, 64))]
+    tables = [RegionTable(at, lo, up, np.arange(1, len(lo) + 1, dtype=np.uint64) * 11) for at, lo, up in specs]
+    versions = torch.empty(n, dtype=torch.int64, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    with _lib.debug_library(235) if case == "chunks" else contextlib.nullcontext():
+        out = hdx.hash_encoded_regions(types, *_to_dev(torch, dev, enc), tables, coords=with_coords,
+                                       versions=versions, status=status)
+        torch.cuda.synchronize()
+    ids, coords = out if with_coords else (out, None)
+    for k, (at, lo, up) in enumerate(specs):
+        want = oracle.lookup_region(at, lo, up, np.arange(1, len(lo) + 1, dtype=np.uint64) * 11, want_coords)
+        assert np.array_equal(ids[k].cpu().numpy().view(np.uint64), want), k
+    if with_coords:
+        assert np.array_equal(coords.cpu().numpy().view(np.uint64), want_coords)
+    assert np.array_equal(versions.cpu().numpy().view(np.uint64), want_versions)
+    assert int(status.item()) == 0
     for t in tables:
         t.close()

@@ -1,7 +1,11 @@
 """Region lookup (configuration::lookup_region): oracle semantics
 on CPU, GPU kernel vs oracle on partition() grids and adversarial tables."""
+import contextlib
+
 import numpy as np
 import pytest
+
+from hyperdex_amd import synth
 
 U64MAX = np.uint64(0xffffffffffffffff)
 
@@ -209,6 +213,49 @@ def test_gpu_batch_regions_fused(oracle, cfg, n, with_coords):
     ids, coords = out if with_coords else (out, None)
     for k, (at, lo, up) in enumerate(specs):
         want = oracle.lookup_region(at, lo, up, np.arange(1, len(lo) + 1, dtype=np.uint64) * 3, want_coords)
+        assert np.array_equal(ids[k].cpu().numpy().view(np.uint64), want), k
+    if with_coords:
+        assert np.array_equal(coords.cpu().numpy().view(np.uint64), want_coords)
+    for t in tables:
+        t.close()
+
+
+WIDE_MIXED = ([synth.Rule(synth.dt.HYPERDATATYPE_STRING, synth.UNIFORM, 0, 40),
+               synth.Rule(synth.dt.HYPERDATATYPE_INT64, synth.NUMERIC, 8, 8)] * 50)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["chunks", "product"])
+@pytest.mark.parametrize("with_coords", [False, True])
+def test_gpu_batch_regions_by_lookup(oracle, case, with_coords):
+    """Large mixed-schema batches take hash + separate lookups (hdx_kernels.hip
+    case 212, hdx_regions.hip regions_by_lookup).  "chunks": debug variant 235
+    (by lookup at any n, 64 MiB of scratch per chunk when no coordinates are
+    wanted): 100 attributes -> 83 886 objects per chunk, so 200 003 objects are
+    3 chunks, the last one ragged.  "product": the product library from its
+    threshold (2^20 objects) on."""
+    import torch
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import RegionTable, _lib
+    dev = torch.device("cuda", 0)
+    if case == "chunks":
+        rules, n, attrs3 = WIDE_MIXED, 200_003, [1, 2, 99]
+    else:
+        rules, n, attrs3 = WIDE_MIXED[:2] + WIDE_MIXED[:1], (1 << 20) + 4097, [1, 2, 0]
+    types, blob, base, lens = synth.make_batch_host(rules, n, seed=77)
+    assert hdx.hashing.kernel_for(types, n)[0] == 212
+    want_coords, _ = oracle.hash_batch(types, blob, base, lens)
+    specs = [([0],) + tuple(oracle.partition(1, 64)), (attrs3,) + tuple(oracle.partition(3, 64))]
+    tables = [RegionTable(at, lo, up, np.arange(1, len(lo) + 1, dtype=np.uint64) * 5) for at, lo, up in specs]
+    with _lib.debug_library(235) if case == "chunks" else contextlib.nullcontext():
+        out = hdx.hash_batch_regions(types, torch.from_numpy(blob).to(dev),
+                                     torch.from_numpy(base.view(np.int64)).to(dev),
+                                     torch.from_numpy(lens.view(np.int32)).to(dev), tables, coords=with_coords)
+        torch.cuda.synchronize()
+    ids, coords = out if with_coords else (out, None)
+    for k, (at, lo, up) in enumerate(specs):
+        want = oracle.lookup_region(at, lo, up, np.arange(1, len(lo) + 1, dtype=np.uint64) * 5, want_coords)
         assert np.array_equal(ids[k].cpu().numpy().view(np.uint64), want), k
     if with_coords:
         assert np.array_equal(coords.cpu().numpy().view(np.uint64), want_coords)
