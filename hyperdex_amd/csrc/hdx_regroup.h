@@ -127,6 +127,60 @@ __device__ __forceinline__ uint32_t work_class3(uint32_t code, uint32_t n, bool 
     return n > 32 ? 0u : n <= 16 ? 1u : 2u;
 }
 
+// Wave-local counting sort of a wave's NCH * 64 slots by work class into
+// perm[] (slot | code << 8, pass t = perm[64 t .. 64 t + 63]); slots s >= ns
+// are pads (hashed as CODE_ZERO, results unused).  A pass pays for the union
+// of the CityHash regimes its lanes hold, so with GAP (NCH == 2) the class
+// that would straddle the pass boundary is moved whole into the second pass
+// when there are pads enough to fill the first pass's rest: that pass then
+// skips the class's regime code (config 3b: the <= 16 / 17..32 regime;
+// config 5's sweep: the first > 64-byte loop).  Without GAP (or without pads
+// enough) pads follow the last class.  fence(): the wave's LDS fence.
+template <int NCH, bool GAP, class Fence>
+__device__ __forceinline__ void class_sort(uint32_t* cnt, uint16_t* perm, const uint32_t (&cls)[NCH],
+                                           const uint32_t (&code)[NCH], uint32_t ns, Fence fence) {
+    const int lane = threadIdx.x & 63;
+    if (lane < kClasses) cnt[lane] = 0;
+    fence();
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+        if ((uint32_t)(c * 64 + lane) < ns)
+            __hip_atomic_fetch_add(&cnt[cls[c]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    fence();
+    uint32_t gap = 0, gap_at = 0;  // wave-uniform
+    {
+        const uint32_t k = lane < kClasses ? cnt[lane] : 0u;
+        uint32_t start = wave_scan_dpp(k) - k;
+        if constexpr (GAP && NCH == 2) {
+            const uint64_t cross = __ballot(lane < kClasses && start < 64 && start + k > 64);
+            if (cross) {
+                const int x = (int)__builtin_ctzll(cross);
+                const uint32_t sx = __builtin_amdgcn_readlane(start, x);
+                if (64 - sx <= NCH * 64 - ns) {
+                    gap = 64 - sx;
+                    gap_at = sx;
+                    if (lane >= x) start += gap;
+                }
+            }
+        }
+        if (lane < kClasses) cnt[lane] = start;
+    }
+    fence();
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+        const uint32_t s = (uint32_t)(c * 64 + lane);
+        uint32_t pos;
+        if (s < ns) {
+            pos = __hip_atomic_fetch_add(&cnt[cls[c]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        } else {
+            const uint32_t p = s - ns;  // pad p: the first `gap` fill the first pass, the rest follow the classes
+            pos = p < gap ? gap_at + p : ns + p;
+        }
+        perm[pos] = (uint16_t)(s | (code[c] << 8));
+    }
+    fence();
+}
+
 
 // ===========================================================================
 // Regroup kernel (variants 18/19/26/35/37 sorted with C = 4/8/2/2/2; 20/21/25

@@ -193,7 +193,10 @@ __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, 
 // REGIONS (hdx_hash_batch_regions_device): the wave's objects are then looked
 // up in the args.T region tables from their coordinates parked in LDS
 // (lookup_tables_wave), coordinates stored only when args.coords is set.
-template <int NCH, uint32_t WB, int SHAPE = 0, bool HT = false, int ORDER = 1, bool W128 = false, bool REGIONS = false>
+// GAP: the class straddling the pass boundary moves whole into the second
+// pass when pads allow (class_sort, hdx_regroup.h).
+template <int NCH, uint32_t WB, int SHAPE = 0, bool HT = false, int ORDER = 1, bool W128 = false, bool REGIONS = false,
+          bool GAP = false>
 __global__ void __launch_bounds__(256)
 hash_wstage_kernel(const BatchArgs args) {
     static_assert(NCH >= 1 && NCH <= 4 && WB % 16 == 0, "slot indices are 8 bits; windows whole DMA units");
@@ -214,24 +217,7 @@ hash_wstage_kernel(const BatchArgs args) {
     const Group<NCH> g = describe_group<NCH, WB, SHAPE, ORDER>(args, o0, win, 0, desc);
 
     // ---- counting sort by work class (wave-local) --------------------------
-    if (lane < kClasses) cnt[lane] = 0;
-    wave_lds_fence();
-#pragma unroll
-    for (int c = 0; c < NCH; ++c)
-        __hip_atomic_fetch_add(&cnt[g.cls[c]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    wave_lds_fence();
-    {
-        const uint32_t k = lane < kClasses ? cnt[lane] : 0u;
-        const uint32_t start = wave_scan_dpp(k) - k;
-        if (lane < kClasses) cnt[lane] = start;
-    }
-    wave_lds_fence();
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const uint32_t pos = __hip_atomic_fetch_add(&cnt[g.cls[c]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        perm[pos] = (uint16_t)((uint32_t)(c * 64 + lane) | (g.code[c] << 8));
-    }
-    wave_lds_fence();
+    class_sort<NCH, GAP>(cnt, perm, g.cls, g.code, g.ns, wave_lds_fence);
     // every LDS-DMA of this wave must have landed before the window is read
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
@@ -268,7 +254,7 @@ hash_wstage_kernel(const BatchArgs args) {
 // sort.
 
 template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, bool HT = false, int ORDER = 1, bool W128 = false,
-          bool REGIONS = false>
+          bool REGIONS = false, bool GAP = false>
 static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     // lane o holds object o's base and lane K the next group's first: K <= 63
     args.K = std::min<uint32_t>(std::min<uint32_t>((uint32_t)(64 * NCH) / args.A, KCAP), 63u);
@@ -277,7 +263,7 @@ static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
     return hipGetLastError();
 }
 

@@ -114,7 +114,9 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
 // in the a.T region tables (configuration::lookup_region, hdx_region_lookup.h:
 // the interval index, or the scan), lane = object, from the coordinates
 // parked in LDS; coordinates are stored only when a.coords is set.
-template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false>
+// GAP: the class straddling the pass boundary moves whole into the second
+// pass when pads allow (class_sort, hdx_regroup.h).
+template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false>
 __global__ void __launch_bounds__(256)
 hash_sweep_wstage_kernel(const EncodedArgs a) {
     constexpr uint32_t SL = NCH * 64;
@@ -253,23 +255,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         cd[c] = valid && !zero ? (uint32_t)codes[j] : (uint32_t)CODE_ZERO;
         cls[c] = sweep_class(cd[c], ln & ~kGlobal, !valid || zero, (ln & kGlobal) != 0);
     }
-    if (lane < kClasses) cnt[lane] = 0;
-    wave_fence();
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) __hip_atomic_fetch_add(&cnt[cls[c]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    wave_fence();
-    {
-        const uint32_t k = lane < kClasses ? cnt[lane] : 0u;
-        const uint32_t start = wave_scan_dpp(k) - k;
-        if (lane < kClasses) cnt[lane] = start;
-    }
-    wave_fence();
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-        const uint32_t p = __hip_atomic_fetch_add(&cnt[cls[c]], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        perm[p] = (uint16_t)((uint32_t)(c * 64 + lane) | (cd[c] << 8));
-    }
-    wave_fence();
+    class_sort<NCH, GAP>(cnt, perm, cls, cd, ns, wave_fence);
 
     // ---- NCH class-sorted passes, coordinates parked over their descriptors ---
 #pragma unroll
@@ -310,14 +296,14 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false>
+template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false>
 static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
     const uint32_t K = std::min<uint32_t>(64 * NCH / a.A, KCAP);
     if (K == 0) return hipErrorInvalidValue;
     const uint64_t waves = (a.n + K - 1) / K;
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -327,23 +313,25 @@ static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
 // lookups is faster (hdx_encoded.hip).  A <= kWsweepMaxAttrs.
 hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
-    if (a.T) return launch_wsweep_t<2, 8704, 6, true>(a, stream);
+    if (a.T) return launch_wsweep_t<2, 8704, 6, true, true>(a, stream);
     if (!a.coords) return hipErrorInvalidValue;
-    return launch_wsweep_t<2, 8704, 6>(a, stream);
+    return launch_wsweep_t<2, 8704, 6, false, true>(a, stream);
 }
 
 #ifndef HDX_DEBUG_BUILD
 #define HDX_DEBUG_BUILD 0
 #endif
 #if HDX_DEBUG_BUILD
-// A/B forms (debug library): 0 = the product's, 1 = 7 objects, 2 = 3 passes / 11 objects / 14 KiB
+// A/B forms (debug library): 0 = the product's, 1 = 7 objects, 2 = 3 passes /
+// 11 objects / 14 KiB, 6 = the product's without the pass-boundary gap
 hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form) {
     if (a.n == 0) return hipSuccess;
     if (!a.coords) return hipErrorInvalidValue;
     switch (form) {
-        case 0: return launch_wsweep_t<2, 8704, 6>(a, stream);
+        case 0: return launch_wsweep_t<2, 8704, 6, false, true>(a, stream);
         case 1: return launch_wsweep_t<2, 8704, 7>(a, stream);
         case 2: return launch_wsweep_t<3, 14336, 11>(a, stream);
+        case 6: return launch_wsweep_t<2, 8704, 6>(a, stream);
         default: return hipErrorInvalidValue;
     }
 }
