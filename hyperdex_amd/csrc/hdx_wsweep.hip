@@ -151,26 +151,45 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
     if ((uint32_t)lane * 4 < A && (uint32_t)lane * 4 < SL)
         reinterpret_cast<uint32_t*>(codes)[lane] = reinterpret_cast<const uint32_t*>(a.codes)[lane];
 
-    // ---- the keys, gathered dword by dword (a store keeps each key in its
-    // own place), then the value span (whatever of it fits) --------------------
-    // lane o < nobj: its key's dwords [kd, kd + kdw) from the key's dword floor
-    const uint64_t kd = (uint64_t)(uintptr_t)(a.keys + koff) >> 2;
-    const uint32_t kdw = (uint32_t)lane < nobj ? ((uint32_t)((uintptr_t)(a.keys + koff) & 3) + klen + 3) >> 2 : 0u;
-    const uint32_t kdx = wave_scan_dpp(kdw) - kdw;  // its first dword in the key region
-    const uint32_t td = __builtin_amdgcn_readlane(kdx + kdw, 63);
-    const bool keys_in = 4 * td <= WB / 4;
-    const uint32_t kreg = keys_in ? (4 * td + 15) & ~15u : 0u;  // the values' region starts 16-byte aligned
-    if (keys_in) {
-        for (uint32_t u0 = 0; u0 < td; u0 += 64) {
-            const uint32_t u = u0 + (uint32_t)lane;
-            // the object whose key holds region dword u (a wave-uniform walk over <= 63 objects)
-            uint64_t src = 0;
-            for (uint32_t o = 0; o < nobj; ++o) {
-                const uint32_t x0 = __builtin_amdgcn_readlane(kdx, (int)o), xn = __builtin_amdgcn_readlane(kdw, (int)o);
-                if (u >= x0 && u < x0 + xn) src = 4 * (rl64(kd, (int)o) + (u - x0));
+    // ---- the keys, then the value span (whatever of it fits) ----------------
+    // Keys stored back to back (a store's usual layout) are one span, copied
+    // by 16-byte LDS DMA; otherwise they are gathered dword by dword (a store
+    // keeps each key in its own place).
+    const uint64_t knext = sh64(koff, (lane + 1) & 63);
+    const bool kruns = __all((uint32_t)lane + 1 >= nobj || koff + klen == knext);
+    const uint64_t k0 = rl64(koff, 0);
+    const uint32_t klead = (uint32_t)((uintptr_t)(a.keys + k0) & 15);
+    uint32_t kdx = 0, kreg = 0;  // kdx: lane o's first dword in the gathered key region
+    bool keys_in, kspan = false;
+    if (kruns) {
+        const uint64_t kend = rl64(koff + klen, (int)nobj - 1);
+        kspan = kend - k0 + klead <= WB / 4;
+        keys_in = kspan;
+        if (kspan) {
+            kreg = (klead + (uint32_t)(kend - k0) + 15) & ~15u;
+            copy_span(a.keys + k0 - klead, win + kFrontS, klead + (uint32_t)(kend - k0), lane);
+        }
+    }
+    if (!kspan) {
+        // lane o < nobj: its key's dwords [kd, kd + kdw) from the key's dword floor
+        const uint64_t kd = (uint64_t)(uintptr_t)(a.keys + koff) >> 2;
+        const uint32_t kdw = (uint32_t)lane < nobj ? ((uint32_t)((uintptr_t)(a.keys + koff) & 3) + klen + 3) >> 2 : 0u;
+        kdx = wave_scan_dpp(kdw) - kdw;
+        const uint32_t td = __builtin_amdgcn_readlane(kdx + kdw, 63);
+        keys_in = 4 * td <= WB / 4;
+        kreg = keys_in ? (4 * td + 15) & ~15u : 0u;  // the values' region starts 16-byte aligned
+        if (keys_in) {
+            for (uint32_t u0 = 0; u0 < td; u0 += 64) {
+                const uint32_t u = u0 + (uint32_t)lane;
+                // the object whose key holds region dword u (a wave-uniform walk over <= 63 objects)
+                uint64_t src = 0;
+                for (uint32_t o = 0; o < nobj; ++o) {
+                    const uint32_t x0 = __builtin_amdgcn_readlane(kdx, (int)o), xn = __builtin_amdgcn_readlane(kdw, (int)o);
+                    if (u >= x0 && u < x0 + xn) src = 4 * (rl64(kd, (int)o) + (u - x0));
+                }
+                if (u < td)
+                    __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)src, (lds_void_t)(win + kFrontS + 4 * u0), 4, 0, 0);
             }
-            if (u < td)
-                __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)src, (lds_void_t)(win + kFrontS + 4 * u0), 4, 0, 0);
         }
     }
     const uint64_t v0 = rl64(voff, 0);
@@ -184,7 +203,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
     // ---- decode_value (datalayer_encodings.cc:168-217), lane = object --------
     bool bad = false, ok = false;
     if ((uint32_t)lane < nobj) {
-        const uint32_t kw = kFrontS + 4 * kdx + (uint32_t)((uintptr_t)(a.keys + koff) & 3);
+        const uint32_t kw = kFrontS + (kspan ? klead + (uint32_t)(koff - k0) : 4 * kdx + (uint32_t)((uintptr_t)(a.keys + koff) & 3));
         desc[lane * A] = keys_in ? ((uint64_t)kw | ((uint64_t)klen << 32)) : ((uint64_t)0 | ((uint64_t)(klen | kGlobal) << 32));
         const uint64_t vrel = voff - v0;
         const bool vin = voff >= v0 && vlead + vrel + vlen <= vheld;
@@ -217,21 +236,23 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         };
         uint64_t version;
         if (vin) {
-            // branch-free from the window: every step reads inside the value
-            // (pos <= vlen: the window holds the value and 64 bytes after it)
-            ok = vlen >= 10;
+            // branch-free from the window: each step's end pos_{k+1} = pos_k +
+            // 4 + len_k only grows, and step k decodes iff pos_{k+1} <= vlen,
+            // so the object decodes iff the last end does (lengths clamped to
+            // WB >= vlen: no wrap, and a clamped one still fails).  Steps past
+            // a failure read garbage (or 0 past the LDS allocation) and their
+            // descriptors are reset below.
             version = w_be64(lw, vw);
-            ok = ok && w_be16(lw, vw + 8) == A - 1;
+            ok = vlen >= 10 && w_be16(lw, vw + 8) == A - 1;
             uint32_t pos = 10;
             uint64_t* dp = desc + lane * A + 1;
 #pragma unroll 4
             for (uint32_t k = 0; k + 1 < A; ++k) {
-                const uint32_t len = w_be32(lw, vw + pos);
-                const uint32_t room = vlen - pos;  // >= 0 while ok
-                ok = ok && room >= 4 && len <= room - 4;
-                dp[k] = ok ? ((uint64_t)(vw + pos + 4) | ((uint64_t)len << 32)) : (uint64_t)kZero;
-                pos = ok ? pos + 4 + len : pos;
+                const uint32_t len = std::min(w_be32(lw, vw + pos), WB);
+                dp[k] = (uint64_t)(vw + pos + 4) | ((uint64_t)len << 32);
+                pos += 4 + len;
             }
+            ok = ok && pos <= vlen;
         } else
             version = walk([&](uint32_t o) { return g_be16(vp + o); }, [&](uint32_t o) { return g_be32(vp + o); },
                            [&](uint32_t o) { return g_be64(vp + o); }, 0u, kGlobal);
