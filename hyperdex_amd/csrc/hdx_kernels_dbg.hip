@@ -727,7 +727,7 @@ hipError_t launch_debug_variant(const BatchArgs& args, hipStream_t stream, int v
         // wave-staged (hdx_wstage.hip): 200 2 passes / 10 KiB, 201 3 / 14 KiB, 202 2 / 8 KiB,
         // 203 1 / 5 KiB, 204 4 / 18 KiB, 205 2 / 8832 B, 206 = 205 with <= 6 objects
         case 200: case 201: case 202: case 203: case 204: case 205: case 206: case 207: case 208:
-        case 209: case 210: case 211: case 213: case 214: case 215: case 216: case 218: case 219: {
+        case 209: case 210: case 211: case 213: case 214: case 215: case 216: case 218: case 219: case 239: {
             const hipError_t e = launch_hash_wstage(args, stream, variant - 200);
             return e == hipErrorInvalidValue ? launch_hash_batch_variant(args, stream, 44) : e;
         }
@@ -786,8 +786,11 @@ static bool known_variant(int v) {
         case 217:  // wave-staged with the fused region lookup (hdx_hash_batch_regions_device)
         case 218:  // debug shape of 212: no hash (WRONG coordinates)
         case 219:  // 212 without the pass-boundary gap (class_sort)
+        case 239:  // 212 / 230 with the one-block > 64-byte loop (city_gt64_lds LOOP 1)
         case 220: case 221: case 222:  // streamed (hdx_stream.hip)
-        case 230: case 231: case 232: case 233: case 234: case 236:  // wave-staged sweep (236: without the pass-boundary gap) (hdx_wsweep.hip; 233: fused regions; 234: the gather sweep's fused regions)
+        case 230: case 231: case 232: case 233: case 234:  // wave-staged sweep (hdx_wsweep.hip; 233: fused regions; 234: the gather sweep's fused regions)
+        case 236:  // 230 without the pass-boundary gap
+        case 237: case 238:  // 230's debug shapes: no hash / no hash, no walk (WRONG coordinates)
         case 235:  // regions by hash + separate lookups at any n, 64 MiB chunks (hdx_regions.hip)
         case 223: case 224: case 225: case 226: case 227:  // its debug shapes (WRONG coordinates)
         case 210: case 211:  // wave-staged, sorted over the workgroup

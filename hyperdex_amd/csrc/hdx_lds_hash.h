@@ -101,7 +101,27 @@ __device__ __forceinline__ Blk lds_block64_w128(ldsw_t w, uint32_t s) {
 
 // city.cc:361-397 for n > 64: the tail block t in registers, the loop blocks
 // read from the window (city_gt64_reg's arithmetic).
-template <bool W128 = false>
+// LOOP 1: one block per trip, the next block read at its end (its registers
+// then copied into the current block's, and x / z swapped by copies: ~9
+// v_mov_b64 a trip); LOOP 2: two blocks per trip, the block after next read
+// into the other register set before the current one is hashed, and x / z
+// trading roles instead of places — no copies.  A read past the string's last
+// block stays inside the LDS allocation or reads 0; its data are never used.
+__device__ __forceinline__ void city_loop_step(uint64_t& x, uint64_t& y, uint64_t& z, uint64_t& v0, uint64_t& v1,
+                                               uint64_t& w0, uint64_t& w1, const Blk& b) {
+    x = ror(x + y + v0 + b.v0.y, 37) * K1;
+    y = ror(y + v1 + b.v3.x, 42) * K1;
+    x ^= w1;
+    y += v0 + b.v2.y;
+    z = ror(z + w0, 33) * K1;
+    uint64_t nv0, nv1, nw0, nw1;
+    weak32(b.v0.x, b.v0.y, b.v1.x, b.v1.y, v1 * K1, x + w0, nv0, nv1);
+    weak32(b.v2.x, b.v2.y, b.v3.x, b.v3.y, z + w1, y + b.v1.x, nw0, nw1);
+    v0 = nv0; v1 = nv1; w0 = nw0; w1 = nw1;
+    // std::swap(z, x) is the caller's (LOOP 2: the next step gets them swapped)
+}
+
+template <bool W128 = false, int LOOP = 1>
 __device__ __forceinline__ uint64_t city_gt64_lds(ldsw_t w, uint32_t off, uint32_t n, const Blk& t) {
     const u64x2 e0 = t.v0, e1 = t.v1, e2 = t.v2, e3 = t.v3;
     uint64_t x = e1.y;
@@ -111,21 +131,30 @@ __device__ __forceinline__ uint64_t city_gt64_lds(ldsw_t w, uint32_t off, uint32
     weak32(e0.x, e0.y, e1.x, e1.y, n, z, v0, v1);
     weak32(e2.x, e2.y, e3.x, e3.y, y + K1, x, w0, w1);
     const uint32_t blocks = (n - 1) >> 6;
-    Blk b = W128 ? lds_block64_w128(w, off) : lds_block64(w, off);
-    x = x * K1 + b.v0.x;
-    for (uint32_t k = 0;;) {
-        x = ror(x + y + v0 + b.v0.y, 37) * K1;
-        y = ror(y + v1 + b.v3.x, 42) * K1;
-        x ^= w1;
-        y += v0 + b.v2.y;
-        z = ror(z + w0, 33) * K1;
-        uint64_t nv0, nv1, nw0, nw1;
-        weak32(b.v0.x, b.v0.y, b.v1.x, b.v1.y, v1 * K1, x + w0, nv0, nv1);
-        weak32(b.v2.x, b.v2.y, b.v3.x, b.v3.y, z + w1, y + b.v1.x, nw0, nw1);
-        v0 = nv0; v1 = nv1; w0 = nw0; w1 = nw1;
-        const uint64_t tt = z; z = x; x = tt;
-        if (++k == blocks) break;
-        b = W128 ? lds_block64_w128(w, off + 64 * k) : lds_block64(w, off + 64 * k);
+    auto rd = [&](uint32_t o) { return W128 ? lds_block64_w128(w, o) : lds_block64(w, o); };
+    if constexpr (LOOP == 2) {
+        Blk ba = rd(off);
+        x = x * K1 + ba.v0.x;
+        for (uint32_t k = 0;;) {
+            const Blk bb = rd(off + 64 * (k + 1));
+            city_loop_step(x, y, z, v0, v1, w0, w1, ba);  // leaves x and z swapped: z is x now
+            if (++k == blocks) {
+                const uint64_t tt = z; z = x; x = tt;
+                break;
+            }
+            ba = rd(off + 64 * (k + 1));
+            city_loop_step(z, y, x, v0, v1, w0, w1, bb);  // roles traded back
+            if (++k == blocks) break;
+        }
+    } else {
+        Blk b = rd(off);
+        x = x * K1 + b.v0.x;
+        for (uint32_t k = 0;;) {
+            city_loop_step(x, y, z, v0, v1, w0, w1, b);
+            const uint64_t tt = z; z = x; x = tt;
+            if (++k == blocks) break;
+            b = rd(off + 64 * k);
+        }
     }
     return mix16(mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z, mix16(v1, w1, KMUL) + x, KMUL);
 }
@@ -211,7 +240,7 @@ __device__ __forceinline__ uint64_t city_le16_ht(uint64_t h0, uint64_t t3, uint3
 // HashLen0to16 / 17to32 / 33to64 / the > 64-byte tail block) and, over 64
 // bytes, the loop blocks.  The window needs 32 readable bytes before off
 // (s[n-32, n) of a short string) and 36 after the value's end.
-template <bool W128 = false>
+template <bool W128 = false, int LOOP = 1>
 __device__ __forceinline__ uint64_t hash_slot_window(ldsw_t w, uint32_t code, uint32_t off, uint32_t n, bool& bad) {
     if (code == CODE_STRING) {
         const Q32 t = lds_read32<W128>(w, off + n - 32);  // s[n-32, n): the front pad covers n < 32
@@ -223,7 +252,7 @@ __device__ __forceinline__ uint64_t hash_slot_window(ldsw_t w, uint32_t code, ui
             b.v1 = u64x2{u.q2, u.q3};
             b.v2 = t01;
             b.v3 = t23;
-            return city_gt64_lds<W128>(w, off, n, b);
+            return city_gt64_lds<W128, LOOP>(w, off, n, b);
         }
         const Q32 h = lds_read32<W128>(w, off);  // s[0, 32): the back pad covers n < 32
         const u64x2 h01 = {h.q0, h.q1};

@@ -171,14 +171,14 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
 // dword instead of the hash.
 // HT: staged slots hashed by hash_slot_window (first / last 32 bytes, every
 // regime from the same two reads; lw then points kFrontHT bytes before the
-// window).
+// window); HT 2: with the two-block > 64-byte loop (city_gt64_lds LOOP 2).
 constexpr uint32_t kFrontHT = 32;
-template <int SHAPE, bool HT = false, bool W128 = false>
+template <int SHAPE, int HT = 0, bool W128 = false>
 __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, bool staged, uint64_t mybase,
                                               uint32_t s, uint32_t cd, uint64_t d, bool& bad) {
     const uint32_t doff = (uint32_t)d, dn = (uint32_t)(d >> 32);
     if (SHAPE == 1) return lw[doff >> 2] ^ dn;
-    if (staged && HT) return hash_slot_window<W128>(lw, cd, doff + kFrontHT, dn, bad);
+    if (staged && HT) return hash_slot_window<W128, (HT > 1 ? 2 : 1)>(lw, cd, doff + kFrontHT, dn, bad);
     if (staged) return cd == CODE_STRING ? hash_string_lds(lw, doff, dn) : hash_numeric_lds(lw, cd, doff, dn, bad);
     const uint32_t o = div_small(s, args.a_magic);
     const uint64_t ob = shfl64(mybase, (int)(o & 63));
@@ -195,7 +195,7 @@ __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, 
 // (lookup_tables_wave), coordinates stored only when args.coords is set.
 // GAP: the class straddling the pass boundary moves whole into the second
 // pass when pads allow (class_sort, hdx_regroup.h).
-template <int NCH, uint32_t WB, int SHAPE = 0, bool HT = false, int ORDER = 1, bool W128 = false, bool REGIONS = false,
+template <int NCH, uint32_t WB, int SHAPE = 0, int HT = 0, int ORDER = 1, bool W128 = false, bool REGIONS = false,
           bool GAP = false>
 __global__ void __launch_bounds__(256)
 hash_wstage_kernel(const BatchArgs args) {
@@ -253,7 +253,7 @@ hash_wstage_kernel(const BatchArgs args) {
 // slots from global memory before the first barrier and takes no part in the
 // sort.
 
-template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, bool HT = false, int ORDER = 1, bool W128 = false,
+template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, int HT = 0, int ORDER = 1, bool W128 = false,
           bool REGIONS = false, bool GAP = false>
 static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     // lane o holds object o's base and lane K the next group's first: K <= 63

@@ -149,7 +149,8 @@ hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int for
         case 15: return launch_wstage_t<2, 8832, 63, 0, true, 3>(args, stream);  // 12 in class order 3
         case 16: return launch_wstage_t<2, 8832, 63, 0, true, 1, true>(args, stream);  // 12 with b128 window reads
         case 18: return launch_wstage_t<2, 8832, 63, 1, true>(args, stream);  // debug shape of 12: no hash (WRONG coordinates)
-        case 19: return launch_wstage_t<2, 8832, 63, 0, true, 1>(args, stream);  // the product without the pass-boundary gap
+        case 19: return launch_wstage_t<2, 8832, 63, 0, 2, 1>(args, stream);  // the product without the pass-boundary gap
+        case 39: return launch_wstage_t<2, 8832, 63, 0, 1, 1, false, false, true>(args, stream);  // the product with the one-block loop
         // the slots class-sorted over the workgroup
         case 10: return launch_wgstage_t<2, 8832>(args, stream);
         case 11: return launch_wgstage_t<1, 4352>(args, stream);

@@ -116,7 +116,9 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
 // parked in LDS; coordinates are stored only when a.coords is set.
 // GAP: the class straddling the pass boundary moves whole into the second
 // pass when pads allow (class_sort, hdx_regroup.h).
-template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false>
+// SHAPE (debug forms 7 / 8, WRONG coordinates): 1 = no hash (a slot's
+// coordinate is its descriptor), 2 = no hash and no walk.
+template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1>
 __global__ void __launch_bounds__(256)
 hash_sweep_wstage_kernel(const EncodedArgs a) {
     constexpr uint32_t SL = NCH * 64;
@@ -246,6 +248,10 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
             ok = vlen >= 10 && w_be16(lw, vw + 8) == A - 1;
             uint32_t pos = 10;
             uint64_t* dp = desc + lane * A + 1;
+            if (SHAPE == 2) {  // debug shape: no walk (descriptors of assorted lengths at the value's start)
+                for (uint32_t k = 0; k + 1 < A; ++k) dp[k] = (uint64_t)(vw + 14) | ((uint64_t)((k * 37) & 127) << 32);
+                pos = vlen;
+            } else
 #pragma unroll 4
             for (uint32_t k = 0; k + 1 < A; ++k) {
                 const uint32_t len = std::min(w_be32(lw, vw + pos), WB);
@@ -299,7 +305,8 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         uint64_t h = 0;
         if (s < ns && off != kZero) {
             if (ln & kGlobal) h = hash_global((j == 0 ? a.keys : a.vals) + ob + off, code, ln & ~kGlobal, bad);
-            else h = hash_slot_window(lw, code, off, ln, bad);
+            else if (SHAPE) h = d ^ lw[off >> 2];
+            else h = hash_slot_window<false, LOOP>(lw, code, off, ln, bad);
         }
         desc[s] = h;
     }
@@ -317,14 +324,14 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false>
+template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1>
 static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
     const uint32_t K = std::min<uint32_t>(64 * NCH / a.A, KCAP);
     if (K == 0) return hipErrorInvalidValue;
     const uint64_t waves = (a.n + K - 1) / K;
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -334,9 +341,9 @@ static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
 // lookups is faster (hdx_encoded.hip).  A <= kWsweepMaxAttrs.
 hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
-    if (a.T) return launch_wsweep_t<2, 8704, 6, true, true>(a, stream);
+    if (a.T) return launch_wsweep_t<2, 8704, 6, true, true, 0, 2>(a, stream);
     if (!a.coords) return hipErrorInvalidValue;
-    return launch_wsweep_t<2, 8704, 6, false, true>(a, stream);
+    return launch_wsweep_t<2, 8704, 6, false, true, 0, 2>(a, stream);
 }
 
 #ifndef HDX_DEBUG_BUILD
@@ -344,15 +351,20 @@ hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream) 
 #endif
 #if HDX_DEBUG_BUILD
 // A/B forms (debug library): 0 = the product's, 1 = 7 objects, 2 = 3 passes /
-// 11 objects / 14 KiB, 6 = the product's without the pass-boundary gap
+// 11 objects / 14 KiB, 6 = the product's without the pass-boundary gap,
+// 7 / 8 debug shapes (WRONG coordinates), 9 = the product's with the one-block
+// > 64-byte loop
 hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form) {
     if (a.n == 0) return hipSuccess;
     if (!a.coords) return hipErrorInvalidValue;
     switch (form) {
-        case 0: return launch_wsweep_t<2, 8704, 6, false, true>(a, stream);
+        case 0: return launch_wsweep_t<2, 8704, 6, false, true, 0, 2>(a, stream);
         case 1: return launch_wsweep_t<2, 8704, 7>(a, stream);
         case 2: return launch_wsweep_t<3, 14336, 11>(a, stream);
-        case 6: return launch_wsweep_t<2, 8704, 6>(a, stream);
+        case 6: return launch_wsweep_t<2, 8704, 6, false, false, 0, 2>(a, stream);
+        case 7: return launch_wsweep_t<2, 8704, 6, false, true, 1>(a, stream);  // debug shape: no hash
+        case 8: return launch_wsweep_t<2, 8704, 6, false, true, 2>(a, stream);  // debug shape: no hash, no walk
+        case 9: return launch_wsweep_t<2, 8704, 6, false, true, 0, 1>(a, stream);  // the one-block loop
         default: return hipErrorInvalidValue;
     }
 }
