@@ -60,6 +60,17 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int l) {
     return pack64((uint32_t)__shfl((int)(uint32_t)v, l, 64), (uint32_t)__shfl((int)(uint32_t)(v >> 32), l, 64));
 }
+// One 16-byte-per-lane LDS DMA (global_load_lds_dwordx4, M0 = the wave's
+// destination) as inline asm: the compiler's wait insertion does not see it,
+// so it neither drains it before an unrelated load's use nor before the
+// first LDS atomic / read of the wave's metadata (it cannot tell those from
+// the window) — the kernel waits for it itself (s_waitcnt vmcnt(0) before the
+// passes).  Any wait the compiler emits for its own loads still covers these
+// (vmcnt counts in issue order), at worst waiting longer.
+__device__ __forceinline__ void dma_x4_asm(const void* src, const void* dst) {
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t)dst);
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+}
 __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -83,7 +94,10 @@ struct Group {
 // staged decision, and every slot's descriptor desc[s] = {offset, length}:
 // the offset in `win` + win_off when staged, else in the object.  SHAPE 2
 // (debug) skips the DMA.
-template <int NCH, uint32_t WB, int SHAPE, int ORDER = 1>
+// ADMA: the DMA as inline asm (dma_x4_asm), the code table loaded with the
+// bases and lengths and waited for before the DMA goes out — nothing in
+// phases 2-3 then waits for the DMA.
+template <int NCH, uint32_t WB, int SHAPE, int ORDER = 1, bool ADMA = false>
 __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint64_t o0, uint8_t* win, uint32_t win_off,
                                                      uint64_t* desc) {
     const int lane = threadIdx.x & 63;
@@ -103,6 +117,11 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
         const uint32_t s = (uint32_t)(c * 64 + lane);
         g.L[c] = s < g.ns ? args.attr_len[g.q0 + s] : 0u;
     }
+    uint32_t packed_codes = 0;
+    if constexpr (ADMA) {
+        packed_codes = reinterpret_cast<const uint32_t*>(args.codes)[lane];
+        asm volatile("" ::"v"(packed_codes));  // its load completes before the DMA is issued
+    }
     const uint64_t b0 = readlane64(mybase, 0);
     const uint64_t bnext = has_next ? readlane64(mybase, (int)g.nobj) : 0;
     const uint32_t lead = (uint32_t)((uintptr_t)(args.blob + b0) & 15);
@@ -110,8 +129,10 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
     auto dma = [&](uint32_t units) {  // units 16-byte units from s16 -> win (units <= WB / 16)
         for (uint32_t u0 = 0; u0 < units; u0 += 64) {
             const uint32_t u = u0 + (uint32_t)lane;
-            if (u < units)  // lanes past the span write nothing: the window need not be whole KiB
-                __builtin_amdgcn_global_load_lds((const void*)(s16 + 16ull * u), (lds_void_t)(win + 16 * u0), 16, 0, 0);
+            if (u < units) {  // lanes past the span write nothing: the window need not be whole KiB
+                if constexpr (ADMA) dma_x4_asm(s16 + 16ull * u, win + 16 * u0);
+                else __builtin_amdgcn_global_load_lds((const void*)(s16 + 16ull * u), (lds_void_t)(win + 16 * u0), 16, 0, 0);
+            }
         }
     };
     // the span up to the next group's first object, before the lengths are back
@@ -119,7 +140,7 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
     if (early && SHAPE != 2) dma((lead + (uint32_t)(bnext - b0) + 15) >> 4);
 
     // ---- in-object offsets, codes, object sizes ----------------------------
-    const uint32_t packed_codes = reinterpret_cast<const uint32_t*>(args.codes)[lane];
+    if constexpr (!ADMA) packed_codes = reinterpret_cast<const uint32_t*>(args.codes)[lane];
     uint32_t off[NCH], endv[NCH];
     uint32_t carry = 0;
 #pragma unroll
@@ -196,7 +217,7 @@ __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, 
 // GAP: the class straddling the pass boundary moves whole into the second
 // pass when pads allow (class_sort, hdx_regroup.h).
 template <int NCH, uint32_t WB, int SHAPE = 0, int HT = 0, int ORDER = 1, bool W128 = false, bool REGIONS = false,
-          bool GAP = false>
+          bool GAP = false, bool ADMA = false>
 __global__ void __launch_bounds__(256)
 hash_wstage_kernel(const BatchArgs args) {
     static_assert(NCH >= 1 && NCH <= 4 && WB % 16 == 0, "slot indices are 8 bits; windows whole DMA units");
@@ -214,7 +235,7 @@ hash_wstage_kernel(const BatchArgs args) {
 
     const uint64_t o0 = ((uint64_t)blockIdx.x * 4 + w) * args.K;
     if (o0 >= args.n) return;  // no barrier anywhere: waves are independent
-    const Group<NCH> g = describe_group<NCH, WB, SHAPE, ORDER>(args, o0, win, 0, desc);
+    const Group<NCH> g = describe_group<NCH, WB, SHAPE, ORDER, ADMA>(args, o0, win, 0, desc);
 
     // ---- counting sort by work class (wave-local) --------------------------
     class_sort<NCH, GAP>(cnt, perm, g.cls, g.code, g.ns, wave_lds_fence);
@@ -254,7 +275,7 @@ hash_wstage_kernel(const BatchArgs args) {
 // sort.
 
 template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, int HT = 0, int ORDER = 1, bool W128 = false,
-          bool REGIONS = false, bool GAP = false>
+          bool REGIONS = false, bool GAP = false, bool ADMA = false>
 static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     // lane o holds object o's base and lane K the next group's first: K <= 63
     args.K = std::min<uint32_t>(std::min<uint32_t>((uint32_t)(64 * NCH) / args.A, KCAP), 63u);
@@ -263,7 +284,7 @@ static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
     return hipGetLastError();
 }
 
