@@ -26,6 +26,26 @@ typedef __attribute__((address_space(3))) uint32_t* ldsw_mut_t;
 
 __device__ __forceinline__ ldsw_t as_ldsw(const void* p) { return (ldsw_t)p; }
 
+// LDS DMA (global_load_lds_dwordx4 / _dword: lane l's 16 / 4 bytes from src
+// to dst + 16 l / 4 l, dst wave-uniform into M0) as inline asm.  The
+// compiler's wait insertion does not see these, so it neither drains them
+// before an unrelated load's use, nor before the first LDS atomic or read of
+// the wave's metadata (it cannot tell those from the window), nor again after
+// the kernel's own drain (then waiting on any store issued since).  The
+// kernels wait for them themselves (s_waitcnt vmcnt(0) before the window is
+// read).  Any wait the compiler emits for its own loads still covers them
+// (vmcnt counts in issue order), at worst waiting longer.
+__device__ __forceinline__ void dma_x4_asm(const void* src, const void* dst) {
+    const uint32_t m0 =
+        __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)dst);
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+}
+__device__ __forceinline__ void dma_x1_asm(const void* src, const void* dst) {
+    const uint32_t m0 =
+        __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)dst);
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+}
+
 // 16 bytes at a dword-aligned LDS address as one ds_read_b128 (gfx950 serves
 // dword-aligned b128 reads; the compiler emits them for 4-byte-aligned
 // vectors).  W128 forms below read 4 dwords per instruction instead of 2.
@@ -121,8 +141,11 @@ __device__ __forceinline__ void city_loop_step(uint64_t& x, uint64_t& y, uint64_
     // std::swap(z, x) is the caller's (LOOP 2: the next step gets them swapped)
 }
 
+// ... up to its last mix16: the result is mix16(u, v, KMUL) (LOOP 3 shares
+// that mix16 with the <= 32-byte regimes' own, hash_slot_window).
 template <bool W128 = false, int LOOP = 1>
-__device__ __forceinline__ uint64_t city_gt64_lds(ldsw_t w, uint32_t off, uint32_t n, const Blk& t) {
+__device__ __forceinline__ void city_gt64_lds_uv(ldsw_t w, uint32_t off, uint32_t n, const Blk& t, uint64_t& u,
+                                                 uint64_t& v) {
     const u64x2 e0 = t.v0, e1 = t.v1, e2 = t.v2, e3 = t.v3;
     uint64_t x = e1.y;
     uint64_t y = e3.x + e0.y;
@@ -132,7 +155,7 @@ __device__ __forceinline__ uint64_t city_gt64_lds(ldsw_t w, uint32_t off, uint32
     weak32(e2.x, e2.y, e3.x, e3.y, y + K1, x, w0, w1);
     const uint32_t blocks = (n - 1) >> 6;
     auto rd = [&](uint32_t o) { return W128 ? lds_block64_w128(w, o) : lds_block64(w, o); };
-    if constexpr (LOOP == 2) {
+    if constexpr (LOOP >= 2) {
         Blk ba = rd(off);
         x = x * K1 + ba.v0.x;
         for (uint32_t k = 0;;) {
@@ -156,7 +179,14 @@ __device__ __forceinline__ uint64_t city_gt64_lds(ldsw_t w, uint32_t off, uint32
             b = rd(off + 64 * k);
         }
     }
-    return mix16(mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z, mix16(v1, w1, KMUL) + x, KMUL);
+    u = mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z;
+    v = mix16(v1, w1, KMUL) + x;
+}
+template <bool W128 = false, int LOOP = 1>
+__device__ __forceinline__ uint64_t city_gt64_lds(ldsw_t w, uint32_t off, uint32_t n, const Blk& t) {
+    uint64_t u, v;
+    city_gt64_lds_uv<W128, LOOP>(w, off, n, t, u, v);
+    return mix16(u, v, KMUL);
 }
 
 // hash(type, slice) of a string slot at byte offset off of the window
@@ -240,11 +270,41 @@ __device__ __forceinline__ uint64_t city_le16_ht(uint64_t h0, uint64_t t3, uint3
 // HashLen0to16 / 17to32 / 33to64 / the > 64-byte tail block) and, over 64
 // bytes, the loop blocks.  The window needs 32 readable bytes before off
 // (s[n-32, n) of a short string) and 36 after the value's end.
+// LOOP: city_gt64_lds's; LOOP 3 = LOOP 2 with one final mix16 shared by the
+// > 64-byte regime and the 8..32-byte ones (a pass holding both runs it once).
 template <bool W128 = false, int LOOP = 1>
 __device__ __forceinline__ uint64_t hash_slot_window(ldsw_t w, uint32_t code, uint32_t off, uint32_t n, bool& bad) {
     if (code == CODE_STRING) {
         const Q32 t = lds_read32<W128>(w, off + n - 32);  // s[n-32, n): the front pad covers n < 32
         const u64x2 t01 = {t.q0, t.q1}, t23 = {t.q2, t.q3};
+        if constexpr (LOOP >= 3) {
+            uint64_t u, v, mul;
+            if (n > 64) {
+                const Q32 q = lds_read32<W128>(w, off + n - 64);
+                Blk b;
+                b.v0 = u64x2{q.q0, q.q1};
+                b.v1 = u64x2{q.q2, q.q3};
+                b.v2 = t01;
+                b.v3 = t23;
+                city_gt64_lds_uv<W128, 2>(w, off, n, b, u, v);
+                mul = KMUL;
+            } else {
+                const Q32 h = lds_read32<W128>(w, off);  // s[0, 32): the back pad covers n < 32
+                if (n > 32) return city_33to64(u64x2{h.q0, h.q1}, u64x2{h.q2, h.q3}, t01, t23, n);
+                if (n < 8) return city_le16_ht(h.q0, t.q3, n);
+                mul = K2 + 2ull * n;
+                if (n > 16) {  // city.cc:305-313 (city_17to32)
+                    const uint64_t a = h.q0 * K1, b = h.q1, c = t.q3 * mul, d = t.q2 * K2;
+                    u = ror(a + b, 43) + ror(c, 30) + d;
+                    v = a + ror(b + K2, 18) + c;
+                } else {  // city.cc:281-286 (city_le16_ht, n >= 8)
+                    const uint64_t a = h.q0 + K2;
+                    u = ror(t.q3, 37) * mul + a;
+                    v = (ror(a, 25) + t.q3) * mul;
+                }
+            }
+            return mix16(u, v, mul);
+        }
         if (n > 64) {
             const Q32 u = lds_read32<W128>(w, off + n - 64);
             Blk b;
@@ -252,7 +312,7 @@ __device__ __forceinline__ uint64_t hash_slot_window(ldsw_t w, uint32_t code, ui
             b.v1 = u64x2{u.q2, u.q3};
             b.v2 = t01;
             b.v3 = t23;
-            return city_gt64_lds<W128, LOOP>(w, off, n, b);
+            return city_gt64_lds<W128, (LOOP > 2 ? 2 : LOOP)>(w, off, n, b);
         }
         const Q32 h = lds_read32<W128>(w, off);  // s[0, 32): the back pad covers n < 32
         const u64x2 h01 = {h.q0, h.q1};

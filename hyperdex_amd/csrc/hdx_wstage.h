@@ -60,17 +60,6 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
 __device__ __forceinline__ uint64_t shfl64(uint64_t v, int l) {
     return pack64((uint32_t)__shfl((int)(uint32_t)v, l, 64), (uint32_t)__shfl((int)(uint32_t)(v >> 32), l, 64));
 }
-// One 16-byte-per-lane LDS DMA (global_load_lds_dwordx4, M0 = the wave's
-// destination) as inline asm: the compiler's wait insertion does not see it,
-// so it neither drains it before an unrelated load's use nor before the
-// first LDS atomic / read of the wave's metadata (it cannot tell those from
-// the window) — the kernel waits for it itself (s_waitcnt vmcnt(0) before the
-// passes).  Any wait the compiler emits for its own loads still covers these
-// (vmcnt counts in issue order), at worst waiting longer.
-__device__ __forceinline__ void dma_x4_asm(const void* src, const void* dst) {
-    const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t)dst);
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
-}
 __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -192,14 +181,14 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
 // dword instead of the hash.
 // HT: staged slots hashed by hash_slot_window (first / last 32 bytes, every
 // regime from the same two reads; lw then points kFrontHT bytes before the
-// window); HT 2: with the two-block > 64-byte loop (city_gt64_lds LOOP 2).
+// window); HT 2 / 3: hash_slot_window's LOOP 2 / 3.
 constexpr uint32_t kFrontHT = 32;
 template <int SHAPE, int HT = 0, bool W128 = false>
 __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, bool staged, uint64_t mybase,
                                               uint32_t s, uint32_t cd, uint64_t d, bool& bad) {
     const uint32_t doff = (uint32_t)d, dn = (uint32_t)(d >> 32);
     if (SHAPE == 1) return lw[doff >> 2] ^ dn;
-    if (staged && HT) return hash_slot_window<W128, (HT > 1 ? 2 : 1)>(lw, cd, doff + kFrontHT, dn, bad);
+    if (staged && HT) return hash_slot_window<W128, (HT > 1 ? HT : 1)>(lw, cd, doff + kFrontHT, dn, bad);
     if (staged) return cd == CODE_STRING ? hash_string_lds(lw, doff, dn) : hash_numeric_lds(lw, cd, doff, dn, bad);
     const uint32_t o = div_small(s, args.a_magic);
     const uint64_t ob = shfl64(mybase, (int)(o & 63));

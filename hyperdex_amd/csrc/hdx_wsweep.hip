@@ -94,16 +94,28 @@ __device__ __forceinline__ uint64_t hash_global(const uint8_t* p, uint32_t code,
 
 // copy [src, src + bytes) (src 16-byte aligned) to LDS dst: whole 16-byte
 // units by LDS DMA, the last partial unit as dwords (a dword never crosses a
-// page, so nothing past the span's last dword is read)
+// page, so nothing past the span's last dword is read); ASM: inline-asm DMA
+// (hdx_lds_hash.h; debug form 13 only — the sweep drains its copies right
+// after issuing them, and the builtin measured faster)
+template <bool ASM = false>
+__device__ __forceinline__ void dma16(const void* src, void* dst) {
+    if constexpr (ASM) dma_x4_asm(src, dst);
+    else __builtin_amdgcn_global_load_lds(src, (lds_void_t)dst, 16, 0, 0);
+}
+template <bool ASM = false>
+__device__ __forceinline__ void dma4(const void* src, void* dst) {
+    if constexpr (ASM) dma_x1_asm(src, dst);
+    else __builtin_amdgcn_global_load_lds(src, (lds_void_t)dst, 4, 0, 0);
+}
+template <bool ASM = false>
 __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint32_t bytes, int lane) {
     const uint32_t units = bytes >> 4;
     for (uint32_t u0 = 0; u0 < units; u0 += 64) {
         const uint32_t u = u0 + (uint32_t)lane;
-        if (u < units) __builtin_amdgcn_global_load_lds((const void*)(src + 16ull * u), (lds_void_t)(dst + 16 * u0), 16, 0, 0);
+        if (u < units) dma16<ASM>(src + 16ull * u, dst + 16 * u0);
     }
     const uint32_t tdw = ((bytes & 15) + 3) >> 2;
-    if ((uint32_t)lane < tdw)
-        __builtin_amdgcn_global_load_lds((const void*)(src + 16ull * units + 4 * lane), (lds_void_t)(dst + 16 * units), 4, 0, 0);
+    if ((uint32_t)lane < tdw) dma4<ASM>(src + 16ull * units + 4 * lane, dst + 16 * units);
 }
 
 }  // namespace
@@ -118,7 +130,8 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
 // pass when pads allow (class_sort, hdx_regroup.h).
 // SHAPE (debug forms 7 / 8, WRONG coordinates): 1 = no hash (a slot's
 // coordinate is its descriptor), 2 = no hash and no walk.
-template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1>
+template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
+          bool ASM = false>
 __global__ void __launch_bounds__(256)
 hash_sweep_wstage_kernel(const EncodedArgs a) {
     constexpr uint32_t SL = NCH * 64;
@@ -169,7 +182,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         keys_in = kspan;
         if (kspan) {
             kreg = (klead + (uint32_t)(kend - k0) + 15) & ~15u;
-            copy_span(a.keys + k0 - klead, win + kFrontS, klead + (uint32_t)(kend - k0), lane);
+            copy_span<ASM>(a.keys + k0 - klead, win + kFrontS, klead + (uint32_t)(kend - k0), lane);
         }
     }
     if (!kspan) {
@@ -190,7 +203,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
                     if (u >= x0 && u < x0 + xn) src = 4 * (rl64(kd, (int)o) + (u - x0));
                 }
                 if (u < td)
-                    __builtin_amdgcn_global_load_lds((const void*)(uintptr_t)src, (lds_void_t)(win + kFrontS + 4 * u0), 4, 0, 0);
+                    dma4<ASM>((const void*)(uintptr_t)src, win + kFrontS + 4 * u0);
             }
         }
     }
@@ -198,12 +211,13 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
     const uint64_t vend = has_next ? rl64(voff, (int)nobj) : 0;
     const uint32_t vlead = (uint32_t)((uintptr_t)(a.vals + v0) & 15);
     const uint32_t vheld = has_next && vend >= v0 ? (uint32_t)std::min<uint64_t>(vlead + (vend - v0), WB - kreg) : 0u;
-    if (vheld) copy_span(a.vals + v0 - vlead, win + kFrontS + kreg, vheld, lane);
+    if (vheld) copy_span<ASM>(a.vals + v0 - vlead, win + kFrontS + kreg, vheld, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the compiler does not order ds_read after LDS DMA
     wave_fence();
 
     // ---- decode_value (datalayer_encodings.cc:168-217), lane = object --------
     bool bad = false, ok = false;
+    uint64_t my_version = 0;  // stored with the coordinates (a store here would stall the LDS atomics' waits)
     if ((uint32_t)lane < nobj) {
         const uint32_t kw = kFrontS + (kspan ? klead + (uint32_t)(koff - k0) : 4 * kdx + (uint32_t)((uintptr_t)(a.keys + koff) & 3));
         desc[lane * A] = keys_in ? ((uint64_t)kw | ((uint64_t)klen << 32)) : ((uint64_t)0 | ((uint64_t)(klen | kGlobal) << 32));
@@ -264,7 +278,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
                            [&](uint32_t o) { return g_be64(vp + o); }, 0u, kGlobal);
         if (!ok)  // undecodable: every coordinate of the object is 0
             for (uint32_t j = 0; j < A; ++j) desc[lane * A + j] = (uint64_t)kZero;
-        if (a.versions) a.versions[o0 + lane] = ok ? version : 0;
+        my_version = ok ? version : 0;
     }
     const bool any_bad = __any((uint32_t)lane < nobj && !ok);
     wave_fence();
@@ -318,20 +332,22 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
             if (s < ns) __builtin_nontemporal_store(desc[s], a.coords + o0 * A + s);
         }
     }
+    if (a.versions && (uint32_t)lane < nobj) a.versions[o0 + lane] = my_version;
     if constexpr (REGIONS)  // the window is free now: the lookups' scratch
         lookup_tables_wave(a.t, a.T, desc, A, nobj, o0, reinterpret_cast<uint64_t*>(win), wave_fence);
     if (a.status && lane == 0 && any_bad) atomicOr(a.status, 1u << 6 /* HDX_E_BADENC */);
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1>
+template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
+          bool ASM = false>
 static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
     const uint32_t K = std::min<uint32_t>(64 * NCH / a.A, KCAP);
     if (K == 0) return hipErrorInvalidValue;
     const uint64_t waves = (a.n + K - 1) / K;
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -341,9 +357,9 @@ static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
 // lookups is faster (hdx_encoded.hip).  A <= kWsweepMaxAttrs.
 hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
-    if (a.T) return launch_wsweep_t<2, 8704, 6, true, true, 0, 2>(a, stream);
+    if (a.T) return launch_wsweep_t<2, 8704, 6, true, true, 0, 3, false>(a, stream);
     if (!a.coords) return hipErrorInvalidValue;
-    return launch_wsweep_t<2, 8704, 6, false, true, 0, 2>(a, stream);
+    return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false>(a, stream);
 }
 
 #ifndef HDX_DEBUG_BUILD
@@ -353,18 +369,21 @@ hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream) 
 // A/B forms (debug library): 0 = the product's, 1 = 7 objects, 2 = 3 passes /
 // 11 objects / 14 KiB, 6 = the product's without the pass-boundary gap,
 // 7 / 8 debug shapes (WRONG coordinates), 9 = the product's with the one-block
-// > 64-byte loop
+// > 64-byte loop, 12 without the shared final mix16, 13 with the DMA as
+// inline asm (4.24 vs 4.20 ms per 10 M: the builtin stays)
 hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form) {
     if (a.n == 0) return hipSuccess;
     if (!a.coords) return hipErrorInvalidValue;
     switch (form) {
-        case 0: return launch_wsweep_t<2, 8704, 6, false, true, 0, 2>(a, stream);
+        case 0: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false>(a, stream);
         case 1: return launch_wsweep_t<2, 8704, 7>(a, stream);
         case 2: return launch_wsweep_t<3, 14336, 11>(a, stream);
         case 6: return launch_wsweep_t<2, 8704, 6, false, false, 0, 2>(a, stream);
         case 7: return launch_wsweep_t<2, 8704, 6, false, true, 1>(a, stream);  // debug shape: no hash
         case 8: return launch_wsweep_t<2, 8704, 6, false, true, 2>(a, stream);  // debug shape: no hash, no walk
         case 9: return launch_wsweep_t<2, 8704, 6, false, true, 0, 1>(a, stream);  // the one-block loop
+        case 12: return launch_wsweep_t<2, 8704, 6, false, true, 0, 2, false>(a, stream);  // without the shared final mix16
+        case 13: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, true>(a, stream);  // the DMA as inline asm
         default: return hipErrorInvalidValue;
     }
 }
