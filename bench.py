@@ -284,14 +284,14 @@ def run_rank(args):
         result["regions"] = time_regions(coords, world, dev, backend, max_over_ranks, stream,
                                          gather=world > 1 and not args.no_allgather)
         if cfg != "cfg5" and A <= 128:
-            # ingest's purpose: regions, hashed + looked up in one launch
-            result["fused_regions"] = time_fused_batch(
+            # ingest's purpose: regions, hashed + looked up in one call
+            result["regions_entry_point"] = time_fused_batch(
                 types, blob, base, lens, n, A, dev, stream, max_over_ranks,
                 result["roofline"]["kernel_ms"], result["regions"]["lookup_ms"])
         if cfg == "cfg5":
             # the sweep's purpose: the new regions, decoded + hashed + looked up
-            # in one launch with no coordinate written (hdx_hash_encoded_regions_device)
-            result["fused_regions"] = time_fused_sweep(
+            # in one call with no coordinate returned (hdx_hash_encoded_regions_device)
+            result["regions_entry_point"] = time_fused_sweep(
                 types, (keys, key_off, key_len, vals, val_off, val_len), n, A, dev, stream, max_over_ranks,
                 result["roofline"]["kernel_ms"], result["regions"]["lookup_ms"])
 
@@ -726,8 +726,10 @@ def time_config(cfg, n, dev, stream, steps=10, warmup=2, warmup_ms=150.0):
 
 def time_fused_sweep(types, enc, n, A, dev, stream, max_over_ranks, sweep_ms, lookup_ms, reps=10):
     """hdx_hash_encoded_regions_device over the same stored objects and the
-    same two tables as time_regions, coordinates not written; next to the
-    sweep + separate lookups it replaces."""
+    same two tables as time_regions, coordinates not returned; next to the
+    sweep + separate lookups.  `form`: what the library runs at this size
+    (one fused launch, or from 2^20 objects the sweep + per-table lookups
+    through pooled scratch; include/hdxhash.h)."""
     import torch
 
     import hyperdex_amd as hdx
@@ -743,15 +745,18 @@ def time_fused_sweep(types, enc, n, A, dev, stream, max_over_ranks, sweep_ms, lo
     (ms,) = max_over_ranks(float(np.mean([s.elapsed_time(e) for s, e in ev])))
     for t in tables:
         t.close()
-    return {"tables": len(tables), "fused_ms": round(ms, 4),
+    return {"tables": len(tables), "ms": round(ms, 4),
+            "form": "sweep + per-table lookups" if n >= (1 << 20) and A <= 128 else "fused launch",
             "separate_ms": round(sweep_ms + lookup_ms, 4),
             "mobjects_per_s": round(n / (ms / 1e3) / 1e6, 2)}
 
 
 def time_fused_batch(types, blob, base, lens, n, A, dev, stream, max_over_ranks, hash_ms, lookup_ms, reps=10):
     """hdx_hash_batch_regions_device over the same batch and the same two
-    tables as time_regions, coordinates not written (the ingest path needs
-    only the regions); next to the hash + separate lookups it replaces."""
+    tables as time_regions, coordinates not returned (the ingest path needs
+    only the regions); next to the hash + separate lookups.  `form`: what the
+    library runs (mixed schemas from 2^20 objects: hash + per-table lookups
+    through pooled scratch, else one fused launch; include/hdxhash.h)."""
     import torch
 
     import hyperdex_amd as hdx
@@ -767,7 +772,9 @@ def time_fused_batch(types, blob, base, lens, n, A, dev, stream, max_over_ranks,
     (ms,) = max_over_ranks(float(np.mean([s.elapsed_time(e) for s, e in ev])))
     for t in tables:
         t.close()
-    return {"tables": len(tables), "fused_ms": round(ms, 4),
+    by_lookup = hdx.hashing.kernel_for(types, n)[0] == 212 and n >= (1 << 20)
+    return {"tables": len(tables), "ms": round(ms, 4),
+            "form": "hash + per-table lookups" if by_lookup else "fused launch",
             "separate_ms": round(hash_ms + lookup_ms, 4),
             "mobjects_per_s": round(n / (ms / 1e3) / 1e6, 2)}
 

@@ -189,9 +189,14 @@ hdx_status hdx_lookup_region_device(hdx_region_table table, const uint64_t* coor
  * hashes and looks up: region_ids[t*n + i] = lookup_region(tables[t], the
  * coordinates of object i) for t < ntables (1..4) — the values
  * hdx_lookup_region_device would give on the coordinates hdx_hash_encoded_device
- * computes (an undecodable object's are zero).  coords may be NULL: then no
- * coordinate leaves the chip.  The tables' subspace attributes must be
- * < attrs_sz.  Device pointers, asynchronous; attrs_sz <= 128. */
+ * computes (an undecodable object's are zero).  coords may be NULL.  The
+ * tables' subspace attributes must be < attrs_sz.  Device pointers,
+ * asynchronous; attrs_sz <= 128.
+ * Implementation note: below 2^20 objects this is one fused launch; from
+ * 2^20 on, the hash and one lookup launch per table (faster there: the hash
+ * kernels are VALU-bound), and with coords NULL the coordinates then pass
+ * through device scratch of at most 4 GiB per call, allocated and freed
+ * stream-ordered on `stream` (hipMallocAsync / hipFreeAsync). */
 hdx_status hdx_hash_encoded_regions_device(const uint32_t* types, uint32_t attrs_sz,
                                            const uint8_t* keys, const uint64_t* key_off,
                                            const uint32_t* key_len, const uint8_t* vals,
@@ -205,10 +210,12 @@ hdx_status hdx_hash_encoded_regions_device(const uint32_t* types, uint32_t attrs
  * object and looks it up in ntables (1..4) region tables — region_ids[t*n + i]
  * = lookup_region(tables[t], hash(schema, key, value) of object i), what
  * hdx_lookup_region_device gives on hdx_hash_batch_device's coordinates.
- * coords may be NULL (then no coordinate leaves the chip: the ingest path
- * key_state::hash_objects -> point_leader / lookup_region needs only the
- * region).  Device pointers, asynchronous; attrs_sz <= 128; status_dev (may be
- * NULL) gets HDX_E_BADSIZE's bit for a numeric value not 0 or 8 bytes long. */
+ * coords may be NULL (the ingest path key_state::hash_objects -> point_leader
+ * / lookup_region needs only the region).  Device pointers, asynchronous;
+ * attrs_sz <= 128; status_dev (may be NULL) gets HDX_E_BADSIZE's bit for a
+ * numeric value not 0 or 8 bytes long.  Mixed string / numeric schemas from
+ * 2^20 objects on take hash + per-table lookups, with the scratch of
+ * hdx_hash_encoded_regions_device's note when coords is NULL. */
 hdx_status hdx_hash_batch_regions_device(const uint32_t* types, uint32_t attrs_sz, const uint8_t* blob,
                                          const uint64_t* obj_base, const uint32_t* attr_len, uint64_t n,
                                          const hdx_region_table* tables, uint32_t ntables,
