@@ -206,7 +206,7 @@ __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, 
 // GAP: the class straddling the pass boundary moves whole into the second
 // pass when pads allow (class_sort, hdx_regroup.h).
 template <int NCH, uint32_t WB, int SHAPE = 0, int HT = 0, int ORDER = 1, bool W128 = false, bool REGIONS = false,
-          bool GAP = false, bool ADMA = false>
+          bool GAP = false, bool ADMA = false, bool PU = true>
 __global__ void __launch_bounds__(256)
 hash_wstage_kernel(const BatchArgs args) {
     static_assert(NCH >= 1 && NCH <= 4 && WB % 16 == 0, "slot indices are 8 bits; windows whole DMA units");
@@ -233,7 +233,8 @@ hash_wstage_kernel(const BatchArgs args) {
 
     // ---- NCH class-sorted passes, coordinates parked over their descriptors ---
     bool bad = false;
-#pragma unroll
+    // PU 0: the pass loop not unrolled (one copy of the hash code instead of NCH)
+#pragma unroll(PU ? NCH : 1)
     for (int t = 0; t < NCH; ++t) {
         const uint32_t e = perm[t * 64 + lane];
         const uint32_t s = e & 0xffu;
@@ -264,7 +265,7 @@ hash_wstage_kernel(const BatchArgs args) {
 // sort.
 
 template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, int HT = 0, int ORDER = 1, bool W128 = false,
-          bool REGIONS = false, bool GAP = false, bool ADMA = false>
+          bool REGIONS = false, bool GAP = false, bool ADMA = false, bool PU = true>
 static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     // lane o holds object o's base and lane K the next group's first: K <= 63
     args.K = std::min<uint32_t>(std::min<uint32_t>((uint32_t)(64 * NCH) / args.A, KCAP), 63u);
@@ -273,7 +274,7 @@ static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA, PU>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
     return hipGetLastError();
 }
 

@@ -131,7 +131,7 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
 // SHAPE (debug forms 7 / 8, WRONG coordinates): 1 = no hash (a slot's
 // coordinate is its descriptor), 2 = no hash and no walk.
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
-          bool ASM = false>
+          bool ASM = false, bool PU = true>
 __global__ void __launch_bounds__(256)
 hash_sweep_wstage_kernel(const EncodedArgs a) {
     constexpr uint32_t SL = NCH * 64;
@@ -299,7 +299,8 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
     class_sort<NCH, GAP>(cnt, perm, cls, cd, ns, wave_fence);
 
     // ---- NCH class-sorted passes, coordinates parked over their descriptors ---
-#pragma unroll
+    // (PU 0: the loop not unrolled, one copy of the hash code instead of NCH)
+#pragma unroll(PU ? NCH : 1)
     for (int t = 0; t < NCH; ++t) {
         const uint32_t e = perm[t * 64 + lane];
         const uint32_t s = e & 0xffu, code = e >> 8;
@@ -340,14 +341,14 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
 }
 
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
-          bool ASM = false>
+          bool ASM = false, bool PU = true>
 static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
     const uint32_t K = std::min<uint32_t>(64 * NCH / a.A, KCAP);
     if (K == 0) return hipErrorInvalidValue;
     const uint64_t waves = (a.n + K - 1) / K;
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -384,6 +385,7 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 9: return launch_wsweep_t<2, 8704, 6, false, true, 0, 1>(a, stream);  // the one-block loop
         case 12: return launch_wsweep_t<2, 8704, 6, false, true, 0, 2, false>(a, stream);  // without the shared final mix16
         case 13: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, true>(a, stream);  // the DMA as inline asm
+        case 14: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false, false>(a, stream);  // pass loop not unrolled
         default: return hipErrorInvalidValue;
     }
 }
