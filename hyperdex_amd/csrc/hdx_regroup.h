@@ -127,6 +127,17 @@ __device__ __forceinline__ uint32_t work_class3(uint32_t code, uint32_t n, bool 
     return n > 32 ? 0u : n <= 16 ? 1u : 2u;
 }
 
+// work_class<1> without branches (selects only): a divergent if / else chain
+// costs exec-mask bookkeeping on every lane of the wave (ORDER 4 of the
+// wave-staged kernel, the sweep's BF form).
+__device__ __forceinline__ uint32_t work_class1_bf(uint32_t code, uint32_t n, bool valid) {
+    const uint32_t b = (n - 1) >> 6;
+    const uint32_t longc = b >= 4 ? 7u : 3u + b;
+    const uint32_t shortc = n > 32 ? 1u : n <= 16 ? 2u : 3u;
+    const uint32_t c = n > 64 ? longc : shortc;
+    return valid && code == CODE_STRING ? c : 0u;
+}
+
 // Wave-local counting sort of a wave's NCH * 64 slots by work class into
 // perm[] (slot | code << 8, pass t = perm[64 t .. 64 t + 63]); slots s >= ns
 // are pads (hashed as CODE_ZERO, results unused).  A pass pays for the union

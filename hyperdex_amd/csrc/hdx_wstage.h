@@ -171,7 +171,9 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
         const uint32_t orel = (uint32_t)__shfl((int)rel, (int)(o & 63), 64);
         const uint32_t doff = g.staged ? orel + off[c] : off[c];
         desc[s] = (uint64_t)doff | ((uint64_t)g.L[c] << 32);
-        g.cls[c] = ORDER == 3 ? work_class3(g.code[c], g.L[c], s < g.ns) : work_class<1>(g.code[c], g.L[c], s < g.ns);
+        g.cls[c] = ORDER == 3   ? work_class3(g.code[c], g.L[c], s < g.ns)
+                   : ORDER == 4 ? work_class1_bf(g.code[c], g.L[c], s < g.ns)
+                                : work_class<1>(g.code[c], g.L[c], s < g.ns);
     }
     return g;
 }

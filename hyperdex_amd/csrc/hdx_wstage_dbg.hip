@@ -150,11 +150,12 @@ hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int for
         case 16: return launch_wstage_t<2, 8832, 63, 0, true, 1, true>(args, stream);  // 12 with b128 window reads
         case 18: return launch_wstage_t<2, 8832, 63, 1, true>(args, stream);  // debug shape of 12: no hash (WRONG coordinates)
         case 19: return launch_wstage_t<2, 8832, 63, 0, 2, 1>(args, stream);  // the product without the pass-boundary gap
-        case 39: return launch_wstage_t<2, 8832, 63, 0, 1, 1, false, false, true, true>(args, stream);  // the product with the one-block loop
+        case 39: return launch_wstage_t<2, 8832, 63, 0, 1, 4, false, false, true, true>(args, stream);  // the product with the one-block loop
         case 40: return launch_wstage_t<2, 8832, 63, 0, 2, 1, false, false, true>(args, stream);  // the product with the DMA as the builtin
         case 41: return launch_wstage_t<2, 8832, 63, 1, 2, 1, false, false, true, true>(args, stream);  // debug shape of the product: no hash
-        case 42: return launch_wstage_t<2, 8832, 63, 0, 3, 1, false, false, true, true>(args, stream);  // the product with the shared final mix16
-        case 44: return launch_wstage_t<2, 8832, 63, 0, 2, 1, false, false, true, true, false>(args, stream);  // the product, pass loop not unrolled
+        case 42: return launch_wstage_t<2, 8832, 63, 0, 3, 4, false, false, true, true>(args, stream);  // the product with the shared final mix16
+        case 44: return launch_wstage_t<2, 8832, 63, 0, 2, 4, false, false, true, true, false>(args, stream);  // the product, pass loop not unrolled
+        case 45: return launch_wstage_t<2, 8832, 63, 0, 2, 1, false, false, true, true>(args, stream);  // the product with the branchy class (ORDER 1)
         // the slots class-sorted over the workgroup
         case 10: return launch_wgstage_t<2, 8832>(args, stream);
         case 11: return launch_wgstage_t<1, 4352>(args, stream);

@@ -87,6 +87,11 @@ __device__ __forceinline__ uint32_t sweep_class(uint32_t code, uint32_t n, bool 
     if (global) return 7;
     return std::min<uint32_t>(work_class<1>(code, n, true), 6u);
 }
+// ... with selects only (BF)
+__device__ __forceinline__ uint32_t sweep_class_bf(uint32_t code, uint32_t n, bool zero, bool global) {
+    const uint32_t c = std::min<uint32_t>(work_class1_bf(code, n, true), 6u);
+    return zero ? 0u : global ? 7u : c;
+}
 
 __device__ __forceinline__ uint64_t hash_global(const uint8_t* p, uint32_t code, uint32_t n, bool& bad) {
     return hash_blk<false, false, true>(code, p, n, consume_any<true>(issue_any<true>(code, p, n)), bad);
@@ -131,7 +136,7 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
 // SHAPE (debug forms 7 / 8, WRONG coordinates): 1 = no hash (a slot's
 // coordinate is its descriptor), 2 = no hash and no walk.
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
-          bool ASM = false, bool PU = true>
+          bool ASM = false, bool PU = true, bool BF = false>
 __global__ void __launch_bounds__(256)
 hash_sweep_wstage_kernel(const EncodedArgs a) {
     constexpr uint32_t SL = NCH * 64;
@@ -289,12 +294,22 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
     for (int c = 0; c < NCH; ++c) {
         const uint32_t s = (uint32_t)(c * 64 + lane);
         const bool valid = s < ns;
-        const uint64_t d = valid ? desc[s] : (uint64_t)kZero;
         const uint32_t j = s - div_small(s, a.a_magic) * A;
-        const bool zero = (uint32_t)d == kZero;
-        const uint32_t ln = (uint32_t)(d >> 32);
-        cd[c] = valid && !zero ? (uint32_t)codes[j] : (uint32_t)CODE_ZERO;
-        cls[c] = sweep_class(cd[c], ln & ~kGlobal, !valid || zero, (ln & kGlobal) != 0);
+        if constexpr (BF) {  // unguarded loads: s < SL and j < A are always inside desc / codes
+            const uint64_t d0 = desc[s];
+            const uint32_t c0 = codes[j];
+            const uint64_t d = valid ? d0 : (uint64_t)kZero;
+            const bool zero = (uint32_t)d == kZero;
+            const uint32_t ln = (uint32_t)(d >> 32);
+            cd[c] = valid && !zero ? c0 : (uint32_t)CODE_ZERO;
+            cls[c] = sweep_class_bf(cd[c], ln & ~kGlobal, !valid || zero, (ln & kGlobal) != 0);
+        } else {
+            const uint64_t d = valid ? desc[s] : (uint64_t)kZero;
+            const bool zero = (uint32_t)d == kZero;
+            const uint32_t ln = (uint32_t)(d >> 32);
+            cd[c] = valid && !zero ? (uint32_t)codes[j] : (uint32_t)CODE_ZERO;
+            cls[c] = sweep_class(cd[c], ln & ~kGlobal, !valid || zero, (ln & kGlobal) != 0);
+        }
     }
     class_sort<NCH, GAP>(cnt, perm, cls, cd, ns, wave_fence);
 
@@ -341,14 +356,14 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
 }
 
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
-          bool ASM = false, bool PU = true>
+          bool ASM = false, bool PU = true, bool BF = false>
 static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
     const uint32_t K = std::min<uint32_t>(64 * NCH / a.A, KCAP);
     if (K == 0) return hipErrorInvalidValue;
     const uint64_t waves = (a.n + K - 1) / K;
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU, BF>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -358,9 +373,9 @@ static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
 // lookups is faster (hdx_encoded.hip).  A <= kWsweepMaxAttrs.
 hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
-    if (a.T) return launch_wsweep_t<2, 8704, 6, true, true, 0, 3, false>(a, stream);
+    if (a.T) return launch_wsweep_t<2, 8704, 6, true, true, 0, 3, false, true, true>(a, stream);
     if (!a.coords) return hipErrorInvalidValue;
-    return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false>(a, stream);
+    return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false, true, true>(a, stream);
 }
 
 #ifndef HDX_DEBUG_BUILD
@@ -376,7 +391,7 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
     if (a.n == 0) return hipSuccess;
     if (!a.coords) return hipErrorInvalidValue;
     switch (form) {
-        case 0: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false>(a, stream);
+        case 0: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false, true, true>(a, stream);
         case 1: return launch_wsweep_t<2, 8704, 7>(a, stream);
         case 2: return launch_wsweep_t<3, 14336, 11>(a, stream);
         case 6: return launch_wsweep_t<2, 8704, 6, false, false, 0, 2>(a, stream);
@@ -385,7 +400,8 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 9: return launch_wsweep_t<2, 8704, 6, false, true, 0, 1>(a, stream);  // the one-block loop
         case 12: return launch_wsweep_t<2, 8704, 6, false, true, 0, 2, false>(a, stream);  // without the shared final mix16
         case 13: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, true>(a, stream);  // the DMA as inline asm
-        case 14: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false, false>(a, stream);  // pass loop not unrolled
+        case 14: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false, false, true>(a, stream);  // pass loop not unrolled
+        case 15: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false, true, false>(a, stream);  // the branchy class, guarded loads
         default: return hipErrorInvalidValue;
     }
 }
