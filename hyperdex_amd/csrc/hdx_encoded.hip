@@ -449,8 +449,8 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
         // 236 = 230 without the pass-boundary gap, 237 / 238 its debug shapes (no hash / no hash, no walk),
         // 239 = 230 with the one-block > 64-byte loop, 242 without the shared final mix16,
         // 243 with the DMA as inline asm, 244 with the pass loop not unrolled, 245 with the
-        // branchy class
-        case 230: case 231: case 232: case 236: case 237: case 238: case 239: case 242: case 243: case 244: case 245: {
+        // branchy class, 246 without TNUM
+        case 230: case 231: case 232: case 236: case 237: case 238: case 239: case 242: case 243: case 244: case 245: case 246: {
             const hipError_t e = launch_hash_wsweep(a, stream, hash_variant() - 230);
             if (e != hipErrorInvalidValue) return e;
             break;

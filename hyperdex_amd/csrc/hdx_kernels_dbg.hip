@@ -727,7 +727,7 @@ hipError_t launch_debug_variant(const BatchArgs& args, hipStream_t stream, int v
         // wave-staged (hdx_wstage.hip): 200 2 passes / 10 KiB, 201 3 / 14 KiB, 202 2 / 8 KiB,
         // 203 1 / 5 KiB, 204 4 / 18 KiB, 205 2 / 8832 B, 206 = 205 with <= 6 objects
         case 200: case 201: case 202: case 203: case 204: case 205: case 206: case 207: case 208:
-        case 209: case 210: case 211: case 213: case 214: case 215: case 216: case 218: case 219: case 239: case 240: case 241: case 242: case 244: case 245: {
+        case 209: case 210: case 211: case 213: case 214: case 215: case 216: case 218: case 219: case 239: case 240: case 241: case 242: case 244: case 245: case 246: {
             const hipError_t e = launch_hash_wstage(args, stream, variant - 200);
             return e == hipErrorInvalidValue ? launch_hash_batch_variant(args, stream, 44) : e;
         }
@@ -793,6 +793,7 @@ static bool known_variant(int v) {
         case 243:  // 230 with the DMA as inline asm
         case 244:  // 212 / 230 with the pass loop not unrolled
         case 245:  // 212 / 230 with the branchy work class (and, 230, guarded loads)
+        case 246:  // 212 / 230 without TNUM (numerics read apart from the strings' tail)
         case 220: case 221: case 222:  // streamed (hdx_stream.hip)
         case 230: case 231: case 232: case 233: case 234:  // wave-staged sweep (hdx_wsweep.hip; 233: fused regions; 234: the gather sweep's fused regions)
         case 236:  // 230 without the pass-boundary gap

@@ -270,56 +270,76 @@ __device__ __forceinline__ uint64_t city_le16_ht(uint64_t h0, uint64_t t3, uint3
 // HashLen0to16 / 17to32 / 33to64 / the > 64-byte tail block) and, over 64
 // bytes, the loop blocks.  The window needs 32 readable bytes before off
 // (s[n-32, n) of a short string) and 36 after the value's end.
-// LOOP: city_gt64_lds's; LOOP 3 = LOOP 2 with one final mix16 shared by the
-// > 64-byte regime and the 8..32-byte ones (a pass holding both runs it once).
+// A string slot from its last 32 bytes t (already read) and, as its regime
+// needs, its first 32 and its loop blocks (hash_slot_window's string side).
 template <bool W128 = false, int LOOP = 1>
-__device__ __forceinline__ uint64_t hash_slot_window(ldsw_t w, uint32_t code, uint32_t off, uint32_t n, bool& bad) {
-    if (code == CODE_STRING) {
-        const Q32 t = lds_read32<W128>(w, off + n - 32);  // s[n-32, n): the front pad covers n < 32
-        const u64x2 t01 = {t.q0, t.q1}, t23 = {t.q2, t.q3};
-        if constexpr (LOOP >= 3) {
-            uint64_t u, v, mul;
-            if (n > 64) {
-                const Q32 q = lds_read32<W128>(w, off + n - 64);
-                Blk b;
-                b.v0 = u64x2{q.q0, q.q1};
-                b.v1 = u64x2{q.q2, q.q3};
-                b.v2 = t01;
-                b.v3 = t23;
-                city_gt64_lds_uv<W128, 2>(w, off, n, b, u, v);
-                mul = KMUL;
-            } else {
-                const Q32 h = lds_read32<W128>(w, off);  // s[0, 32): the back pad covers n < 32
-                if (n > 32) return city_33to64(u64x2{h.q0, h.q1}, u64x2{h.q2, h.q3}, t01, t23, n);
-                if (n < 8) return city_le16_ht(h.q0, t.q3, n);
-                mul = K2 + 2ull * n;
-                if (n > 16) {  // city.cc:305-313 (city_17to32)
-                    const uint64_t a = h.q0 * K1, b = h.q1, c = t.q3 * mul, d = t.q2 * K2;
-                    u = ror(a + b, 43) + ror(c, 30) + d;
-                    v = a + ror(b + K2, 18) + c;
-                } else {  // city.cc:281-286 (city_le16_ht, n >= 8)
-                    const uint64_t a = h.q0 + K2;
-                    u = ror(t.q3, 37) * mul + a;
-                    v = (ror(a, 25) + t.q3) * mul;
-                }
-            }
-            return mix16(u, v, mul);
-        }
+__device__ __forceinline__ uint64_t hash_string_window(ldsw_t w, uint32_t off, uint32_t n, const Q32& t) {
+    const u64x2 t01 = {t.q0, t.q1}, t23 = {t.q2, t.q3};
+    if constexpr (LOOP >= 3) {
+        uint64_t u, v, mul;
         if (n > 64) {
-            const Q32 u = lds_read32<W128>(w, off + n - 64);
+            const Q32 q = lds_read32<W128>(w, off + n - 64);
             Blk b;
-            b.v0 = u64x2{u.q0, u.q1};
-            b.v1 = u64x2{u.q2, u.q3};
+            b.v0 = u64x2{q.q0, q.q1};
+            b.v1 = u64x2{q.q2, q.q3};
             b.v2 = t01;
             b.v3 = t23;
-            return city_gt64_lds<W128, (LOOP > 2 ? 2 : LOOP)>(w, off, n, b);
+            city_gt64_lds_uv<W128, 2>(w, off, n, b, u, v);
+            mul = KMUL;
+        } else {
+            const Q32 h = lds_read32<W128>(w, off);  // s[0, 32): the back pad covers n < 32
+            if (n > 32) return city_33to64(u64x2{h.q0, h.q1}, u64x2{h.q2, h.q3}, t01, t23, n);
+            if (n < 8) return city_le16_ht(h.q0, t.q3, n);
+            mul = K2 + 2ull * n;
+            if (n > 16) {  // city.cc:305-313 (city_17to32)
+                const uint64_t a = h.q0 * K1, b = h.q1, c = t.q3 * mul, d = t.q2 * K2;
+                u = ror(a + b, 43) + ror(c, 30) + d;
+                v = a + ror(b + K2, 18) + c;
+            } else {  // city.cc:281-286 (city_le16_ht, n >= 8)
+                const uint64_t a = h.q0 + K2;
+                u = ror(t.q3, 37) * mul + a;
+                v = (ror(a, 25) + t.q3) * mul;
+            }
         }
-        const Q32 h = lds_read32<W128>(w, off);  // s[0, 32): the back pad covers n < 32
-        const u64x2 h01 = {h.q0, h.q1};
-        if (n > 32) return city_33to64(h01, u64x2{h.q2, h.q3}, t01, t23, n);
-        if (n > 16) return city_17to32(h01, t23, n);
-        return city_le16_ht(h.q0, t.q3, n);
+        return mix16(u, v, mul);
     }
+    if (n > 64) {
+        const Q32 u = lds_read32<W128>(w, off + n - 64);
+        Blk b;
+        b.v0 = u64x2{u.q0, u.q1};
+        b.v1 = u64x2{u.q2, u.q3};
+        b.v2 = t01;
+        b.v3 = t23;
+        return city_gt64_lds<W128, (LOOP > 2 ? 2 : LOOP)>(w, off, n, b);
+    }
+    const Q32 h = lds_read32<W128>(w, off);  // s[0, 32): the back pad covers n < 32
+    const u64x2 h01 = {h.q0, h.q1};
+    if (n > 32) return city_33to64(h01, u64x2{h.q2, h.q3}, t01, t23, n);
+    if (n > 16) return city_17to32(h01, t23, n);
+    return city_le16_ht(h.q0, t.q3, n);
+}
+
+// LOOP: city_gt64_lds's; LOOP 3 = LOOP 2 with one final mix16 shared by the
+// > 64-byte regime and the 8..32-byte ones (a pass holding both runs it once).
+// TNUM: every slot reads its last 32 bytes before the type dispatch, and an
+// 8-byte numeric takes its value from them (q3) — one read for the numeric
+// and string lanes of a pass instead of two.
+template <bool W128 = false, int LOOP = 1, bool TNUM = false>
+__device__ __forceinline__ uint64_t hash_slot_window(ldsw_t w, uint32_t code, uint32_t off, uint32_t n, bool& bad) {
+    if constexpr (TNUM) {
+        if (code == CODE_ZERO) return 0;
+        const Q32 t = lds_read32<W128>(w, off + n - 32);  // the front pad covers n < 32
+        if (code != CODE_STRING) {
+            if (n != 8 && n != 0) {
+                bad = true;
+                return 0;
+            }
+            return hash_numeric(code, n == 8 ? t.q3 : 0);
+        }
+        return hash_string_window<W128, LOOP>(w, off, n, t);
+    }
+    if (code == CODE_STRING)
+        return hash_string_window<W128, LOOP>(w, off, n, lds_read32<W128>(w, off + n - 32));  // front pad: n < 32
     if (code == CODE_ZERO) return 0;
     uint64_t bits = 0;
     if (n == 8) {

@@ -155,7 +155,8 @@ hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int for
         case 41: return launch_wstage_t<2, 8832, 63, 1, 2, 1, false, false, true, true>(args, stream);  // debug shape of the product: no hash
         case 42: return launch_wstage_t<2, 8832, 63, 0, 3, 4, false, false, true, true>(args, stream);  // the product with the shared final mix16
         case 44: return launch_wstage_t<2, 8832, 63, 0, 2, 4, false, false, true, true, false>(args, stream);  // the product, pass loop not unrolled
-        case 45: return launch_wstage_t<2, 8832, 63, 0, 2, 1, false, false, true, true>(args, stream);  // the product with the branchy class (ORDER 1)
+        case 45: return launch_wstage_t<2, 8832, 63, 0, 5, 1, false, false, true, true>(args, stream);  // the product with the branchy class (ORDER 1)
+        case 46: return launch_wstage_t<2, 8832, 63, 0, 2, 4, false, false, true, true>(args, stream);  // the product without TNUM
         // the slots class-sorted over the workgroup
         case 10: return launch_wgstage_t<2, 8832>(args, stream);
         case 11: return launch_wgstage_t<1, 4352>(args, stream);

@@ -133,6 +133,7 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
 // parked in LDS; coordinates are stored only when a.coords is set.
 // GAP: the class straddling the pass boundary moves whole into the second
 // pass when pads allow (class_sort, hdx_regroup.h).
+// LOOP: hash_slot_window's; + 10: with TNUM.
 // SHAPE (debug forms 7 / 8, WRONG coordinates): 1 = no hash (a slot's
 // coordinate is its descriptor), 2 = no hash and no walk.
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
@@ -336,7 +337,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         if (s < ns && off != kZero) {
             if (ln & kGlobal) h = hash_global((j == 0 ? a.keys : a.vals) + ob + off, code, ln & ~kGlobal, bad);
             else if (SHAPE) h = d ^ lw[off >> 2];
-            else h = hash_slot_window<false, LOOP>(lw, code, off, ln, bad);
+            else h = hash_slot_window<false, (LOOP >= 10 ? LOOP - 10 : LOOP), (LOOP >= 10)>(lw, code, off, ln, bad);
         }
         desc[s] = h;
     }
@@ -373,9 +374,9 @@ static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
 // lookups is faster (hdx_encoded.hip).  A <= kWsweepMaxAttrs.
 hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
-    if (a.T) return launch_wsweep_t<2, 8704, 6, true, true, 0, 3, false, true, true>(a, stream);
+    if (a.T) return launch_wsweep_t<2, 8704, 6, true, true, 0, 13, false, true, true>(a, stream);
     if (!a.coords) return hipErrorInvalidValue;
-    return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false, true, true>(a, stream);
+    return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true>(a, stream);
 }
 
 #ifndef HDX_DEBUG_BUILD
@@ -391,7 +392,7 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
     if (a.n == 0) return hipSuccess;
     if (!a.coords) return hipErrorInvalidValue;
     switch (form) {
-        case 0: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false, true, true>(a, stream);
+        case 0: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true>(a, stream);
         case 1: return launch_wsweep_t<2, 8704, 7>(a, stream);
         case 2: return launch_wsweep_t<3, 14336, 11>(a, stream);
         case 6: return launch_wsweep_t<2, 8704, 6, false, false, 0, 2>(a, stream);
@@ -401,7 +402,8 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 12: return launch_wsweep_t<2, 8704, 6, false, true, 0, 2, false>(a, stream);  // without the shared final mix16
         case 13: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, true>(a, stream);  // the DMA as inline asm
         case 14: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false, false, true>(a, stream);  // pass loop not unrolled
-        case 15: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false, true, false>(a, stream);  // the branchy class, guarded loads
+        case 15: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, false>(a, stream);  // the branchy class, guarded loads
+        case 16: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false, true, true>(a, stream);  // without TNUM
         default: return hipErrorInvalidValue;
     }
 }

@@ -304,10 +304,10 @@ def test_full_size_sampled(oracle, torch_dev, cfg):
 
 
 VARIANTS = [12, 18, 19, 20, 21, 25, 26, 30, 31, 35, 37, 38, 39, 44, 45, 46, 60, 61, 62, 63, 64, 65, 66, 67, 68, 69, 70, 71, 72, 73, 80, 81, 82, 83, 84, 85, 86, 90, 140, 141, 142, 143, 144, 145, 146, 147, 150, 151, 152, 153, 154, 155, 160, 161, 180, 181, 182, 190, 191,
-            200, 201, 202, 203, 204, 205, 206, 210, 211, 212, 214, 215, 216, 219, 220, 239, 240, 242, 244, 245, 221, 222]
+            200, 201, 202, 203, 204, 205, 206, 210, 211, 212, 214, 215, 216, 219, 220, 239, 240, 242, 244, 245, 246, 221, 222]
 
 
-@pytest.mark.parametrize("variant", [200, 201, 202, 203, 204, 205, 206, 210, 211, 212, 214, 215, 216, 219, 220, 221, 222, 239, 240, 242, 244, 245])
+@pytest.mark.parametrize("variant", [200, 201, 202, 203, 204, 205, 206, 210, 211, 212, 214, 215, 216, 219, 220, 221, 222, 239, 240, 242, 244, 245, 246])
 def test_wave_staged_layouts(oracle, torch_dev, variant):
     """The wave-staged kernel (hdx_wstage.hip) stages a group's span only when
     its objects are back to back and fit the window: gaps after some objects
