@@ -42,12 +42,21 @@ class SynthRule(ctypes.Structure):
     _fields_ = [("type", _u32), ("kind", _u32), ("lo", _u32), ("hi", _u32)]
 
 
+class Shard(ctypes.Structure):
+    """struct hdx_shard (include/hdxhash.h): one device's shard."""
+    _fields_ = [("blob", _vp), ("obj_base", _vp), ("attr_len", _vp), ("n", _u64), ("coords", _vp),
+                ("status_dev", _vp)]
+
+
 SIGNATURES = [
     ("hdx_abi_version", _i32, []),
     ("hdx_version", _cp, []),
     ("hdx_init", _i32, [_i32]),
     ("hdx_init_mask", _i32, [_u64]),
     ("hdx_shutdown", _i32, []),
+    ("hdx_device_set", _i32, [_vp, _i32]),
+    ("hdx_shard_ranges", _i32, [_vp, _u32, _u64, _u32, ctypes.c_double, _vp]),
+    ("hdx_hash_batch_device_multi", _i32, [_vp, _u32, ctypes.POINTER(Shard), _u32, _i32]),
     ("hdx_device_count", _i32, []),
     ("hdx_last_error", _cp, []),
     ("hdx_sync", _i32, [_vp]),
@@ -80,6 +89,7 @@ SIGNATURES = [
     ("hdx_synth_lengths", _i32, [ctypes.POINTER(SynthRule), _u32, _u64, _u64, _u64, _vp, _vp]),
     ("hdxdbg_kernel_for", _i32, [_vp, _u32, _u64, ctypes.POINTER(ctypes.c_char_p)]),
     ("hdxdbg_stream_probe", _i32, [_vp, _u64, _vp, _i32, _vp]),
+    ("hdxdbg_region_chunk_objects", _u64, [_u64, _u32]),
     ("hdx_synth_fill", _i32, [ctypes.POINTER(SynthRule), _u32, _u64, _u64, _u64, _vp, _vp, _vp,
                               _u64, _vp]),
 ]

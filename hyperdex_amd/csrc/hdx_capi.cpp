@@ -182,9 +182,9 @@ static bool is_numeric_code(uint8_t c) { return c >= CODE_INT64; }
 
 static constexpr uint64_t kChunkBytes = 128ull << 20;  // blob bytes per in-flight chunk
 
-static hdx_status hash_host(const uint8_t* codes, uint32_t A, const uint8_t* blob,
-                            uint64_t blob_bytes, const uint64_t* obj_base,
-                            const uint32_t* attr_len, uint64_t n, uint64_t* coords) {
+hdx_status hash_host(const uint8_t* codes, uint32_t A, const uint8_t* blob,
+                     uint64_t blob_bytes, const uint64_t* obj_base,
+                     const uint32_t* attr_len, uint64_t n, uint64_t* coords) {
     hdx_status st = bind_device(-1);
     if (st != HDX_OK) return st;
     ThreadState& ts = t_state;
@@ -328,22 +328,26 @@ HDX_EXPORT hdx_status hdx_init_mask(uint64_t device_mask) {
     std::call_once(g_probe_once, probe);
     if (device_mask == 0) return fail(HDX_E_INVALID, "empty device mask");
     if (g_ndev <= 0) return fail(HDX_E_DEVICE, "no HIP device visible");
-    int first = -1;
+    std::vector<int> devs;
     for (int d = 0; d < 64; ++d) {
         if (!(device_mask >> d & 1)) continue;
         if (d >= g_ndev) return fail(HDX_E_INVALID, "device %d in the mask >= device count %d", d, g_ndev);
         if (!g_is_gfx950[d]) return fail(HDX_E_DEVICE, "device %d is not gfx950 (MI355X)", d);
-        if (first < 0) first = d;
+        devs.push_back(d);
     }
-    hdx_status st = bind_device(first);
+    hdx_status st = bind_device(devs[0]);
     if (st != HDX_OK) return st;
     hipStream_t s;
-    return thread_stream(&s);
+    if ((st = thread_stream(&s)) != HDX_OK) return st;
+    // one worker, stream set and staging per device (hdx_multi.cpp)
+    return device_set_create(device_mask, devs);
 }
 
 HDX_EXPORT hdx_status hdx_shutdown(void) {
-    // each release() binds its scratch's device; the caller's current device
-    // is restored afterwards, so its lazy rebind returns to the same device
+    // the device set's workers exit first (their scratch is released as they
+    // do); then each remaining release() binds its scratch's device and the
+    // caller's current device is restored, so its lazy rebind returns to it
+    device_set_teardown();
     int dev = -1;
     const bool had = hipGetDevice(&dev) == hipSuccess;
     {
@@ -542,6 +546,8 @@ HDX_EXPORT hdx_status hdx_hash_batch_host(const uint32_t* types, uint32_t attrs_
     if (!obj_base || !attr_len || !coords || (!blob && blob_bytes))
         return fail(HDX_E_INVALID, "NULL host pointer");
     static const uint8_t one = 0;
+    if (host_batch_uses_set())  // hdx_init_mask: split over its devices (hdx_multi.cpp)
+        return hash_host_set(codes, attrs_sz, blob ? blob : &one, blob_bytes, obj_base, attr_len, n, coords);
     return hash_host(codes, attrs_sz, blob ? blob : &one, blob_bytes, obj_base, attr_len, n, coords);
 }
 
@@ -728,6 +734,10 @@ HDX_EXPORT int hdxdbg_stream_probe(const void* src, uint64_t bytes, uint64_t* si
     if (!src || (write && !sink) || write < 0 || write > 4 || bytes % 4096) return HDX_E_INVALID;
     HIP_TRY(launch_stream_probe((const uint8_t*)src, bytes, sink, write, (hipStream_t)stream));
     return HDX_OK;
+}
+
+HDX_EXPORT uint64_t hdxdbg_region_chunk_objects(uint64_t n, uint32_t attrs_sz) {
+    return attrs_sz ? regions_chunk_objects(n, attrs_sz) : 0;
 }
 
 HDX_EXPORT int hdxdbg_kernel_for(const uint32_t* types, uint32_t attrs_sz, uint64_t n, const char** name) {

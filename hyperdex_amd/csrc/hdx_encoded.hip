@@ -402,7 +402,10 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
                     b.T = 0;
                     return launch_hash_wsweep_product(b, stream);
                 };
-                return regions_by_lookup(a.n, a.A, a.t, a.T, a.coords, hash, stream);
+                bool no_scratch = false;
+                const hipError_t e = regions_by_lookup(a.n, a.A, a.t, a.T, a.coords, hash, stream, &no_scratch);
+                if (!no_scratch) return e;
+                // no scratch for the coordinates: the gather sweep's fused form below
             }
         }
         // stage each indexed table (index + ids) in LDS while they fit in 16 KiB together

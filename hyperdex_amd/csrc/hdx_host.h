@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cstddef>
+#include <vector>
 
 #include "hdx_internal.h"
 
@@ -34,6 +35,18 @@ void untrack_scratch(Scratch* s);
 hdx_status bind_device(int want);
 // The calling thread's library stream (created on first use).
 hdx_status thread_stream(hipStream_t* out);
+// The single-device host-resident pipeline (hdx_capi.cpp) on the calling
+// thread's device: codes validated, n > 0.
+hdx_status hash_host(const uint8_t* codes, uint32_t A, const uint8_t* blob, uint64_t blob_bytes,
+                     const uint64_t* obj_base, const uint32_t* attr_len, uint64_t n, uint64_t* coords);
+// The device set of hdx_init_mask (hdx_multi.cpp): create (replacing a set
+// of another mask), tear down (joins its workers), and the host-resident
+// batch split over it.
+hdx_status device_set_create(uint64_t mask, const std::vector<int>& devs);
+void device_set_teardown();
+bool host_batch_uses_set();
+hdx_status hash_host_set(const uint8_t* codes, uint32_t A, const uint8_t* blob, uint64_t blob_bytes,
+                         const uint64_t* obj_base, const uint32_t* attr_len, uint64_t n, uint64_t* coords);
 
 template <typename T>
 inline hdx_status grow_dev(T** p, size_t* cap, size_t need) {

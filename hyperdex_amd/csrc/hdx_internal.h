@@ -107,16 +107,19 @@ hipError_t launch_lookup_region(const RegionArgs& a, hipStream_t stream);
 // [first, first + count) into c.  With coords, all n objects are hashed there
 // first; without, chunks of at most kRegionChunkBytes of coordinates go
 // through a stream-ordered scratch buffer (hipMallocAsync; each chunk pays a
-// launch tail: config 3b 4.59 / 3.72 / 3.52 ms with 16 / 64 / 256 MiB chunks,
-// 3.47 unchunked, profiles/r3/ab_regions_by_lookup.jsonl).
-// Debug variant 235: by lookup at any n, 64 MiB chunks (tests).
+// launch tail of ~0.01 ms: config 3b 4.59 / 3.72 / 3.52 ms with 16 / 64 /
+// 256 MiB chunks, 3.47 unchunked, profiles/r3/ab_regions_by_lookup.jsonl).
+// If that scratch cannot be allocated nothing is launched and *no_scratch is
+// set: the caller then runs its fused form, which needs none.
+// Debug variant 235: by lookup at any n, 64 MiB chunks (tests); 247: the
+// same with the scratch allocation failing (the fallback).
 using RegionHashFn = std::function<hipError_t(uint64_t first, uint64_t count, uint64_t* coords)>;
-constexpr uint64_t kRegionChunkBytes = 4ull << 30;
+constexpr uint64_t kRegionChunkBytes = 1ull << 30;
 constexpr uint64_t kRegionLookupMinObjects = 1ull << 20;
 bool regions_by_lookup_pays(uint64_t n);
 uint64_t regions_chunk_objects(uint64_t n, uint32_t A);
 hipError_t regions_by_lookup(uint64_t n, uint32_t A, const SweepTable* t, uint32_t T, uint64_t* coords,
-                             const RegionHashFn& hash, hipStream_t stream);
+                             const RegionHashFn& hash, hipStream_t stream, bool* no_scratch);
 
 // Several subspaces at once (the batcher's prev/this/next lookups): table t's
 // region ids for object i go to out[t * out_stride + i].

@@ -91,7 +91,10 @@ hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream) 
                 b.T = 0;
                 return launch_hash_wstage_product(b, stream);
             };
-            return regions_by_lookup(args.n, args.A, args.t, args.T, args.coords, hash, stream);
+            bool no_scratch = false;
+            const hipError_t e = regions_by_lookup(args.n, args.A, args.t, args.T, args.coords, hash, stream,
+                                                   &no_scratch);
+            return no_scratch ? launch_hash_wstage_regions(args, stream) : e;
         }
         default: return launch_regroup_regions<3, true, true, true, 1, true>(args, stream);
     }

@@ -799,6 +799,7 @@ static bool known_variant(int v) {
         case 236:  // 230 without the pass-boundary gap
         case 237: case 238:  // 230's debug shapes: no hash / no hash, no walk (WRONG coordinates)
         case 235:  // regions by hash + separate lookups at any n, 64 MiB chunks (hdx_regions.hip)
+        case 247:  // 235 with the scratch allocation failing: the fused fallback
         case 223: case 224: case 225: case 226: case 227:  // its debug shapes (WRONG coordinates)
         case 210: case 211:  // wave-staged, sorted over the workgroup
         case 40: case 41:

@@ -161,7 +161,7 @@ hipError_t launch_lookup_region(const RegionArgs& a, hipStream_t stream) {
 
 bool regions_by_lookup_pays(uint64_t n) {
 #if HDX_DEBUG_BUILD
-    if (hash_variant() == 235) return true;
+    if (hash_variant() == 235 || hash_variant() == 247) return true;
 #endif
     return n >= kRegionLookupMinObjects;
 }
@@ -169,18 +169,35 @@ bool regions_by_lookup_pays(uint64_t n) {
 uint64_t regions_chunk_objects(uint64_t n, uint32_t A) {
     uint64_t bytes = kRegionChunkBytes;
 #if HDX_DEBUG_BUILD
-    if (hash_variant() == 235) bytes = 64ull << 20;  // tests: several chunks at small n
+    if (hash_variant() == 235 || hash_variant() == 247) bytes = 64ull << 20;  // tests: several chunks at small n
 #endif
     return std::min<uint64_t>(n, std::max<uint64_t>(1, bytes / (8ull * A)));
 }
 
 hipError_t regions_by_lookup(uint64_t n, uint32_t A, const SweepTable* t, uint32_t T, uint64_t* coords,
-                             const RegionHashFn& hash, hipStream_t stream) {
+                             const RegionHashFn& hash, hipStream_t stream, bool* no_scratch) {
+    *no_scratch = false;
     if (n == 0) return hipSuccess;
     const uint64_t chunk = coords ? n : regions_chunk_objects(n, A);
     uint64_t* scratch = nullptr;
     hipError_t e = hipSuccess;
-    if (!coords && (e = hipMallocAsync((void**)&scratch, chunk * A * 8, stream)) != hipSuccess) return e;
+    if (!coords) {
+        e = hipMallocAsync((void**)&scratch, chunk * A * 8, stream);
+#if HDX_DEBUG_BUILD
+        if (e == hipSuccess && hash_variant() == 247) {  // tests: the allocation "fails"
+            (void)hipFreeAsync(scratch, stream);
+            scratch = nullptr;
+            e = hipErrorOutOfMemory;
+        }
+#endif
+        if (e != hipSuccess) {
+            // nothing launched yet: the caller runs its fused form, which
+            // needs no scratch (no new out-of-memory failure)
+            (void)hipGetLastError();
+            *no_scratch = true;
+            return hipSuccess;
+        }
+    }
     for (uint64_t first = 0; first < n && e == hipSuccess; first += chunk) {
         const uint64_t count = std::min(chunk, n - first);
         uint64_t* c = coords ? coords + first * A : scratch;

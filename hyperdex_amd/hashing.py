@@ -240,3 +240,70 @@ def kernel_for(types, n: int):
     name = ctypes.c_char_p()
     v = lib().hdxdbg_kernel_for(t.ctypes.data, len(t), n, ctypes.byref(name))
     return v, (name.value or b"").decode()
+
+
+# ---- the device set (hdx_init_mask; include/hdxhash.h "multi-device") ------
+
+def init_mask(mask: int) -> None:
+    """hdx_init_mask: the process's device set (bit d = HIP ordinal d).  After
+    it hash_batch_host splits every batch over the set's devices, and
+    hash_batch_device_multi takes one shard per device."""
+    check(lib().hdx_init_mask(mask))
+
+
+def device_set():
+    """The device set's HIP ordinals (empty before init_mask)."""
+    buf = (ctypes.c_int * 64)()
+    k = lib().hdx_device_set(buf, 64)
+    return list(buf[:k])
+
+
+def shutdown() -> None:
+    """hdx_shutdown: tear the device set down and free every thread's scratch."""
+    check(lib().hdx_shutdown())
+
+
+def shard_ranges(attr_len, attrs_sz: int, n: int, world: int, equal_count_tol: float = 0.0):
+    """hdx_shard_ranges (the C++ cut rule): (first, count) per shard, the
+    same cuts as hyperdex_amd.dist.shard_ranges(n, world, per-object bytes)."""
+    first = np.zeros(world + 1, dtype=np.uint64)
+    if attr_len is None:
+        check(lib().hdx_shard_ranges(None, attrs_sz, n, world, equal_count_tol, first.ctypes.data))
+    else:
+        lens = np.ascontiguousarray(attr_len, dtype=np.uint32)
+        assert lens.size == n * attrs_sz
+        check(lib().hdx_shard_ranges(lens.ctypes.data, attrs_sz, n, world, equal_count_tol, first.ctypes.data))
+    f = [int(x) for x in first]
+    return [(f[k], f[k + 1] - f[k]) for k in range(world)]
+
+
+def hash_batch_device_multi(types, shards, gather: bool = True, coords=None):
+    """hdx_hash_batch_device_multi: shards[k] = (blob, obj_base, attr_len) torch
+    tensors on the k-th device of the set (status tensors optional as a 4th
+    item).  gather: returns one (N, A) int64 matrix per device, every device
+    holding all rows (RCCL over the set); else each shard's own (n_k, A)
+    coordinates.  `coords` may pass those output tensors in."""
+    import torch
+
+    t = _u32_array(types)
+    A = len(t)
+    counts = [int(s[1].numel()) for s in shards]
+    N = sum(counts)
+    outs = []
+    arr = (_lib.Shard * max(len(shards), 1))()
+    for k, s in enumerate(shards):
+        blob, base, lens = s[0], s[1], s[2]
+        status = s[3] if len(s) > 3 else None
+        _check_packed(blob, base, lens, A)
+        rows = N if gather else counts[k]
+        out = coords[k] if coords is not None else torch.empty((rows, A), dtype=torch.int64, device=base.device)
+        _check_out(out, rows * A, base.device, "coords")
+        _check_status(status, base.device)
+        outs.append(out)
+        arr[k] = _lib.Shard(blob.data_ptr(), base.data_ptr(), lens.data_ptr(), counts[k], out.data_ptr(),
+                            status.data_ptr() if status is not None else None)
+    # the library's streams run the work: order it after torch's current streams
+    for s in shards:
+        torch.cuda.current_stream(s[1].device).synchronize()
+    check(lib().hdx_hash_batch_device_multi(t.ctypes.data, A, arr, len(shards), 1 if gather else 0))
+    return outs

@@ -37,9 +37,14 @@
  * exactly as in the reference (hash.cc:40-43).
  *
  * Threading: every entry point is thread-safe.  Device work is issued on the
- * caller's stream (batch API; NULL = null stream) or on per-thread library
- * streams (host-resident and per-object API).  There is no CPU implementation behind any entry point:
- * without a usable gfx950 device every compute call returns HDX_E_DEVICE.
+ * caller's stream (batch API; NULL = null stream) or on library streams
+ * (host-resident and multi-device API).
+ *
+ * Two implementations, split by call shape: the per-object entry points
+ * (hdx_hash_value / hdx_hash_key / hdx_hash_object, the C forms of
+ * common/hash.h) run on the host CPU, bit-exact, with no device and no
+ * allocation; every batch entry point runs the gfx950 kernels, with no CPU
+ * substitute — without a usable gfx950 device it returns HDX_E_DEVICE.
  */
 #ifndef HDXHASH_H
 #define HDXHASH_H
@@ -76,14 +81,25 @@ const char* hdx_version(void);
  * gfx950 part.  Optional: every entry point initialises lazily on device 0
  * or on the thread's current HIP device. */
 hdx_status hdx_init(int device);
-/* Checks that every device in device_mask (bit d = HIP ordinal d) is a
- * visible gfx950 part, binds the calling thread to the lowest one and creates
- * its stream (hdx_init(device_mask)). */
+/* The process's device set (hdx_init(device_mask)).  Checks that
+ * every device in device_mask (bit d = HIP ordinal d) is a visible gfx950
+ * part, binds the calling thread to the lowest one, and creates per device
+ * one worker thread (with its own streams and pinned / device staging) and
+ * one stream; the RCCL communicator over the set is created on the first
+ * gathering hdx_hash_batch_device_multi.  From then on hdx_hash_batch_host
+ * splits every batch over the set, and hdx_hash_batch_device_multi takes one
+ * shard per device.  Calling it again with the same mask does nothing; with
+ * another mask it replaces the set (no call may be in progress). */
 hdx_status hdx_init_mask(uint64_t device_mask);
-/* Frees every thread's library scratch (streams, pinned and device staging)
- * after waiting for the work queued on it.  No call may be in progress;
- * region tables and batchers are the caller's to destroy.  Threads rebind
- * lazily on their next call. */
+/* The device set's HIP ordinals, ascending, into devices[0..max_devices);
+ * returns how many devices it has (0: no hdx_init_mask yet). */
+int hdx_device_set(int* devices, int max_devices);
+/* Tears the device set down (joins its workers, destroys its streams and
+ * communicator) and frees every thread's library scratch (streams, pinned
+ * and device staging) after waiting for the work queued on it.  No call may
+ * be in progress; region tables and batchers are the caller's to destroy.
+ * Threads rebind lazily on their next call; the host-resident path runs on
+ * the calling thread's device again until the next hdx_init_mask. */
 hdx_status hdx_shutdown(void);
 /* Number of HIP devices visible (0 without a GPU; never initialises one). */
 int hdx_device_count(void);
@@ -121,13 +137,54 @@ hdx_status hdx_hash_batch_device(const uint32_t* types, uint32_t attrs_sz,
  * overlapping H2D copies, kernels and D2H copies on two streams, and
  * validates numeric sizes and object extents on the host chunk by chunk
  * ahead of the copies.  blob_bytes is the size of the blob allocation (every
- * object must lie inside it).  On HDX_E_BADSIZE / HDX_E_INVALID nothing is in
- * flight when the call returns; coordinates of objects before the offending
- * one may have been written, the rest are untouched. */
+ * object must lie inside it).  After hdx_init_mask the batch is split into
+ * one contiguous object range per device of the set, balanced by payload
+ * bytes (hdx_shard_ranges with no equal-count tolerance), and each device's
+ * worker pipelines its range into its rows of coords; without a device set
+ * the calling thread's device takes the whole batch.  On HDX_E_BADSIZE /
+ * HDX_E_INVALID nothing is in flight when the call returns and the status
+ * is the first failing range's (in device order); coordinates of other
+ * objects may have been written. */
 hdx_status hdx_hash_batch_host(const uint32_t* types, uint32_t attrs_sz,
                                const uint8_t* blob, uint64_t blob_bytes,
                                const uint64_t* obj_base, const uint32_t* attr_len,
                                uint64_t n, uint64_t* coords);
+
+/* ---- multi-device (the device set of hdx_init_mask) ---------------------- */
+
+/* Contiguous object ranges, one per shard, balanced by payload bytes (SURVEY
+ * §8e; the rule of hyperdex_amd/dist.py shard_ranges): object i's size is
+ * the sum of attr_len[i*attrs_sz .. +attrs_sz), and shard k starts at the
+ * first object whose byte prefix reaches k/world of the total.  With
+ * equal_count_tol > 0 the equal-count cuts (n*k/world) are taken instead
+ * whenever every shard's bytes stay within that fraction of the mean share
+ * (so the gather needs no padding).  attr_len NULL: equal counts.  Output:
+ * first[0..world], first[world] = n.  Host only; no device needed. */
+hdx_status hdx_shard_ranges(const uint32_t* attr_len, uint32_t attrs_sz, uint64_t n, uint32_t world,
+                            double equal_count_tol, uint64_t* first);
+
+/* One device's shard of a device-resident batch (the packed layout above;
+ * device pointers on that device). */
+typedef struct hdx_shard {
+    const uint8_t* blob;
+    const uint64_t* obj_base;   /* offsets into this shard's blob */
+    const uint32_t* attr_len;   /* n * attrs_sz */
+    uint64_t n;                 /* objects in this shard (may be 0) */
+    uint64_t* coords;           /* gather: the whole (N x attrs_sz) matrix on this
+                                   device, N = the shards' total; else this
+                                   shard's own (n x attrs_sz) rows */
+    uint32_t* status_dev;       /* may be NULL; as hdx_hash_batch_device */
+} hdx_shard;
+/* Hashes shards[k] on the k-th device of the set (nshards = the set's size)
+ * on the library's per-device streams.  gather != 0: shard k is hashed into
+ * rows [first_k, first_k + n_k) of its device's matrix (first_k = the
+ * earlier shards' total), then the rows are exchanged over the devices' RCCL
+ * communicator (ncclCommInitAll over the set, xGMI) in ONE group: an
+ * in-place all-gather when every shard has the same count, else one in-place
+ * broadcast per shard — no staging memory either way — so every device ends
+ * with all N rows.  Synchronous: returns when every device is done. */
+hdx_status hdx_hash_batch_device_multi(const uint32_t* types, uint32_t attrs_sz, const hdx_shard* shards,
+                                       uint32_t nshards, int gather);
 
 /* Reindex sweep over stored objects: value i is
  * vals[val_off[i], +val_len[i]) in the daemon's on-disk encoding

@@ -2,8 +2,9 @@
  * hdxhash_debug.h — measurement and tuning hooks (not part of the drop-in
  * boundary).
  *
- * Both libraries: hdxdbg_kernel_for (which kernel the automatic policy runs)
- * and hdxdbg_stream_probe (bench.py's practical HBM ceiling).
+ * Both libraries: hdxdbg_kernel_for (which kernel the automatic policy runs),
+ * hdxdbg_stream_probe (bench.py's practical HBM ceiling) and
+ * hdxdbg_region_chunk_objects (tests/test_scale.py's chunk edges).
  * libhdxhash_dbg.so only (HDX_DEBUG_BUILD, hyperdex_amd/csrc/Makefile):
  * hdxdbg_set_kernel_variant / hdxdbg_kernel_variant, used by
  * scripts/ab_variants.py and the variant parity tests.  The product library
@@ -34,6 +35,9 @@ int hdxdbg_kernel_for(const uint32_t* types, uint32_t attrs_sz, uint64_t n, cons
  * 64-byte-attribute configs).  Asynchronous on `stream`.  bench.py reports the
  * rate as the practical ceiling beside the HBM3E spec. */
 int hdxdbg_stream_probe(const void* src, uint64_t bytes, uint64_t* sink, int write, void* stream);
+/* Objects per scratch chunk of the regions entry points when the caller
+ * wants no coordinates (n objects of attrs_sz attributes; hdx_regions.hip). */
+uint64_t hdxdbg_region_chunk_objects(uint64_t n, uint32_t attrs_sz);
 
 #ifdef __cplusplus
 }

@@ -306,7 +306,7 @@ def _encoded_regions_fused(oracle, with_coords):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["chunks", "product"])
+@pytest.mark.parametrize("case", ["chunks", "product", "no_scratch"])
 @pytest.mark.parametrize("with_coords", [False, True])
 def test_gpu_encoded_regions_by_lookup(oracle, case, with_coords):
     """The product's regions sweep from 2^20 objects on is the wave-staged
@@ -325,7 +325,7 @@ def test_gpu_encoded_regions_by_lookup(oracle, case, with_coords):
     dev = torch.device("cuda", 0)
     rules = [synth.Rule(synth.dt.HYPERDATATYPE_STRING, synth.UNIFORM, 0, 40),
              synth.Rule(synth.dt.HYPERDATATYPE_INT64, synth.NUMERIC, 8, 8)] * 50
-    if case == "chunks":
+    if case in ("chunks", "no_scratch"):
         n, attrs3 = 200_003, [1, 2, 99]
     else:
         rules, n, attrs3 = rules[:2] + rules[:1], (1 << 20) + 4097, [1, 2, 0]
@@ -336,7 +336,8 @@ def test_gpu_encoded_regions_by_lookup(oracle, case, with_coords):
     tables = [RegionTable(at, lo, up, np.arange(1, len(lo) + 1, dtype=np.uint64) * 11) for at, lo, up in specs]
     versions = torch.empty(n, dtype=torch.int64, device=dev)
     status = torch.zeros(1, dtype=torch.int32, device=dev)
-    with _lib.debug_library(235) if case == "chunks" else contextlib.nullcontext():
+    variant = {"chunks": 235, "no_scratch": 247}.get(case)
+    with _lib.debug_library(variant) if variant else contextlib.nullcontext():
         out = hdx.hash_encoded_regions(types, *_to_dev(torch, dev, enc), tables, coords=with_coords,
                                        versions=versions, status=status)
         torch.cuda.synchronize()

@@ -225,7 +225,7 @@ WIDE_MIXED = ([synth.Rule(synth.dt.HYPERDATATYPE_STRING, synth.UNIFORM, 0, 40),
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["chunks", "product"])
+@pytest.mark.parametrize("case", ["chunks", "product", "no_scratch"])
 @pytest.mark.parametrize("with_coords", [False, True])
 def test_gpu_batch_regions_by_lookup(oracle, case, with_coords):
     """Large mixed-schema batches take hash + separate lookups (hdx_kernels.hip
@@ -233,13 +233,15 @@ def test_gpu_batch_regions_by_lookup(oracle, case, with_coords):
     (by lookup at any n, 64 MiB of scratch per chunk when no coordinates are
     wanted): 100 attributes -> 83 886 objects per chunk, so 200 003 objects are
     3 chunks, the last one ragged.  "product": the product library from its
-    threshold (2^20 objects) on."""
+    threshold (2^20 objects) on.  "no_scratch": debug variant 247, the same
+    with the scratch allocation failing — the call falls back to the fused
+    launch, which needs none."""
     import torch
 
     import hyperdex_amd as hdx
     from hyperdex_amd import RegionTable, _lib
     dev = torch.device("cuda", 0)
-    if case == "chunks":
+    if case in ("chunks", "no_scratch"):
         rules, n, attrs3 = WIDE_MIXED, 200_003, [1, 2, 99]
     else:
         rules, n, attrs3 = WIDE_MIXED[:2] + WIDE_MIXED[:1], (1 << 20) + 4097, [1, 2, 0]
@@ -248,7 +250,8 @@ def test_gpu_batch_regions_by_lookup(oracle, case, with_coords):
     want_coords, _ = oracle.hash_batch(types, blob, base, lens)
     specs = [([0],) + tuple(oracle.partition(1, 64)), (attrs3,) + tuple(oracle.partition(3, 64))]
     tables = [RegionTable(at, lo, up, np.arange(1, len(lo) + 1, dtype=np.uint64) * 5) for at, lo, up in specs]
-    with _lib.debug_library(235) if case == "chunks" else contextlib.nullcontext():
+    variant = {"chunks": 235, "no_scratch": 247}.get(case)
+    with _lib.debug_library(variant) if variant else contextlib.nullcontext():
         out = hdx.hash_batch_regions(types, torch.from_numpy(blob).to(dev),
                                      torch.from_numpy(base.view(np.int64)).to(dev),
                                      torch.from_numpy(lens.view(np.int32)).to(dev), tables, coords=with_coords)
