@@ -238,6 +238,15 @@ HDX_EXPORT hdx_status hdx_search_space(const hdx_region_table* tables, uint32_t 
         rmax = std::max(rmax, tables[i]->R);
     }
     if (rmax && !include) return fail(HDX_E_INVALID, "NULL include");
+    // configuration.cc:761-768: an invalid range clears the server list before
+    // any subspace is looked at (so also with no subspaces at all)
+    for (uint32_t k = 0; k < nranges; ++k) {
+        if (ranges[k].invalid) {
+            *cleared = 1;
+            if (rmax) std::memset(include, 0, rmax);
+            return HDX_OK;
+        }
+    }
     // configuration.cc:771-866: subspaces in order; the first initialises the
     // choice, a later one replaces it only if its server set is non-empty and
     // no larger (so the last of equal non-empty sizes wins); a cleared server

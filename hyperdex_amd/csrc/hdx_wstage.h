@@ -257,15 +257,8 @@ hash_wstage_kernel(const BatchArgs args) {
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-// The same groups, the slots class-sorted over the whole workgroup (4 waves,
-// 4 * NCH * 64 slots) instead of one wave: a pass then runs one or two
-// CityHash regimes instead of three to five.  Every byte is already in the
-// workgroup's LDS, so a wave may hash any wave's slot; three barriers per
-// workgroup (counts published; permutation and every window landed; parked
-// coordinates complete).  A wave whose group is not staged hashes its own
-// slots from global memory before the first barrier and takes no part in the
-// sort.
-
+// Launch: K = floor(64 * NCH / A) whole objects per wave (at most 63), four
+// independent waves per 256-thread workgroup, no workgroup barrier.
 template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, int HT = 0, int ORDER = 1, bool W128 = false,
           bool REGIONS = false, bool GAP = false, bool ADMA = false, bool PU = true>
 static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {

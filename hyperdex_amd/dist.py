@@ -102,7 +102,14 @@ def allgather_coords(local, counts: Sequence[int], group=None, out=None):
     is copied there.  Equal counts: the all-gather runs in place in `out`
     (this rank's rows are its input), no padding, no copy.  Unequal counts
     (byte-balanced shards): every block is padded to the largest count in one
-    staging matrix, gathered there, and its rows copied into `out`."""
+    staging matrix, gathered there, and its rows copied into `out`.
+
+    Memory: the unequal form allocates that staging matrix (world *
+    max(counts) * A elements) beside `out`, roughly doubling the gather's
+    device memory (config 4: +13.6 GB); shard_ranges(..., equal_count_tol)
+    avoids it whenever equal counts stay within the tolerance, and the
+    C-ABI's hdx_hash_batch_device_multi gathers unequal counts with grouped
+    in-place broadcasts and no staging."""
     import torch
     import torch.distributed as dist
 

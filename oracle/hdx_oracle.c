@@ -538,6 +538,12 @@ int hdxo_search_space(uint32_t ntables, const uint32_t* D, const uint32_t* R, co
     int initialized = 0, chosen = -1; /* :771-772 */
     uint32_t smallest = 0;
     *cleared = 0;
+    for (uint32_t k = 0; k < nranges; ++k) { /* :761-768, before any subspace */
+        if (ranges[k].invalid) {
+            *cleared = 1;
+            return -1;
+        }
+    }
     for (uint32_t i = 0; i < ntables; ++i) { /* :774 */
         uint8_t* mine = (uint8_t*)calloc(R[i] ? R[i] : 1, 1);
         int rc = hdxo_search_regions(D[i], R[i], attrs[i], lower[i], upper[i],

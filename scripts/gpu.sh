@@ -11,6 +11,8 @@
 #   smoke              __graft_entry__.smoke()
 #   bench[=ARGS]       python bench.py ARGS   (ARGS: commas for spaces)
 #   ab=CFG:V1,V2[:R]   scripts/ab_variants.py, interleaved A/B of debug variants
+#   pmc=CFG:V1,V2[:SET] counter passes over scripts/run_kernel.py per variant (pmc_profile.sh),
+#                      summarised by pmc_summary.py; SET "lds" = the LDS / VALU / wait set
 #   profile            scripts/profile_r2.sh TAG (round evidence: traces + PMC traffic)
 #   py=SCRIPT[,ARGS]   python SCRIPT ARGS (commas for spaces)
 set -o pipefail
@@ -41,6 +43,18 @@ for STEP in "$@"; do
       IFS=: read -r cfg vars reps <<< "$arg"
       timeout -k 10 600 python -u scripts/ab_variants.py --configs "$cfg" --variants="$vars" --reps "${reps:-9}" \
           > "$log" 2> "$log.err" ;;
+    pmc)
+      IFS=: read -r cfg vars set <<< "$arg"
+      if [ "$set" = lds ]; then
+        export PMC_SETS="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES GRBM_GUI_ACTIVE;SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY;FETCH_SIZE;WRITE_SIZE"
+      fi
+      rc=0
+      for v in ${vars//,/ }; do
+        timeout -k 10 600 bash scripts/pmc_profile.sh "$TAG" "$cfg" "$v" >> "$log" 2>&1 || { rc=$?; break; }
+        echo "== $cfg v$v" >> "$log"
+        python scripts/pmc_summary.py "gpurun_out/pmc_${TAG}_${cfg}_v$v" >> "$log" 2>&1 || { rc=$?; break; }
+      done
+      (exit $rc) ;;
     profile)
       timeout -k 10 1100 bash scripts/profile_r2.sh "$TAG" > "$log" 2>&1 ;;
     py)

@@ -259,9 +259,26 @@ def test_oracle_search_space_choice(oracle):
     sp[3][1][5, 1], sp[3][2][5, 1] = sp[3][2][5, 1], sp[3][1][5, 1]
     c, inc, cl = oracle.search_space(sp, [(2, INT64, i64(-5), None)])
     assert c == -1 and cl
-    # an invalid range clears before any subspace
+    # an invalid range clears before any subspace (:761-768) — with no subspaces too
     c, inc, cl = oracle.search_space(sp[:3], [(0, INT64, i64(0), None, True)])
     assert c == -1 and cl
+    c, inc, cl = oracle.search_space([], [(0, INT64, i64(0), None, True)])
+    assert c == -1 and cl
+
+
+def test_search_space_invalid_range_without_subspaces():
+    """hdx_search_space rejects an invalid range before looking at any
+    subspace (configuration.cc:761-768), so ntables == 0 reports cleared
+    (ADVICE r3); no device is touched."""
+    import ctypes
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd.index import _ranges
+    arr = _ranges([(0, INT64, struct.pack("<q", 0), None, True)])
+    chosen, servers, cleared = ctypes.c_int32(7), ctypes.c_uint32(7), ctypes.c_int(0)
+    assert hdx.lib().hdx_search_space(None, 0, arr, 1, None, ctypes.byref(chosen), None, ctypes.byref(servers),
+                                      ctypes.byref(cleared)) == 0
+    assert (chosen.value, servers.value, cleared.value) == (-1, 0, 1)
 
 
 def _random_space(rng, oracle):
