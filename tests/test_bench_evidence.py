@@ -27,11 +27,12 @@ def test_traffic_file_is_used_only_for_its_own_sources():
 
 
 def test_default_profile_matches_default_kernel():
-    """profiles/<latest round>/default_bench_kernel_stats.csv holds the kernel
-    the default bench line names (roofline.kernel)."""
+    """default_bench_kernel_stats.csv of the latest round that has one holds
+    the kernel the default bench line names (roofline.kernel)."""
     from hyperdex_amd import synth
     from hyperdex_amd.hashing import kernel_for
-    rnd = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")))[-1]
+    rnd = sorted(os.path.dirname(p) for p in
+                 glob.glob(os.path.join(ROOT, "profiles", "r*", "default_bench_kernel_stats.csv")))[-1]
     stats = open(os.path.join(rnd, "default_bench_kernel_stats.csv")).read()
     _, name = kernel_for([r.type for r in synth.CONFIGS["cfg3a"]], 10_000_000)
     assert '"%s"' % name in stats, name
