@@ -24,6 +24,14 @@
 //                     the status and wakes the slot's callers, who copy their
 //                     rows out; the last reader frees the slot.
 //
+// Objects of at most host_max_bytes never reach any of that: the calling
+// thread hashes them with the per-object CPU path (hdx_cpu.cpp) and looks
+// them up in host copies of the tables — one core does a config-3b object in
+// ~0.15 us where the lone caller's device round trip costs ~36 us, so for
+// synchronous per-object callers the device only pays for large objects
+// (HDX_BATCHER_DEVICE_ONLY ships everything, for hosts whose
+// cores are needed elsewhere).
+//
 // Shipping as soon as the pipeline is idle keeps a lone caller's latency at
 // one round trip, while concurrent callers pile into the next batch during
 // the current one (batch size adapts to load).  With `slots` >= 2 buffers in
@@ -92,6 +100,8 @@ struct hdx_batcher_s {
     int device = -1;
     uint32_t A = 0;
     uint8_t codes[HDX_MAX_ATTRS];
+    uint32_t types[HDX_MAX_ATTRS];
+    uint64_t host_max_bytes = 0;  // 0 with HDX_BATCHER_DEVICE_ONLY
     uint32_t max_obj = 0;
     uint64_t max_bytes = 0;
     bool stage_device = false;
@@ -112,7 +122,7 @@ struct hdx_batcher_s {
     bool stop = false, flusher_done = false;
     std::thread flusher, completer;
 
-    std::atomic<uint64_t> n_objects{0}, n_batches{0}, n_full{0}, n_direct{0};
+    std::atomic<uint64_t> n_objects{0}, n_batches{0}, n_full{0}, n_direct{0}, n_host{0};
     std::atomic<int> spinners{0};
 };
 
@@ -403,6 +413,9 @@ HDX_EXPORT hdx_status hdx_batcher_create(const uint32_t* types, uint32_t attrs_s
     b->max_bytes = c.max_bytes ? c.max_bytes : (8ull << 20);
     b->delay = std::chrono::microseconds(c.max_delay_us ? c.max_delay_us : 50);
     b->stage_device = (c.flags & HDX_BATCHER_STAGE_DEVICE) != 0;
+    std::memcpy(b->types, types, attrs_sz * sizeof(uint32_t));
+    b->host_max_bytes = (c.flags & HDX_BATCHER_DEVICE_ONLY) ? 0
+                        : c.host_max_bytes ? c.host_max_bytes : HDX_BATCHER_HOST_MAX_BYTES;
     const uint32_t nslots = c.slots ? std::max(c.slots, 2u) : 4;
     for (uint32_t t = 0; t < c.ntables; ++t) {
         if (!c.tables[t]) {
@@ -461,6 +474,7 @@ HDX_EXPORT hdx_status hdx_batcher_get_stats(hdx_batcher b, hdx_batcher_stats* ou
     out->batches = b->n_batches.load();
     out->full_batches = b->n_full.load();
     out->direct = b->n_direct.load();
+    out->host = b->n_host.load();
     return HDX_OK;
 }
 
@@ -505,6 +519,16 @@ HDX_EXPORT hdx_status hdx_batcher_hash_object(hdx_batcher b, const uint8_t* key,
         if (b->codes[j] >= CODE_INT64 && L != 0 && L != 8)
             return fail(HDX_E_BADSIZE, "attribute %u: numeric value of %zu bytes", j, L);
         total += L;
+    }
+    if (b->host_max_bytes && total <= b->host_max_bytes) {
+        // the calling thread: the per-object CPU path and host lookups
+        hdx_status st = hdx_hash_object(b->types, b->A, key, key_len, values, value_lens, hs);
+        if (st != HDX_OK) return st;
+        if (region_ids)
+            for (size_t t = 0; t < b->tables.size(); ++t) region_ids[t] = region_lookup_host(b->tables[t], hs);
+        b->n_host.fetch_add(1, std::memory_order_relaxed);
+        b->n_objects.fetch_add(1, std::memory_order_relaxed);
+        return HDX_OK;
     }
     if (total > b->max_bytes) return hash_direct(b, total, key, key_len, values, value_lens, hs, region_ids);
 

@@ -652,6 +652,9 @@ HDX_EXPORT hdx_status hdx_region_table_create(uint32_t dims, uint32_t regions, c
     t->D = dims;
     t->R = regions;
     std::memcpy(t->attrs, attrs, dims * sizeof(uint16_t));
+    t->h_lower.assign(lower, lower + (size_t)regions * dims);
+    t->h_upper.assign(upper, upper + (size_t)regions * dims);
+    t->h_ids.assign(ids, ids + regions);
     const size_t box = (size_t)regions * dims * 8;
     if (hipMalloc((void**)&t->d_lower, box + 8) != hipSuccess ||
         hipMalloc((void**)&t->d_upper, box + 8) != hipSuccess ||

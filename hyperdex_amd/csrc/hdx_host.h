@@ -90,5 +90,24 @@ struct hdx_region_table_s {
     uint64_t* d_ids;
     uint64_t* d_index;  // interval index (NULL: lookups scan the boxes)
     uint32_t W, index_words;
+    // host copies (the batcher's calling-thread lookups)
+    std::vector<uint64_t> h_lower, h_upper, h_ids;
 };
+
+// configuration::lookup_region (common/configuration.cc:698-735) on the host:
+// the first region whose box holds hs[attrs[d]] on every dimension (bounds
+// inclusive), else 0 (region_id()).
+inline uint64_t region_lookup_host(const hdx_region_table_s* t, const uint64_t* hs) {
+    for (uint32_t r = 0; r < t->R; ++r) {
+        const uint64_t* lo = t->h_lower.data() + (size_t)r * t->D;
+        const uint64_t* up = t->h_upper.data() + (size_t)r * t->D;
+        bool in = true;
+        for (uint32_t d = 0; in && d < t->D; ++d) {
+            const uint64_t h = hs[t->attrs[d]];
+            in = lo[d] <= h && h <= up[d];
+        }
+        if (in) return t->h_ids[r];
+    }
+    return 0;
+}
 

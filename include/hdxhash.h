@@ -56,7 +56,7 @@
 extern "C" {
 #endif
 
-#define HDX_ABI_VERSION 2
+#define HDX_ABI_VERSION 3
 #define HDX_MAX_ATTRS 256
 
 typedef enum hdx_status {
@@ -347,11 +347,18 @@ hdx_status hdx_search_space(const hdx_region_table* tables, uint32_t ntables, co
 
 /* key_state::hash_objects (daemon/key_state.cc:1455-1543) hashes one or two
  * objects per replicated op, from every daemon::loop thread at once.  A
- * batcher coalesces those concurrent per-object calls into device batches:
- * each caller copies its object into a pinned staging buffer and blocks; a
- * flush thread ships a batch as soon as the previous one has completed, when
- * it is full, or `max_delay_us` after its first object, runs the hash kernel
- * (and the region lookups of the batcher's tables) and wakes the callers.
+ * batcher keeps that synchronous per-object call.  An object of at most
+ * host_max_bytes payload is hashed on the calling thread by the per-object
+ * CPU path (hdx_hash_object) and looked up in the batcher's tables on the
+ * host (configuration::lookup_region's scan) — one core hashes a config-3b
+ * object in ~0.15 us, while a device round trip costs ~36 us, so no batch
+ * of synchronous callers can beat the calling threads' own cores.  Larger
+ * objects (or every object, with HDX_BATCHER_DEVICE_ONLY, for hosts whose
+ * cores are needed elsewhere) are coalesced into device batches: each caller
+ * copies its object into a pinned staging buffer and blocks; a flush thread
+ * ships a batch as soon as the previous one has completed, when it is full,
+ * or `max_delay_us` after its first object, runs the hash kernel (and the
+ * region lookups of the batcher's tables) and wakes the callers.
  * One batcher per space (schema). */
 typedef struct hdx_batcher_s* hdx_batcher;
 typedef struct hdx_batcher_config {
@@ -363,16 +370,25 @@ typedef struct hdx_batcher_config {
     const hdx_region_table* tables; /* optional: subspaces to look every object up in */
     uint32_t ntables;        /* <= 16 */
     uint32_t flags;          /* HDX_BATCHER_* */
+    uint64_t host_max_bytes; /* objects of at most this many payload bytes are hashed on the
+                                calling thread; 0 = HDX_BATCHER_HOST_MAX_BYTES */
 } hdx_batcher_config;
 /* Stage batches through device memory (H2D, kernels, D2H) instead of letting
  * the kernels read and write the pinned staging buffers in place (default,
  * fewer operations per batch; best for the small batches of a daemon). */
 #define HDX_BATCHER_STAGE_DEVICE 1u
+/* Every object goes to the device, whatever its size (the calling threads'
+ * cores stay free for the rest of the daemon). */
+#define HDX_BATCHER_DEVICE_ONLY 2u
+/* The default host_max_bytes: the object size above which one device round
+ * trip (~36 us + PCIe) undercuts one core's hash (~7 GB/s), DESIGN.md §4.7. */
+#define HDX_BATCHER_HOST_MAX_BYTES (256u * 1024u)
 typedef struct hdx_batcher_stats {
     uint64_t objects;        /* objects hashed */
     uint64_t batches;        /* device batches shipped */
     uint64_t full_batches;   /* batches shipped because they were full */
-    uint64_t direct;         /* objects larger than max_bytes, hashed on their own */
+    uint64_t direct;         /* objects larger than max_bytes, hashed on the device on their own */
+    uint64_t host;           /* objects hashed on the calling thread */
 } hdx_batcher_stats;
 /* cfg may be NULL (all defaults).  The tables must outlive the batcher. */
 hdx_status hdx_batcher_create(const uint32_t* types, uint32_t attrs_sz, const hdx_batcher_config* cfg,
@@ -380,11 +396,12 @@ hdx_status hdx_batcher_create(const uint32_t* types, uint32_t attrs_sz, const hd
 /* Waits for in-flight batches, then frees everything.  No call may be in
  * progress on the batcher. */
 hdx_status hdx_batcher_destroy(hdx_batcher b);
-/* hdx_hash_object through the batcher: blocks until the object's batch has
- * run.  Thread-safe; any number of threads.  When the batcher has tables,
- * region_ids[t] receives lookup_region(tables[t], hs) (region_ids may be NULL
- * to skip).  A numeric attribute whose size is not 0 or 8 returns
- * HDX_E_BADSIZE before the object is queued. */
+/* hdx_hash_object through the batcher: returns once the object is hashed
+ * (on the calling thread, or after its device batch has run).  Thread-safe;
+ * any number of threads.  When the batcher has tables, region_ids[t]
+ * receives lookup_region(tables[t], hs) (region_ids may be NULL to skip).  A
+ * numeric attribute whose size is not 0 or 8 returns HDX_E_BADSIZE before
+ * anything is hashed. */
 hdx_status hdx_batcher_hash_object(hdx_batcher b, const uint8_t* key, size_t key_len,
                                    const uint8_t* const* values, const size_t* value_lens,
                                    uint64_t* hs, uint64_t* region_ids);

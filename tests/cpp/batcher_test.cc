@@ -56,6 +56,7 @@ int main(int argc, char** argv) {
     cfg.slots = argc > 4 ? (uint32_t)atoi(argv[4]) : 0;
     cfg.max_delay_us = argc > 5 ? (uint32_t)atoi(argv[5]) : 0;
     cfg.flags = argc > 6 ? (uint32_t)atoi(argv[6]) : 0;
+    cfg.host_max_bytes = argc > 7 ? (uint64_t)atoll(argv[7]) : 0;
     cfg.max_bytes = 64 << 10;  // objects above 64 KiB take the direct path
     cfg.device = -1;
     if (hdx_init(0) != HDX_OK) {
@@ -149,9 +150,10 @@ int main(int argc, char** argv) {
     hdx_batcher_destroy(b);
     hdx_region_table_destroy(key_space.h);
     hdx_region_table_destroy(sub.h);
-    printf("objects %llu batches %llu full %llu direct %llu checked %ld badsize %ld failures %ld\n",
+    printf("objects %llu batches %llu full %llu direct %llu host %llu checked %ld badsize %ld failures %ld\n",
            (unsigned long long)s.objects, (unsigned long long)s.batches, (unsigned long long)s.full_batches,
-           (unsigned long long)s.direct, checked.load(), badsize.load(), failures.load());
+           (unsigned long long)s.direct, (unsigned long long)s.host, checked.load(), badsize.load(),
+           failures.load());
     if (failures == 0 && checked + badsize == (long)threads * per_thread && s.objects == (uint64_t)checked) {
         printf("batcher ok\n");
         return 0;

@@ -29,17 +29,29 @@ def test_batcher_test_builds():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("args", [
-    ("16", "1500", "0", "0", "0"),      # defaults: 4096 objects, 4 slots, 50 us
-    ("8", "600", "7", "2", "10"),       # tiny batches, two slots: constant sealing/reuse
-    ("1", "200", "0", "0", "2000"),     # one caller: every batch ships on the deadline
-    ("48", "300", "64", "3", "100"),    # more callers than a batch holds
-    ("16", "800", "0", "0", "0", "1"),  # staged through HBM (HDX_BATCHER_STAGE_DEVICE)
+    # device batches (HDX_BATCHER_DEVICE_ONLY = 2)
+    ("16", "1500", "0", "0", "0", "2"),      # defaults: 4096 objects, 4 slots, 50 us
+    ("8", "600", "7", "2", "10", "2"),       # tiny batches, two slots: constant sealing/reuse
+    ("1", "200", "0", "0", "2000", "2"),     # one caller: every batch ships on the deadline
+    ("48", "300", "64", "3", "100", "2"),    # more callers than a batch holds
+    ("16", "800", "0", "0", "0", "3"),       # staged through HBM (| HDX_BATCHER_STAGE_DEVICE)
+    # the calling thread (default: objects up to 256 KiB), and a split at 300 bytes
+    ("16", "1500", "0", "0", "0", "0"),
+    ("16", "1500", "0", "0", "0", "0", "300"),
 ])
 def test_batcher_concurrent_callers_match_oracle(args):
     build()
     r = subprocess.run([EXE, *args], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "batcher ok" in r.stdout
+    host = int(r.stdout.split(" host ")[1].split()[0])
+    batches = int(r.stdout.split(" batches ")[1].split()[0])
+    if args[5] in ("2", "3"):
+        assert host == 0 and batches > 0, r.stdout       # everything on the device
+    elif len(args) == 6:
+        assert host > 0 and batches == 0, r.stdout       # everything on the calling threads
+    else:
+        assert host > 0 and batches > 0, r.stdout        # split by size
 
 
 @pytest.mark.gpu
@@ -54,7 +66,7 @@ def test_batcher_python_threads_match_oracle(oracle):
     lo, up = oracle.partition(1, 64)
     table = hdx.RegionTable([0], lo, up, np.arange(1, 65, dtype=np.uint64))
     errors = []
-    with hdx.Batcher(types, tables=[table], max_delay_us=200) as b:
+    with hdx.Batcher(types, tables=[table], max_delay_us=200, host_max_bytes=100) as b:
         def worker(t):
             rng = np.random.default_rng(t)
             for _ in range(150):
@@ -76,4 +88,4 @@ def test_batcher_python_threads_match_oracle(oracle):
         st = b.stats()
     table.close()
     assert not errors, errors[:2]
-    assert st["objects"] == 8 * 150 and st["batches"] >= 1
+    assert st["objects"] == 8 * 150 and st["batches"] >= 1 and st["host"] >= 1

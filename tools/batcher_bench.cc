@@ -1,6 +1,6 @@
 // Throughput and latency of the daemon batching shim.
 //
-//   batcher_bench [threads] [seconds] [max_objects] [delay_us] [tables] [flags]
+//   batcher_bench [threads] [seconds] [max_objects] [delay_us] [tables] [flags] [host_max_bytes] [scale]
 //
 // `threads` callers (daemon::loop threads) each hash config-3b objects (key
 // STRING 64 B; 10 STRING U{0..195}; 3 INT64; 3 FLOAT) through
@@ -59,6 +59,9 @@ int main(int argc, char** argv) {
     cfg.max_delay_us = argc > 4 ? (uint32_t)atoi(argv[4]) : 0;
     const uint32_t ntables = argc > 5 ? (uint32_t)atoi(argv[5]) : 3;
     cfg.flags = argc > 6 ? (uint32_t)atoi(argv[6]) : 0;
+    cfg.host_max_bytes = argc > 7 ? (uint64_t)atoll(argv[7]) : 0;
+    // scale > 1 multiplies every string length (object-size sweeps for the crossover)
+    const uint32_t scale = argc > 8 ? (uint32_t)atoi(argv[8]) : 1;
     cfg.device = -1;
     if (hdx_init(0) != HDX_OK) {
         fprintf(stderr, "init: %s\n", hdx_last_error());
@@ -78,7 +81,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     // pre-generated objects, 1024 per thread, reused round robin
-    const int kObj = 1024;
+    const int kObj = scale > 16 ? 64 : 1024;
     struct Obj {
         std::vector<uint8_t> bytes;
         size_t len[A];
@@ -90,7 +93,7 @@ int main(int argc, char** argv) {
         for (auto& o : objs[t]) {
             size_t total = 0;
             for (uint32_t j = 0; j < A; ++j) {
-                o.len[j] = j == 0 ? 64 : j <= 10 ? rng() % 196 : (rng() % 100 == 0 ? 0 : 8);
+                o.len[j] = j == 0 ? 64 : j <= 10 ? (rng() % 196) * scale : (rng() % 100 == 0 ? 0 : 8);
                 total += o.len[j];
             }
             o.bytes.resize(total);
@@ -148,12 +151,14 @@ int main(int argc, char** argv) {
     printf("{\"tool\": \"batcher_bench\", \"threads\": %d, \"tables\": %u, \"max_objects\": %u, "
            "\"max_delay_us\": %u, \"flags\": %u, \"objects_per_s\": %.0f, \"batches_per_s\": %.0f, "
            "\"mean_batch\": %.1f, \"full_batches\": %llu, \"lat_us_p50\": %.1f, \"lat_us_p90\": %.1f, "
-           "\"lat_us_p99\": %.1f, \"lat_us_max\": %.1f, \"errors\": %ld}\n",
+           "\"lat_us_p99\": %.1f, \"lat_us_max\": %.1f, \"errors\": %ld, \"host_objects_per_s\": %.0f, "
+           "\"host_max_bytes\": %llu, \"scale\": %u}\n",
            threads, cfg.ntables, cfg.max_objects ? cfg.max_objects : 4096,
            cfg.max_delay_us ? cfg.max_delay_us : 50, cfg.flags, objs_s, batches / el,
            batches > 0 ? (double)(s1.objects - s0.objects) / batches : 0.0,
            (unsigned long long)(s1.full_batches - s0.full_batches), pct(0.5), pct(0.9), pct(0.99),
-           pct(1.0), errors.load());
+           pct(1.0), errors.load(), (double)(s1.host - s0.host) / el, (unsigned long long)cfg.host_max_bytes,
+           scale);
     hdx_batcher_destroy(b);
     for (auto t : tables) hdx_region_table_destroy(t);
     return errors.load() ? 1 : 0;
