@@ -63,6 +63,10 @@ def parse_args(argv=None):
     ap.add_argument("--config", default="cfg3a")
     ap.add_argument("--objects", type=int, default=0,
                     help="objects per GPU (default 10M; 50M for cfg5, BASELINE config 5)")
+    ap.add_argument("--store-layout", default="columns", choices=("columns", "records"),
+                    help="cfg5's stored objects: 'columns' (each key in place in its packed object, values "
+                         "back to back: round 3's layout) or 'records' ([key][value] back to back, a "
+                         "LevelDB block's adjacency)")
     ap.add_argument("--config4-objects", type=int, default=100_000_000,
                     help="config 4: objects of the whole sharded batch (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -182,7 +186,7 @@ def run_rank(args):
         # config 5: reindex sweep over stored objects (values in the daemon's
         # on-disk encoding, keys apart) of the config-3b shape
         types, keys, key_off, key_len, vals, val_off, val_len = synth.make_encoded_device(
-            "cfg3b", n, first=rank * n, device=dev)
+            "cfg3b", n, first=rank * n, device=dev, layout=args.store_layout)
         A = len(types)
         key_bytes = int(key_len.to(torch.int64).sum().item())
         payload = key_bytes + int(val_len.to(torch.int64).sum().item())
@@ -260,7 +264,8 @@ def run_rank(args):
                                 }.get(cfg, cfg) +
                    ": %dM objects/GPU, key + %d attrs" % (n // 1_000_000, A - 1),
                    "objects_per_gpu": n, "attrs": A, "payload_bytes_per_gpu": payload,
-                   "parallelism": "shard%d" % world},
+                   "parallelism": "shard%d" % world,
+                   **({"store_layout": args.store_layout} if cfg == "cfg5" else {})},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4),
                      "traffic": traffic,

@@ -31,8 +31,8 @@ class _Stats(ctypes.Structure):
 class Batcher:
     """One per space: types = the schema's attribute types (attr 0 = key);
     tables = the subspaces every object is looked up in (RegionTable).
-    Objects up to host_max_bytes (0: the library's default crossover) are
-    hashed on the calling thread; device_only ships every object to the GPU."""
+    Objects up to host_max_bytes (0: every object) are hashed on the calling
+    thread; device_only ships every object to the GPU."""
 
     def __init__(self, types: Sequence[int], tables: Sequence[RegionTable] = (),
                  max_objects: int = 0, max_delay_us: int = 0, max_bytes: int = 0,

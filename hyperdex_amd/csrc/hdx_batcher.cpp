@@ -24,13 +24,15 @@
 //                     the status and wakes the slot's callers, who copy their
 //                     rows out; the last reader frees the slot.
 //
-// Objects of at most host_max_bytes never reach any of that: the calling
-// thread hashes them with the per-object CPU path (hdx_cpu.cpp) and looks
-// them up in host copies of the tables — one core does a config-3b object in
-// ~0.15 us where the lone caller's device round trip costs ~36 us, so for
-// synchronous per-object callers the device only pays for large objects
-// (HDX_BATCHER_DEVICE_ONLY ships everything, for hosts whose
-// cores are needed elsewhere).
+// By default no object reaches any of that: the calling thread hashes it with
+// the per-object CPU path (hdx_cpu.cpp) and looks it up in host copies of the
+// tables.  One core does a config-3b object in ~0.27 us with three lookups,
+// a lone caller's device round trip costs ~36 us, and at no object size does
+// the device win one synchronous object: CityHash is serial within a string,
+// so a 1 MB object takes 42 us on a core and 2.9 ms as a one-object device
+// batch.  host_max_bytes sends larger objects to the device;
+// HDX_BATCHER_DEVICE_ONLY ships everything, for hosts whose cores are needed
+// elsewhere (the device then does the work while the callers sleep).
 //
 // Shipping as soon as the pipeline is idle keeps a lone caller's latency at
 // one round trip, while concurrent callers pile into the next batch during
@@ -122,7 +124,18 @@ struct hdx_batcher_s {
     bool stop = false, flusher_done = false;
     std::thread flusher, completer;
 
-    std::atomic<uint64_t> n_objects{0}, n_batches{0}, n_full{0}, n_direct{0}, n_host{0};
+    std::atomic<uint64_t> n_objects{0}, n_batches{0}, n_full{0}, n_direct{0};
+    // calling-thread objects, counted per thread shard: one shared counter
+    // bounced between 16 callers' cores cost more than the hash itself
+    struct alignas(64) Shard {
+        std::atomic<uint64_t> v{0};
+    };
+    Shard n_host[32];
+    uint64_t host_total() const {
+        uint64_t s = 0;
+        for (const Shard& c : n_host) s += c.v.load(std::memory_order_relaxed);
+        return s;
+    }
     std::atomic<int> spinners{0};
 };
 
@@ -414,8 +427,7 @@ HDX_EXPORT hdx_status hdx_batcher_create(const uint32_t* types, uint32_t attrs_s
     b->delay = std::chrono::microseconds(c.max_delay_us ? c.max_delay_us : 50);
     b->stage_device = (c.flags & HDX_BATCHER_STAGE_DEVICE) != 0;
     std::memcpy(b->types, types, attrs_sz * sizeof(uint32_t));
-    b->host_max_bytes = (c.flags & HDX_BATCHER_DEVICE_ONLY) ? 0
-                        : c.host_max_bytes ? c.host_max_bytes : HDX_BATCHER_HOST_MAX_BYTES;
+    b->host_max_bytes = (c.flags & HDX_BATCHER_DEVICE_ONLY) ? 0 : c.host_max_bytes ? c.host_max_bytes : UINT64_MAX;
     const uint32_t nslots = c.slots ? std::max(c.slots, 2u) : 4;
     for (uint32_t t = 0; t < c.ntables; ++t) {
         if (!c.tables[t]) {
@@ -470,11 +482,12 @@ HDX_EXPORT hdx_status hdx_batcher_destroy(hdx_batcher b) {
 
 HDX_EXPORT hdx_status hdx_batcher_get_stats(hdx_batcher b, hdx_batcher_stats* out) {
     if (!b || !out) return fail(HDX_E_INVALID, "NULL pointer");
-    out->objects = b->n_objects.load();
+    const uint64_t host = b->host_total();
+    out->objects = b->n_objects.load() + host;
     out->batches = b->n_batches.load();
     out->full_batches = b->n_full.load();
     out->direct = b->n_direct.load();
-    out->host = b->n_host.load();
+    out->host = host;
     return HDX_OK;
 }
 
@@ -526,8 +539,9 @@ HDX_EXPORT hdx_status hdx_batcher_hash_object(hdx_batcher b, const uint8_t* key,
         if (st != HDX_OK) return st;
         if (region_ids)
             for (size_t t = 0; t < b->tables.size(); ++t) region_ids[t] = region_lookup_host(b->tables[t], hs);
-        b->n_host.fetch_add(1, std::memory_order_relaxed);
-        b->n_objects.fetch_add(1, std::memory_order_relaxed);
+        static std::atomic<uint32_t> next_shard{0};
+        thread_local const uint32_t shard = next_shard.fetch_add(1, std::memory_order_relaxed) % 32;
+        b->n_host[shard].v.fetch_add(1, std::memory_order_relaxed);
         return HDX_OK;
     }
     if (total > b->max_bytes) return hash_direct(b, total, key, key_len, values, value_lens, hs, region_ids);

@@ -458,6 +458,11 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
             if (e != hipErrorInvalidValue) return e;
             break;
         }
+        case 250: {  // the product sweep without the record span (round 3's key / value paths only)
+            const hipError_t e = launch_hash_wsweep(a, stream, 17);
+            if (e != hipErrorInvalidValue) return e;
+            break;
+        }
         default: break;
     }
     // 49: the gather sweep (the product's sweep up to round 2), for A/B runs

@@ -234,8 +234,9 @@ hipError_t launch_synth_lengths(const SynthArgs& a, uint32_t* attr_len, hipStrea
 hipError_t launch_synth_fill(const SynthArgs& a, const uint64_t* obj_base, const uint32_t* attr_len,
                              uint8_t* blob, uint64_t bytes, hipStream_t s);
 
+// records: each key is also written right before its value ([key][value])
 hipError_t launch_synth_encode(const uint8_t* blob, const uint64_t* obj_base, const uint32_t* attr_len,
                                uint32_t A, uint64_t n, uint64_t first_version, const uint64_t* val_off,
-                               uint8_t* vals, hipStream_t s);
+                               uint8_t* vals, hipStream_t s, bool records = false);
 
 }  // namespace hdx

@@ -103,6 +103,14 @@ __device__ __forceinline__ Blk lds_block64(ldsw_t w, uint32_t s) {
     return use64<true>(b, s & 3);
 }
 
+// Debug shapes (WRONG coordinates): W128 == 2 (variant 248) the same reads at
+// addresses whose 32 lanes of a half-wave fall on 32 distinct banks — what
+// the per-lane byte offsets' bank conflicts cost; W128 == 3 (249) the reads
+// at the dword floor with no funnel shift — what the v_alignbyte cost.
+__device__ __forceinline__ ldsw_t conflict_free(ldsw_t w, uint32_t o) {
+    return w + (((o >> 2) & ~1023u) | (uint32_t)(threadIdx.x & 31));
+}
+
 __device__ __forceinline__ Blk lds_block64_w128(ldsw_t w, uint32_t s) {
     const ldsw_t d = w + (s >> 2);
     const u32x4_t q0 = lds_q(d), q1 = lds_q(d + 4), q2 = lds_q(d + 8), q3 = lds_q(d + 12);
@@ -143,7 +151,7 @@ __device__ __forceinline__ void city_loop_step(uint64_t& x, uint64_t& y, uint64_
 
 // ... up to its last mix16: the result is mix16(u, v, KMUL) (LOOP 3 shares
 // that mix16 with the <= 32-byte regimes' own, hash_slot_window).
-template <bool W128 = false, int LOOP = 1>
+template <int W128 = 0, int LOOP = 1>
 __device__ __forceinline__ void city_gt64_lds_uv(ldsw_t w, uint32_t off, uint32_t n, const Blk& t, uint64_t& u,
                                                  uint64_t& v) {
     const u64x2 e0 = t.v0, e1 = t.v1, e2 = t.v2, e3 = t.v3;
@@ -154,7 +162,11 @@ __device__ __forceinline__ void city_gt64_lds_uv(ldsw_t w, uint32_t off, uint32_
     weak32(e0.x, e0.y, e1.x, e1.y, n, z, v0, v1);
     weak32(e2.x, e2.y, e3.x, e3.y, y + K1, x, w0, w1);
     const uint32_t blocks = (n - 1) >> 6;
-    auto rd = [&](uint32_t o) { return W128 ? lds_block64_w128(w, o) : lds_block64(w, o); };
+    auto rd = [&](uint32_t o) {
+        if constexpr (W128 == 2) return lds_block64(conflict_free(w, o), o & 3);
+        else if constexpr (W128 == 3) return lds_block64(w + (o >> 2), 0);
+        else return W128 ? lds_block64_w128(w, o) : lds_block64(w, o);
+    };
     if constexpr (LOOP >= 2) {
         Blk ba = rd(off);
         x = x * K1 + ba.v0.x;
@@ -182,7 +194,7 @@ __device__ __forceinline__ void city_gt64_lds_uv(ldsw_t w, uint32_t off, uint32_
     u = mix16(v0, w0, KMUL) + shiftmix(y) * K1 + z;
     v = mix16(v1, w1, KMUL) + x;
 }
-template <bool W128 = false, int LOOP = 1>
+template <int W128 = 0, int LOOP = 1>
 __device__ __forceinline__ uint64_t city_gt64_lds(ldsw_t w, uint32_t off, uint32_t n, const Blk& t) {
     uint64_t u, v;
     city_gt64_lds_uv<W128, LOOP>(w, off, n, t, u, v);
@@ -220,12 +232,12 @@ __device__ __forceinline__ uint64_t hash_numeric_lds(ldsw_t w, uint32_t code, ui
 struct Q32 {
     uint64_t q0, q1, q2, q3;
 };
-template <bool W128 = false>
+template <int W128 = 0>
 __device__ __forceinline__ Q32 lds_read32(ldsw_t w, uint32_t o) {
-    const ldsw_t d = w + (o >> 2);
-    const uint32_t r = o & 3;
+    const ldsw_t d = W128 == 2 ? conflict_free(w, o) : w + (o >> 2);
+    const uint32_t r = W128 == 3 ? 0 : o & 3;
     uint32_t x[9];
-    if constexpr (W128) {
+    if constexpr (W128 == 1) {
         const u32x4_t a = lds_q(d), b = lds_q(d + 4);
         x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w;
         x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
@@ -272,7 +284,7 @@ __device__ __forceinline__ uint64_t city_le16_ht(uint64_t h0, uint64_t t3, uint3
 // (s[n-32, n) of a short string) and 36 after the value's end.
 // A string slot from its last 32 bytes t (already read) and, as its regime
 // needs, its first 32 and its loop blocks (hash_slot_window's string side).
-template <bool W128 = false, int LOOP = 1>
+template <int W128 = 0, int LOOP = 1>
 __device__ __forceinline__ uint64_t hash_string_window(ldsw_t w, uint32_t off, uint32_t n, const Q32& t) {
     const u64x2 t01 = {t.q0, t.q1}, t23 = {t.q2, t.q3};
     if constexpr (LOOP >= 3) {
@@ -324,7 +336,7 @@ __device__ __forceinline__ uint64_t hash_string_window(ldsw_t w, uint32_t off, u
 // TNUM: every slot reads its last 32 bytes before the type dispatch, and an
 // 8-byte numeric takes its value from them (q3) — one read for the numeric
 // and string lanes of a pass instead of two.
-template <bool W128 = false, int LOOP = 1, bool TNUM = false>
+template <int W128 = 0, int LOOP = 1, bool TNUM = false>
 __device__ __forceinline__ uint64_t hash_slot_window(ldsw_t w, uint32_t code, uint32_t off, uint32_t n, bool& bad) {
     if constexpr (TNUM) {
         if (code == CODE_ZERO) return 0;

@@ -185,7 +185,7 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
 // regime from the same two reads; lw then points kFrontHT bytes before the
 // window); HT 2 / 3: hash_slot_window's LOOP 2 / 3; HT 5: LOOP 2 with TNUM.
 constexpr uint32_t kFrontHT = 32;
-template <int SHAPE, int HT = 0, bool W128 = false>
+template <int SHAPE, int HT = 0, int W128 = 0>
 __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, bool staged, uint64_t mybase,
                                               uint32_t s, uint32_t cd, uint64_t d, bool& bad) {
     const uint32_t doff = (uint32_t)d, dn = (uint32_t)(d >> 32);
@@ -207,7 +207,7 @@ __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, 
 // (lookup_tables_wave), coordinates stored only when args.coords is set.
 // GAP: the class straddling the pass boundary moves whole into the second
 // pass when pads allow (class_sort, hdx_regroup.h).
-template <int NCH, uint32_t WB, int SHAPE = 0, int HT = 0, int ORDER = 1, bool W128 = false, bool REGIONS = false,
+template <int NCH, uint32_t WB, int SHAPE = 0, int HT = 0, int ORDER = 1, int W128 = 0, bool REGIONS = false,
           bool GAP = false, bool ADMA = false, bool PU = true>
 __global__ void __launch_bounds__(256)
 hash_wstage_kernel(const BatchArgs args) {
@@ -259,7 +259,7 @@ hash_wstage_kernel(const BatchArgs args) {
 
 // Launch: K = floor(64 * NCH / A) whole objects per wave (at most 63), four
 // independent waves per 256-thread workgroup, no workgroup barrier.
-template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, int HT = 0, int ORDER = 1, bool W128 = false,
+template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, int HT = 0, int ORDER = 1, int W128 = 0,
           bool REGIONS = false, bool GAP = false, bool ADMA = false, bool PU = true>
 static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     // lane o holds object o's base and lane K the next group's first: K <= 63

@@ -137,7 +137,7 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
 // SHAPE (debug forms 7 / 8, WRONG coordinates): 1 = no hash (a slot's
 // coordinate is its descriptor), 2 = no hash and no walk.
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
-          bool ASM = false, bool PU = true, bool BF = false>
+          bool ASM = false, bool PU = true, bool BF = false, bool RECS = true>
 __global__ void __launch_bounds__(256)
 hash_sweep_wstage_kernel(const EncodedArgs a) {
     constexpr uint32_t SL = NCH * 64;
@@ -172,52 +172,77 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
     if ((uint32_t)lane * 4 < A && (uint32_t)lane * 4 < SL)
         reinterpret_cast<uint32_t*>(codes)[lane] = reinterpret_cast<const uint32_t*>(a.codes)[lane];
 
-    // ---- the keys, then the value span (whatever of it fits) ----------------
-    // Keys stored back to back (a store's usual layout) are one span, copied
-    // by 16-byte LDS DMA; otherwise they are gathered dword by dword (a store
-    // keeps each key in its own place).
+    // ---- records [key][value] back to back: one span ------------------------
+    // A store whose entries keep each key right before its value (a LevelDB
+    // block's adjacency; synth.make_encoded_device(layout="records")) is one
+    // contiguous run of bytes per group: copied by one span DMA, keys and
+    // values then both read from it.
+    const uint64_t ka = (uint64_t)(uintptr_t)(a.keys + koff), va = (uint64_t)(uintptr_t)(a.vals + voff);
+    const uint64_t ka_next = sh64(ka, (lane + 1) & 63);
+    const bool recs = RECS && __all((uint32_t)lane >= nobj ||
+                                    (va == ka + klen && ((uint32_t)lane + 1 >= nobj || ka_next == va + vlen)));
+    uint64_t rend = 0;
+    bool rspan = false;
+    if (recs) {
+        rend = rl64(va + vlen, (int)nobj - 1);
+        rspan = rend - rl64(ka, 0) + (rl64(ka, 0) & 15) <= WB;
+    }
+
+    // ---- else the keys, then the value span (whatever of it fits) -----------
+    // Keys stored back to back (a key column) are one span, copied by 16-byte
+    // LDS DMA; otherwise they are gathered dword by dword (a store keeps each
+    // key in its own place).
     const uint64_t knext = sh64(koff, (lane + 1) & 63);
-    const bool kruns = __all((uint32_t)lane + 1 >= nobj || koff + klen == knext);
+    const bool kruns = rspan || __all((uint32_t)lane + 1 >= nobj || koff + klen == knext);
     const uint64_t k0 = rl64(koff, 0);
     const uint32_t klead = (uint32_t)((uintptr_t)(a.keys + k0) & 15);
     uint32_t kdx = 0, kreg = 0;  // kdx: lane o's first dword in the gathered key region
-    bool keys_in, kspan = false;
-    if (kruns) {
-        const uint64_t kend = rl64(koff + klen, (int)nobj - 1);
-        kspan = kend - k0 + klead <= WB / 4;
-        keys_in = kspan;
-        if (kspan) {
-            kreg = (klead + (uint32_t)(kend - k0) + 15) & ~15u;
-            copy_span<ASM>(a.keys + k0 - klead, win + kFrontS, klead + (uint32_t)(kend - k0), lane);
-        }
-    }
-    if (!kspan) {
-        // lane o < nobj: its key's dwords [kd, kd + kdw) from the key's dword floor
-        const uint64_t kd = (uint64_t)(uintptr_t)(a.keys + koff) >> 2;
-        const uint32_t kdw = (uint32_t)lane < nobj ? ((uint32_t)((uintptr_t)(a.keys + koff) & 3) + klen + 3) >> 2 : 0u;
-        kdx = wave_scan_dpp(kdw) - kdw;
-        const uint32_t td = __builtin_amdgcn_readlane(kdx + kdw, 63);
-        keys_in = 4 * td <= WB / 4;
-        kreg = keys_in ? (4 * td + 15) & ~15u : 0u;  // the values' region starts 16-byte aligned
-        if (keys_in) {
-            for (uint32_t u0 = 0; u0 < td; u0 += 64) {
-                const uint32_t u = u0 + (uint32_t)lane;
-                // the object whose key holds region dword u (a wave-uniform walk over <= 63 objects)
-                uint64_t src = 0;
-                for (uint32_t o = 0; o < nobj; ++o) {
-                    const uint32_t x0 = __builtin_amdgcn_readlane(kdx, (int)o), xn = __builtin_amdgcn_readlane(kdw, (int)o);
-                    if (u >= x0 && u < x0 + xn) src = 4 * (rl64(kd, (int)o) + (u - x0));
-                }
-                if (u < td)
-                    dma4<ASM>((const void*)(uintptr_t)src, win + kFrontS + 4 * u0);
+    bool keys_in = false, kspan = false;
+    const uint64_t v0 = rl64(voff, 0);
+    uint32_t vlead = (uint32_t)((uintptr_t)(a.vals + v0) & 15), vheld = 0;
+    if (rspan) {
+        const uint64_t ka0 = rl64(ka, 0);
+        kspan = keys_in = true;  // kreg 0: the values lie in the same span
+        vlead = klead + (uint32_t)(rl64(va, 0) - ka0);
+        vheld = klead + (uint32_t)(rend - ka0);
+        copy_span<ASM>(a.keys + k0 - klead, win + kFrontS, vheld, lane);
+    } else {
+        if (kruns) {
+            const uint64_t kend = rl64(koff + klen, (int)nobj - 1);
+            kspan = kend - k0 + klead <= WB / 4;
+            keys_in = kspan;
+            if (kspan) {
+                kreg = (klead + (uint32_t)(kend - k0) + 15) & ~15u;
+                copy_span<ASM>(a.keys + k0 - klead, win + kFrontS, klead + (uint32_t)(kend - k0), lane);
             }
         }
+        if (!kspan) {
+            // lane o < nobj: its key's dwords [kd, kd + kdw) from the key's dword floor
+            const uint64_t kd = (uint64_t)(uintptr_t)(a.keys + koff) >> 2;
+            const uint32_t kdw =
+                (uint32_t)lane < nobj ? ((uint32_t)((uintptr_t)(a.keys + koff) & 3) + klen + 3) >> 2 : 0u;
+            kdx = wave_scan_dpp(kdw) - kdw;
+            const uint32_t td = __builtin_amdgcn_readlane(kdx + kdw, 63);
+            keys_in = 4 * td <= WB / 4;
+            kreg = keys_in ? (4 * td + 15) & ~15u : 0u;  // the values' region starts 16-byte aligned
+            if (keys_in) {
+                for (uint32_t u0 = 0; u0 < td; u0 += 64) {
+                    const uint32_t u = u0 + (uint32_t)lane;
+                    // the object whose key holds region dword u (a wave-uniform walk over <= 63 objects)
+                    uint64_t src = 0;
+                    for (uint32_t o = 0; o < nobj; ++o) {
+                        const uint32_t x0 = __builtin_amdgcn_readlane(kdx, (int)o),
+                                       xn = __builtin_amdgcn_readlane(kdw, (int)o);
+                        if (u >= x0 && u < x0 + xn) src = 4 * (rl64(kd, (int)o) + (u - x0));
+                    }
+                    if (u < td) dma4<ASM>((const void*)(uintptr_t)src, win + kFrontS + 4 * u0);
+                }
+            }
+        }
+        const uint64_t vend = has_next ? rl64(voff, (int)nobj) : 0;
+        vheld = has_next && vend >= v0 ? (uint32_t)std::min<uint64_t>(vlead + (vend - v0), WB - kreg) : 0u;
+        if (vheld) copy_span<ASM>(a.vals + v0 - vlead, win + kFrontS + kreg, vheld, lane);
     }
-    const uint64_t v0 = rl64(voff, 0);
-    const uint64_t vend = has_next ? rl64(voff, (int)nobj) : 0;
-    const uint32_t vlead = (uint32_t)((uintptr_t)(a.vals + v0) & 15);
-    const uint32_t vheld = has_next && vend >= v0 ? (uint32_t)std::min<uint64_t>(vlead + (vend - v0), WB - kreg) : 0u;
-    if (vheld) copy_span<ASM>(a.vals + v0 - vlead, win + kFrontS + kreg, vheld, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the compiler does not order ds_read after LDS DMA
     wave_fence();
 
@@ -357,14 +382,14 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
 }
 
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
-          bool ASM = false, bool PU = true, bool BF = false>
+          bool ASM = false, bool PU = true, bool BF = false, bool RECS = true>
 static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
     const uint32_t K = std::min<uint32_t>(64 * NCH / a.A, KCAP);
     if (K == 0) return hipErrorInvalidValue;
     const uint64_t waves = (a.n + K - 1) / K;
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU, BF>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU, BF, RECS>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -404,6 +429,7 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 14: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false, false, true>(a, stream);  // pass loop not unrolled
         case 15: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, false>(a, stream);  // the branchy class, guarded loads
         case 16: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false, true, true>(a, stream);  // without TNUM
+        case 17: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false>(a, stream);  // without the record span
         default: return hipErrorInvalidValue;
     }
 }

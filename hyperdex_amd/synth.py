@@ -226,25 +226,63 @@ def encode_values_host(types, blob, obj_base, attr_len, first_version=0):
     return blob, key_off, key_len, vals, val_off, val_len
 
 
-def make_encoded_device(name_or_rules, n: int, seed: int = SEED, first: int = 0, device=None):
+def encode_records_host(types, blob, obj_base, attr_len, first_version=0):
+    """encode_values_host's objects as one store of records [key][value]
+    (make_encoded_device's "records" layout): returns (store, key_off,
+    key_len, store, val_off, val_len)."""
+    _, _, key_len, vals, val_off, val_len = encode_values_host(types, blob, obj_base, attr_len, first_version)
+    n = len(obj_base)
+    rec = key_len.astype(np.uint64) + val_len.astype(np.uint64)
+    rec_off = np.zeros(n, np.uint64)
+    if n > 1:
+        rec_off[1:] = np.cumsum(rec[:-1])
+    store = np.zeros(int(rec.sum()) if n else 0, np.uint8)
+    for i in range(n):
+        r, k, v = int(rec_off[i]), int(key_len[i]), int(val_len[i])
+        store[r:r + k] = blob[int(obj_base[i]):int(obj_base[i]) + k]
+        store[r + k:r + k + v] = vals[int(val_off[i]):int(val_off[i]) + v]
+    return store, rec_off, key_len, store, rec_off + key_len.astype(np.uint64), val_len
+
+
+def make_encoded_device(name_or_rules, n: int, seed: int = SEED, first: int = 0, device=None,
+                        layout: str = "columns"):
     """A packed synthetic batch re-encoded as stored objects in HBM (config 5):
-    returns (types, keys, key_off, key_len, vals, val_off, val_len) with
-    keys = the batch blob (key_off = obj_base), values in a new buffer."""
+    returns (types, keys, key_off, key_len, vals, val_off, val_len).
+    layout "columns": keys = the batch blob (key_off = obj_base: each key in
+    place inside its packed object), values in a new buffer, back to back.
+    layout "records": one store of records [key][value] back to back (the
+    adjacency of a LevelDB block's key / value entries); keys and vals are
+    the same tensor and the batch blob is freed."""
     import torch
 
     from ._lib import check, lib
 
+    assert layout in ("columns", "records")
     types, blob, obj_base, attr_len = make_batch_device(name_or_rules, n, seed, first, device)
     A = len(types)
     L = attr_len.view(n, A).to(torch.int64)
     key_len = attr_len.view(n, A)[:, 0].contiguous()
     val_len64 = 10 + (4 + L[:, 1:]).sum(dim=1)
+    stream = torch.cuda.current_stream(blob.device).cuda_stream
+    if layout == "records":
+        rec = val_len64 + L[:, 0]
+        rec_off = torch.zeros(n, dtype=torch.int64, device=blob.device)
+        if n > 1:
+            rec_off[1:] = torch.cumsum(rec[:-1], dim=0)
+        total = int(rec.sum().item()) if n else 0
+        del rec, L
+        val_off = rec_off + key_len.to(torch.int64)
+        store = torch.empty(max(total, 1), dtype=torch.uint8, device=blob.device)
+        check(lib().hdx_synth_encode_records(blob.data_ptr(), obj_base.data_ptr(), attr_len.data_ptr(), A, n,
+                                             first, val_off.data_ptr(), store.data_ptr(), stream))
+        torch.cuda.current_stream(blob.device).synchronize()
+        del blob, obj_base, attr_len
+        return (types, store, rec_off, key_len, store, val_off, val_len64.to(torch.int32))
     val_off = torch.zeros(n, dtype=torch.int64, device=blob.device)
     if n > 1:
         val_off[1:] = torch.cumsum(val_len64[:-1], dim=0)
     total = int(val_len64.sum().item()) if n else 0
     vals = torch.empty(max(total, 1), dtype=torch.uint8, device=blob.device)
-    stream = torch.cuda.current_stream(blob.device).cuda_stream
     check(lib().hdx_synth_encode_values(blob.data_ptr(), obj_base.data_ptr(), attr_len.data_ptr(), A, n,
                                         first, val_off.data_ptr(), vals.data_ptr(), stream))
     return (types, blob, obj_base, key_len, vals, val_off, val_len64.to(torch.int32))

@@ -347,18 +347,19 @@ hdx_status hdx_search_space(const hdx_region_table* tables, uint32_t ntables, co
 
 /* key_state::hash_objects (daemon/key_state.cc:1455-1543) hashes one or two
  * objects per replicated op, from every daemon::loop thread at once.  A
- * batcher keeps that synchronous per-object call.  An object of at most
- * host_max_bytes payload is hashed on the calling thread by the per-object
- * CPU path (hdx_hash_object) and looked up in the batcher's tables on the
- * host (configuration::lookup_region's scan) — one core hashes a config-3b
- * object in ~0.15 us, while a device round trip costs ~36 us, so no batch
- * of synchronous callers can beat the calling threads' own cores.  Larger
- * objects (or every object, with HDX_BATCHER_DEVICE_ONLY, for hosts whose
- * cores are needed elsewhere) are coalesced into device batches: each caller
- * copies its object into a pinned staging buffer and blocks; a flush thread
- * ships a batch as soon as the previous one has completed, when it is full,
- * or `max_delay_us` after its first object, runs the hash kernel (and the
- * region lookups of the batcher's tables) and wakes the callers.
+ * batcher keeps that synchronous per-object call.  By default every object is
+ * hashed on the calling thread by the per-object CPU path (hdx_hash_object)
+ * and looked up in the batcher's tables on the host (configuration::
+ * lookup_region's scan): a core hashes a config-3b object in ~0.15 us, a
+ * device round trip costs ~36 us, and CityHash is serial within a string, so
+ * no device batch of synchronous callers beats their own cores at any object
+ * size.  Objects above host_max_bytes, or every object with
+ * HDX_BATCHER_DEVICE_ONLY (hosts whose cores are needed elsewhere: the
+ * callers sleep while the device works), are coalesced into device batches:
+ * each caller copies its object into a pinned staging buffer and blocks; a
+ * flush thread ships a batch as soon as the previous one has completed, when
+ * it is full, or `max_delay_us` after its first object, runs the hash kernel
+ * (and the region lookups of the batcher's tables) and wakes the callers.
  * One batcher per space (schema). */
 typedef struct hdx_batcher_s* hdx_batcher;
 typedef struct hdx_batcher_config {
@@ -371,7 +372,7 @@ typedef struct hdx_batcher_config {
     uint32_t ntables;        /* <= 16 */
     uint32_t flags;          /* HDX_BATCHER_* */
     uint64_t host_max_bytes; /* objects of at most this many payload bytes are hashed on the
-                                calling thread; 0 = HDX_BATCHER_HOST_MAX_BYTES */
+                                calling thread; 0 = every object */
 } hdx_batcher_config;
 /* Stage batches through device memory (H2D, kernels, D2H) instead of letting
  * the kernels read and write the pinned staging buffers in place (default,
@@ -380,9 +381,6 @@ typedef struct hdx_batcher_config {
 /* Every object goes to the device, whatever its size (the calling threads'
  * cores stay free for the rest of the daemon). */
 #define HDX_BATCHER_DEVICE_ONLY 2u
-/* The default host_max_bytes: the object size above which one device round
- * trip (~36 us + PCIe) undercuts one core's hash (~7 GB/s), DESIGN.md §4.7. */
-#define HDX_BATCHER_HOST_MAX_BYTES (256u * 1024u)
 typedef struct hdx_batcher_stats {
     uint64_t objects;        /* objects hashed */
     uint64_t batches;        /* device batches shipped */
@@ -441,6 +439,15 @@ hdx_status hdx_synth_encode_values(const uint8_t* blob_dev, const uint64_t* obj_
                                    const uint32_t* attr_len_dev, uint32_t attrs_sz, uint64_t n,
                                    uint64_t first_version, const uint64_t* val_off_dev,
                                    uint8_t* vals_dev, hdx_stream stream);
+
+/* The same, as records [key][value] in one store (the adjacency of a LevelDB
+ * block's entries): key i (attribute 0 of object i) is written at
+ * store_dev + val_off_dev[i] - attr_len[i*A], its encoded value at
+ * store_dev + val_off_dev[i]. */
+hdx_status hdx_synth_encode_records(const uint8_t* blob_dev, const uint64_t* obj_base_dev,
+                                    const uint32_t* attr_len_dev, uint32_t attrs_sz, uint64_t n,
+                                    uint64_t first_version, const uint64_t* val_off_dev,
+                                    uint8_t* store_dev, hdx_stream stream);
 
 #ifdef __cplusplus
 }

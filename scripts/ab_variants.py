@@ -35,10 +35,11 @@ def main():
     lib = ctx.__enter__()
     dev = torch.device("cuda", 0)
     variants = [int(v) for v in args.variants.split(",")]
-    checked = set(int(v) for v in args.check.split(",")) if args.check else set(variants) - {40, 41, 57, 58, 207, 208, 218, 241, 223, 224, 225, 226, 227, 237, 238}
+    checked = set(int(v) for v in args.check.split(",")) if args.check else set(variants) - {40, 41, 57, 58, 207, 208, 218, 241, 223, 224, 225, 226, 227, 237, 238, 248, 249}
     for cfg in args.configs.split(","):
-        if cfg == "cfg5":  # stored-object sweep (variants 30-32)
-            types, *enc = synth.make_encoded_device("cfg3b", args.objects, device=dev)
+        if cfg in ("cfg5", "cfg5r"):  # stored-object sweep; cfg5r: the records layout
+            types, *enc = synth.make_encoded_device("cfg3b", args.objects, device=dev,
+                                                    layout="records" if cfg == "cfg5r" else "columns")
             blob = enc[0][:int(enc[2].to(torch.int64).sum().item())]  # key bytes ...
             extra = int(enc[5].to(torch.int64).sum().item())            # ... + value bytes
 

@@ -15,6 +15,7 @@
 #                      summarised by pmc_summary.py; SET "lds" = the LDS / VALU / wait set
 #   profile            scripts/profile_r2.sh TAG (round evidence: traces + PMC traffic)
 #   py=SCRIPT[,ARGS]   python SCRIPT ARGS (commas for spaces)
+#   sh=SCRIPT[,ARGS]   bash SCRIPT ARGS (commas for spaces)
 set -o pipefail
 TAG=${1:?tag}; shift
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -59,6 +60,8 @@ for STEP in "$@"; do
       timeout -k 10 1100 bash scripts/profile_r2.sh "$TAG" > "$log" 2>&1 ;;
     py)
       timeout -k 10 900 python -u ${arg//,/ } > "$log" 2> "$log.err" ;;
+    sh)
+      timeout -k 10 900 bash ${arg//,/ } > "$log" 2> "$log.err" ;;
     *)
       echo "unknown step $STEP"; exit 2 ;;
   esac

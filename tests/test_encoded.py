@@ -351,3 +351,79 @@ def test_gpu_encoded_regions_by_lookup(oracle, case, with_coords):
     assert int(status.item()) == 0
     for t in tables:
         t.close()
+
+
+# ---- records [key][value] back to back (a LevelDB block's adjacency) ----------
+
+def test_oracle_records_layout(oracle):
+    """encode_records_host: the same objects as one store of records decode
+    and hash to the packed batch's coordinates."""
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 200, seed=51)
+    rec = synth.encode_records_host(types, blob, base, lens, first_version=5)
+    coords, versions, bad = oracle.hash_encoded(types, *rec)
+    want, _ = oracle.hash_batch(types, blob, base, lens)
+    assert not bad.any() and np.array_equal(coords, want)
+    assert np.array_equal(versions, 5 + np.arange(200, dtype=np.uint64))
+
+
+def _records_with_gaps(rec, rng):
+    """Move a few records apart (gaps in the store): the groups holding them
+    are no longer one run and take the key / value paths instead."""
+    store, key_off, key_len, _, val_off, val_len = [np.array(x) for x in rec]
+    n = len(key_off)
+    shift = np.zeros(n, np.uint64)
+    for i in sorted(rng.choice(n, max(1, n // 50), replace=False)):
+        shift[i:] += np.uint64(int(rng.integers(1, 40)))
+    out = np.zeros(len(store) + int(shift[-1]) + 64, np.uint8)
+    for i in range(n):
+        r, k, v = int(key_off[i]), int(key_len[i]), int(val_len[i])
+        out[r + int(shift[i]):r + int(shift[i]) + k + v] = store[r:r + k + v]
+    return out, key_off + shift, key_len, out, val_off + shift, val_len
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [-1, 250])
+@pytest.mark.parametrize("case", ["packed", "gaps", "corrupt"])
+def test_gpu_encoded_records(oracle, case, variant):
+    """The sweep on the records layout: a group whose records are back to back
+    is one span (keys and values read from it); gaps between records and
+    corrupt values keep the reference's results; 250 = the product without the
+    record span (round 3's key / value paths) on the same store."""
+    import contextlib
+
+    import torch
+
+    import hyperdex_amd as hdx
+    dev = torch.device("cuda", 0)
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 3001, seed=52)
+    rec = synth.encode_records_host(types, blob, base, lens, first_version=11)
+    rng = np.random.default_rng(53)
+    if case == "gaps":
+        rec = _records_with_gaps(rec, rng)
+    elif case == "corrupt":
+        enc, _ = _corrupt(rec, rng)
+        rec = (enc[3],) + enc[1:3] + (enc[3],) + enc[4:]  # the corrupted store is both keys and values
+    want, wver, _ = oracle.hash_encoded(types, *rec)
+    d = _to_dev(torch, dev, rec)
+    d[3] = d[0]  # one store on the device too
+    versions = torch.zeros(len(rec[1]), dtype=torch.int64, device=dev)
+    with _lib.debug_library(variant) if variant >= 0 else contextlib.nullcontext():
+        got = hdx.hash_encoded(types, *d, versions=versions)
+        torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().view(np.uint64), want)
+    assert np.array_equal(versions.cpu().numpy().view(np.uint64), wver)
+
+
+@pytest.mark.gpu
+def test_gpu_encoded_records_device_generator(oracle):
+    """make_encoded_device(layout="records") writes exactly the host encoding."""
+    import torch
+    dev = torch.device("cuda", 0)
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 1500, seed=54, first=777)
+    want = synth.encode_records_host(types, blob, base, lens, first_version=777)
+    got = synth.make_encoded_device("cfg3b", 1500, seed=54, first=777, device=dev, layout="records")
+    assert np.array_equal(got[1].cpu().numpy()[:len(want[0])], want[0])
+    for g, w in zip(got[2:4], want[1:3]):
+        assert np.array_equal(g.cpu().numpy().view(w.dtype), w)
+    assert np.array_equal(got[5].cpu().numpy().view(np.uint64), want[4])
+    assert np.array_equal(got[6].cpu().numpy().view(np.uint32), want[5])

@@ -54,16 +54,19 @@ def torch_dev():
     return torch, torch.device("cuda", 0)
 
 
-def test_cfg5_sweep_at_50M(oracle, torch_dev):
+@pytest.mark.parametrize("layout", ["columns", "records"])
+def test_cfg5_sweep_at_50M(oracle, torch_dev, layout):
     """Config 5 at BASELINE size: 50 M stored objects, values far past 4 GiB
     of offsets; coordinates, versions and the status word sampled against
     the oracle, two launches identical, and the regions entry point with no
     coordinates (its 1 GiB scratch chunks) equal to lookups on the sweep's
-    own coordinates."""
+    own coordinates.  Both store layouts: keys in place in their packed
+    objects beside a value column, and records [key][value] in one store."""
     from hyperdex_amd import RegionTable
     torch, dev = torch_dev
     n = 50_000_000
-    types, keys, key_off, key_len, vals, val_off, val_len = synth.make_encoded_device("cfg3b", n, device=dev)
+    types, keys, key_off, key_len, vals, val_off, val_len = synth.make_encoded_device("cfg3b", n, device=dev,
+                                                                                      layout=layout)
     A = len(types)
     assert vals.numel() > 12 * (4 * GiB)  # ~58 GB: offsets well past 2^32
     versions = torch.zeros(n, dtype=torch.int64, device=dev)
