@@ -63,10 +63,10 @@ def parse_args(argv=None):
     ap.add_argument("--config", default="cfg3a")
     ap.add_argument("--objects", type=int, default=0,
                     help="objects per GPU (default 10M; 50M for cfg5, BASELINE config 5)")
-    ap.add_argument("--store-layout", default="columns", choices=("columns", "records"),
+    ap.add_argument("--store-layout", default="columns", choices=("columns", "keycol", "records"),
                     help="cfg5's stored objects: 'columns' (each key in place in its packed object, values "
-                         "back to back: round 3's layout) or 'records' ([key][value] back to back, a "
-                         "LevelDB block's adjacency)")
+                         "back to back: round 3's layout), 'keycol' (a key column and a value column, "
+                         "SURVEY §8d) or 'records' ([key][value] back to back, a LevelDB block's adjacency)")
     ap.add_argument("--config4-objects", type=int, default=100_000_000,
                     help="config 4: objects of the whole sharded batch (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -280,7 +280,7 @@ def run_rank(args):
         result["roofline"]["frac_of_probe"] = round(
             achieved / sp.get("read_write_mix_GBps", sp["read_write_1to8_GBps"]), 4)
     if cfg == "cfg5":
-        result["roofline"]["kernel"] = "void hdx::hash_sweep_wstage_kernel<2, 8704u, 6u, false, true, 0, 13, false, true, true>(hdx::EncodedArgs)"
+        result["roofline"]["kernel"] = "void hdx::hash_sweep_wstage_kernel<2, 8704u, 6u, false, true, 0, 13, false, true, true, true>(hdx::EncodedArgs)"
     if world > 1 and not args.no_allgather:
         result["allgather"] = time_allgather(coords, world, dev, backend, max_over_ranks)
         # hash phase then the coordinate exchange, back to back

@@ -66,7 +66,7 @@ SIGNATURES = [
     ("hdx_hash_encoded_device", _i32, [_vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _u64, _vp, _vp,
                                        _vp, _vp]),
     ("hdx_synth_encode_values", _i32, [_vp, _vp, _vp, _u32, _u64, _u64, _vp, _vp, _vp]),
-    ("hdx_synth_encode_records", _i32, [_vp, _vp, _vp, _u32, _u64, _u64, _vp, _vp, _vp]),
+    ("hdx_synth_encode_store", _i32, [_vp, _vp, _vp, _u32, _u64, _u64, _vp, _vp, _vp, _vp, _vp]),
     ("hdx_hash_batch_host", _i32, [_vp, _u32, _vp, _u64, _vp, _vp, _u64, _vp]),
     ("hdx_hash_value", _i32, [_u32, _vp, _sz, _vp]),
     ("hdx_hash_key", _i32, [_vp, _u32, _vp, _sz, _vp]),

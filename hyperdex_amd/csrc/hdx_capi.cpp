@@ -599,15 +599,16 @@ HDX_EXPORT hdx_status hdx_synth_encode_values(const uint8_t* blob_dev, const uin
     return HDX_OK;
 }
 
-HDX_EXPORT hdx_status hdx_synth_encode_records(const uint8_t* blob_dev, const uint64_t* obj_base_dev,
-                                               const uint32_t* attr_len_dev, uint32_t attrs_sz, uint64_t n,
-                                               uint64_t first_version, const uint64_t* val_off_dev,
-                                               uint8_t* store_dev, hdx_stream stream) {
+HDX_EXPORT hdx_status hdx_synth_encode_store(const uint8_t* blob_dev, const uint64_t* obj_base_dev,
+                                             const uint32_t* attr_len_dev, uint32_t attrs_sz, uint64_t n,
+                                             uint64_t first_version, const uint64_t* val_off_dev, uint8_t* vals_dev,
+                                             const uint64_t* key_off_dev, uint8_t* keys_dev, hdx_stream stream) {
     if (attrs_sz == 0 || attrs_sz > 65535) return fail(HDX_E_INVALID, "attrs_sz=%u", attrs_sz);
+    if (n && (!key_off_dev || !keys_dev)) return fail(HDX_E_INVALID, "NULL key column");
     hdx_status st = bind_device(-1);
     if (st != HDX_OK) return st;
     HIP_TRY(launch_synth_encode(blob_dev, obj_base_dev, attr_len_dev, attrs_sz, n, first_version, val_off_dev,
-                                store_dev, (hipStream_t)stream, true));
+                                vals_dev, (hipStream_t)stream, key_off_dev, keys_dev));
     return HDX_OK;
 }
 

@@ -234,9 +234,10 @@ hipError_t launch_synth_lengths(const SynthArgs& a, uint32_t* attr_len, hipStrea
 hipError_t launch_synth_fill(const SynthArgs& a, const uint64_t* obj_base, const uint32_t* attr_len,
                              uint8_t* blob, uint64_t bytes, hipStream_t s);
 
-// records: each key is also written right before its value ([key][value])
+// keys (may be NULL): each key is also copied to keys + key_off[i]
 hipError_t launch_synth_encode(const uint8_t* blob, const uint64_t* obj_base, const uint32_t* attr_len,
                                uint32_t A, uint64_t n, uint64_t first_version, const uint64_t* val_off,
-                               uint8_t* vals, hipStream_t s, bool records = false);
+                               uint8_t* vals, hipStream_t s, const uint64_t* key_off = nullptr,
+                               uint8_t* keys = nullptr);
 
 }  // namespace hdx

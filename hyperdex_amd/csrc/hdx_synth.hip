@@ -97,18 +97,19 @@ __global__ void synth_numeric_kernel(const SynthArgs a, const uint64_t* obj_base
 
 // daemon/datalayer_encodings.cc:139-166 (encode_value) for object i of a
 // packed batch: attributes 1..A-1 become the value (attribute 0 is the key).
-// records: the key is written right before its value (a record [key][value],
-// the adjacency of a LevelDB block's entries)
+// keys (may be NULL): key i (attribute 0) is also copied to keys + key_off[i]
+// (a key column, or records [key][value] when keys == vals)
 __global__ void synth_encode_kernel(const uint8_t* blob, const uint64_t* obj_base, const uint32_t* attr_len,
                                     uint32_t A, uint64_t n, uint64_t first_version, const uint64_t* val_off,
-                                    uint8_t* vals, bool records) {
+                                    uint8_t* vals, const uint64_t* key_off, uint8_t* keys) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint8_t* o = vals + val_off[i];
-    if (records) {
+    if (keys) {
         const uint32_t kl = attr_len[i * A];
         const uint8_t* k = blob + obj_base[i];
-        for (uint32_t b = 0; b < kl; ++b) o[(int64_t)b - (int64_t)kl] = k[b];
+        uint8_t* kd = keys + key_off[i];
+        for (uint32_t b = 0; b < kl; ++b) kd[b] = k[b];
     }
     const uint64_t ver = first_version + i;
     for (int b = 0; b < 8; ++b) o[b] = (uint8_t)(ver >> (56 - 8 * b));
@@ -137,10 +138,10 @@ __global__ void synth_encode_kernel(const uint8_t* blob, const uint64_t* obj_bas
 
 hipError_t launch_synth_encode(const uint8_t* blob, const uint64_t* obj_base, const uint32_t* attr_len,
                                uint32_t A, uint64_t n, uint64_t first_version, const uint64_t* val_off,
-                               uint8_t* vals, hipStream_t s, bool records) {
+                               uint8_t* vals, hipStream_t s, const uint64_t* key_off, uint8_t* keys) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(synth_encode_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, s, blob, obj_base,
-                       attr_len, A, n, first_version, val_off, vals, records);
+                       attr_len, A, n, first_version, val_off, vals, key_off, keys);
     return hipGetLastError();
 }
 

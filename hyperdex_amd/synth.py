@@ -226,63 +226,89 @@ def encode_values_host(types, blob, obj_base, attr_len, first_version=0):
     return blob, key_off, key_len, vals, val_off, val_len
 
 
-def encode_records_host(types, blob, obj_base, attr_len, first_version=0):
-    """encode_values_host's objects as one store of records [key][value]
-    (make_encoded_device's "records" layout): returns (store, key_off,
-    key_len, store, val_off, val_len)."""
+def encode_store_host(types, blob, obj_base, attr_len, first_version=0, layout="records"):
+    """encode_values_host's objects in make_encoded_device's "keycol" or
+    "records" layout: returns (keys, key_off, key_len, vals, val_off, val_len)."""
     _, _, key_len, vals, val_off, val_len = encode_values_host(types, blob, obj_base, attr_len, first_version)
     n = len(obj_base)
-    rec = key_len.astype(np.uint64) + val_len.astype(np.uint64)
-    rec_off = np.zeros(n, np.uint64)
-    if n > 1:
-        rec_off[1:] = np.cumsum(rec[:-1])
+    kl = key_len.astype(np.uint64)
+
+    def exclusive_cumsum(x):
+        out = np.zeros(n, np.uint64)
+        if n > 1:
+            out[1:] = np.cumsum(x[:-1])
+        return out
+    if layout == "keycol":
+        key_off = exclusive_cumsum(kl)
+        keys = np.zeros(int(kl.sum()) if n else 0, np.uint8)
+        for i in range(n):
+            keys[int(key_off[i]):int(key_off[i] + kl[i])] = blob[int(obj_base[i]):int(obj_base[i] + kl[i])]
+        return keys, key_off, key_len, vals, val_off, val_len
+    assert layout == "records"
+    rec = kl + val_len.astype(np.uint64)
+    rec_off = exclusive_cumsum(rec)
     store = np.zeros(int(rec.sum()) if n else 0, np.uint8)
     for i in range(n):
-        r, k, v = int(rec_off[i]), int(key_len[i]), int(val_len[i])
+        r, k, v = int(rec_off[i]), int(kl[i]), int(val_len[i])
         store[r:r + k] = blob[int(obj_base[i]):int(obj_base[i]) + k]
         store[r + k:r + k + v] = vals[int(val_off[i]):int(val_off[i]) + v]
-    return store, rec_off, key_len, store, rec_off + key_len.astype(np.uint64), val_len
+    return store, rec_off, key_len, store, rec_off + kl, val_len
 
 
 def make_encoded_device(name_or_rules, n: int, seed: int = SEED, first: int = 0, device=None,
                         layout: str = "columns"):
     """A packed synthetic batch re-encoded as stored objects in HBM (config 5):
     returns (types, keys, key_off, key_len, vals, val_off, val_len).
-    layout "columns": keys = the batch blob (key_off = obj_base: each key in
-    place inside its packed object), values in a new buffer, back to back.
-    layout "records": one store of records [key][value] back to back (the
-    adjacency of a LevelDB block's key / value entries); keys and vals are
-    the same tensor and the batch blob is freed."""
+      "columns": keys = the batch blob (key_off = obj_base: each key in place
+                 inside its packed object), values back to back in a new
+                 buffer (round 3's layout);
+      "keycol":  keys back to back in a key column (key_off = their prefix
+                 offsets, SURVEY §8d's "key, obj_base[n+1]"), values back to
+                 back beside it;
+      "records": one store of records [key][value] back to back (the
+                 adjacency of a LevelDB block's key / value entries); keys
+                 and vals are the same tensor.
+    The last two free the batch blob."""
     import torch
 
     from ._lib import check, lib
 
-    assert layout in ("columns", "records")
+    assert layout in ("columns", "keycol", "records")
     types, blob, obj_base, attr_len = make_batch_device(name_or_rules, n, seed, first, device)
     A = len(types)
+    dev = blob.device
     L = attr_len.view(n, A).to(torch.int64)
     key_len = attr_len.view(n, A)[:, 0].contiguous()
     val_len64 = 10 + (4 + L[:, 1:]).sum(dim=1)
-    stream = torch.cuda.current_stream(blob.device).cuda_stream
-    if layout == "records":
-        rec = val_len64 + L[:, 0]
-        rec_off = torch.zeros(n, dtype=torch.int64, device=blob.device)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    def exclusive_cumsum(x):
+        out = torch.zeros(n, dtype=torch.int64, device=dev)
         if n > 1:
-            rec_off[1:] = torch.cumsum(rec[:-1], dim=0)
-        total = int(rec.sum().item()) if n else 0
-        del rec, L
-        val_off = rec_off + key_len.to(torch.int64)
-        store = torch.empty(max(total, 1), dtype=torch.uint8, device=blob.device)
-        check(lib().hdx_synth_encode_records(blob.data_ptr(), obj_base.data_ptr(), attr_len.data_ptr(), A, n,
-                                             first, val_off.data_ptr(), store.data_ptr(), stream))
-        torch.cuda.current_stream(blob.device).synchronize()
-        del blob, obj_base, attr_len
-        return (types, store, rec_off, key_len, store, val_off, val_len64.to(torch.int32))
-    val_off = torch.zeros(n, dtype=torch.int64, device=blob.device)
-    if n > 1:
-        val_off[1:] = torch.cumsum(val_len64[:-1], dim=0)
-    total = int(val_len64.sum().item()) if n else 0
-    vals = torch.empty(max(total, 1), dtype=torch.uint8, device=blob.device)
-    check(lib().hdx_synth_encode_values(blob.data_ptr(), obj_base.data_ptr(), attr_len.data_ptr(), A, n,
-                                        first, val_off.data_ptr(), vals.data_ptr(), stream))
-    return (types, blob, obj_base, key_len, vals, val_off, val_len64.to(torch.int32))
+            out[1:] = torch.cumsum(x[:-1], dim=0)
+        return out
+
+    if layout == "columns":
+        val_off = exclusive_cumsum(val_len64)
+        vals = torch.empty(max(int(val_len64.sum().item()) if n else 0, 1), dtype=torch.uint8, device=dev)
+        check(lib().hdx_synth_encode_values(blob.data_ptr(), obj_base.data_ptr(), attr_len.data_ptr(), A, n,
+                                            first, val_off.data_ptr(), vals.data_ptr(), stream))
+        return (types, blob, obj_base, key_len, vals, val_off, val_len64.to(torch.int32))
+    if layout == "records":
+        rec_off = exclusive_cumsum(val_len64 + L[:, 0])
+        val_off = rec_off + L[:, 0]
+        total = int((val_len64 + L[:, 0]).sum().item()) if n else 0
+        vals = keys = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+        key_off = rec_off
+    else:
+        key_off = exclusive_cumsum(L[:, 0])
+        val_off = exclusive_cumsum(val_len64)
+        keys = torch.empty(max(int(L[:, 0].sum().item()) if n else 0, 1), dtype=torch.uint8, device=dev)
+        vals = torch.empty(max(int(val_len64.sum().item()) if n else 0, 1), dtype=torch.uint8, device=dev)
+    del L
+    check(lib().hdx_synth_encode_store(blob.data_ptr(), obj_base.data_ptr(), attr_len.data_ptr(), A, n, first,
+                                       val_off.data_ptr(), vals.data_ptr(), key_off.data_ptr(), keys.data_ptr(),
+                                       stream))
+    torch.cuda.current_stream(dev).synchronize()
+    del blob, obj_base, attr_len
+    return (types, keys, key_off, key_len, vals, val_off, val_len64.to(torch.int32))

@@ -440,14 +440,14 @@ hdx_status hdx_synth_encode_values(const uint8_t* blob_dev, const uint64_t* obj_
                                    uint64_t first_version, const uint64_t* val_off_dev,
                                    uint8_t* vals_dev, hdx_stream stream);
 
-/* The same, as records [key][value] in one store (the adjacency of a LevelDB
- * block's entries): key i (attribute 0 of object i) is written at
- * store_dev + val_off_dev[i] - attr_len[i*A], its encoded value at
- * store_dev + val_off_dev[i]. */
-hdx_status hdx_synth_encode_records(const uint8_t* blob_dev, const uint64_t* obj_base_dev,
-                                    const uint32_t* attr_len_dev, uint32_t attrs_sz, uint64_t n,
-                                    uint64_t first_version, const uint64_t* val_off_dev,
-                                    uint8_t* store_dev, hdx_stream stream);
+/* The same, with every key (attribute 0 of object i) also copied to
+ * keys_dev + key_off_dev[i]: a key column beside the values, or — keys_dev ==
+ * vals_dev and key_off = val_off - key_len — records [key][value] in one
+ * store (the adjacency of a LevelDB block's entries). */
+hdx_status hdx_synth_encode_store(const uint8_t* blob_dev, const uint64_t* obj_base_dev,
+                                  const uint32_t* attr_len_dev, uint32_t attrs_sz, uint64_t n,
+                                  uint64_t first_version, const uint64_t* val_off_dev, uint8_t* vals_dev,
+                                  const uint64_t* key_off_dev, uint8_t* keys_dev, hdx_stream stream);
 
 #ifdef __cplusplus
 }

@@ -37,9 +37,9 @@ def main():
     variants = [int(v) for v in args.variants.split(",")]
     checked = set(int(v) for v in args.check.split(",")) if args.check else set(variants) - {40, 41, 57, 58, 207, 208, 218, 241, 223, 224, 225, 226, 227, 237, 238, 248, 249}
     for cfg in args.configs.split(","):
-        if cfg in ("cfg5", "cfg5r"):  # stored-object sweep; cfg5r: the records layout
+        if cfg in ("cfg5", "cfg5r", "cfg5k"):  # stored-object sweep; cfg5r / cfg5k: records / key column
             types, *enc = synth.make_encoded_device("cfg3b", args.objects, device=dev,
-                                                    layout="records" if cfg == "cfg5r" else "columns")
+                                                    layout={"cfg5r": "records", "cfg5k": "keycol"}.get(cfg, "columns"))
             blob = enc[0][:int(enc[2].to(torch.int64).sum().item())]  # key bytes ...
             extra = int(enc[5].to(torch.int64).sum().item())            # ... + value bytes
 

@@ -25,9 +25,9 @@ def main():
         ctx = _lib.debug_library(a.variant)  # a collected context manager restores the product lib)
         ctx.__enter__()
     dev = torch.device("cuda", 0)
-    if a.config in ("cfg5", "cfg5r"):  # stored-object sweep over config-3b objects (cfg5r: records layout)
+    if a.config in ("cfg5", "cfg5r", "cfg5k"):  # stored-object sweep over config-3b objects
         types, *enc = synth.make_encoded_device("cfg3b", a.objects, device=dev,
-                                                layout="records" if a.config == "cfg5r" else "columns")
+                                                layout={"cfg5r": "records", "cfg5k": "keycol"}.get(a.config, "columns"))
         coords = torch.empty((a.objects, len(types)), dtype=torch.int64, device=dev)
         for _ in range(a.launches):
             hdx.hash_encoded(types, *enc, coords=coords)

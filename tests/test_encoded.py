@@ -359,7 +359,7 @@ def test_oracle_records_layout(oracle):
     """encode_records_host: the same objects as one store of records decode
     and hash to the packed batch's coordinates."""
     types, blob, base, lens = synth.make_batch_host("cfg3b", 200, seed=51)
-    rec = synth.encode_records_host(types, blob, base, lens, first_version=5)
+    rec = synth.encode_store_host(types, blob, base, lens, first_version=5)
     coords, versions, bad = oracle.hash_encoded(types, *rec)
     want, _ = oracle.hash_batch(types, blob, base, lens)
     assert not bad.any() and np.array_equal(coords, want)
@@ -396,7 +396,7 @@ def test_gpu_encoded_records(oracle, case, variant):
     import hyperdex_amd as hdx
     dev = torch.device("cuda", 0)
     types, blob, base, lens = synth.make_batch_host("cfg3b", 3001, seed=52)
-    rec = synth.encode_records_host(types, blob, base, lens, first_version=11)
+    rec = synth.encode_store_host(types, blob, base, lens, first_version=11)
     rng = np.random.default_rng(53)
     if case == "gaps":
         rec = _records_with_gaps(rec, rng)
@@ -415,15 +415,23 @@ def test_gpu_encoded_records(oracle, case, variant):
 
 
 @pytest.mark.gpu
-def test_gpu_encoded_records_device_generator(oracle):
-    """make_encoded_device(layout="records") writes exactly the host encoding."""
+@pytest.mark.parametrize("layout", ["keycol", "records"])
+def test_gpu_encoded_store_device_generator(oracle, layout):
+    """make_encoded_device(layout=...) writes exactly the host encoding, and
+    the sweep over it (keys as one span, or records as one span) matches the
+    oracle."""
     import torch
+
+    import hyperdex_amd as hdx
     dev = torch.device("cuda", 0)
     types, blob, base, lens = synth.make_batch_host("cfg3b", 1500, seed=54, first=777)
-    want = synth.encode_records_host(types, blob, base, lens, first_version=777)
-    got = synth.make_encoded_device("cfg3b", 1500, seed=54, first=777, device=dev, layout="records")
+    want = synth.encode_store_host(types, blob, base, lens, first_version=777, layout=layout)
+    got = synth.make_encoded_device("cfg3b", 1500, seed=54, first=777, device=dev, layout=layout)
     assert np.array_equal(got[1].cpu().numpy()[:len(want[0])], want[0])
-    for g, w in zip(got[2:4], want[1:3]):
+    assert np.array_equal(got[4].cpu().numpy()[:len(want[3])], want[3])
+    for g, w in zip(got[2:4] + got[5:], want[1:3] + want[4:]):
         assert np.array_equal(g.cpu().numpy().view(w.dtype), w)
-    assert np.array_equal(got[5].cpu().numpy().view(np.uint64), want[4])
-    assert np.array_equal(got[6].cpu().numpy().view(np.uint32), want[5])
+    coords, _, _ = oracle.hash_encoded(types, *want)
+    c = hdx.hash_encoded(types, *got[1:])
+    torch.cuda.synchronize()
+    assert np.array_equal(c.cpu().numpy().view(np.uint64), coords)

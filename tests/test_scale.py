@@ -54,14 +54,15 @@ def torch_dev():
     return torch, torch.device("cuda", 0)
 
 
-@pytest.mark.parametrize("layout", ["columns", "records"])
+@pytest.mark.parametrize("layout", ["columns", "keycol", "records"])
 def test_cfg5_sweep_at_50M(oracle, torch_dev, layout):
     """Config 5 at BASELINE size: 50 M stored objects, values far past 4 GiB
     of offsets; coordinates, versions and the status word sampled against
     the oracle, two launches identical, and the regions entry point with no
     coordinates (its 1 GiB scratch chunks) equal to lookups on the sweep's
-    own coordinates.  Both store layouts: keys in place in their packed
-    objects beside a value column, and records [key][value] in one store."""
+    own coordinates.  Every store layout: keys in place in their packed
+    objects beside a value column, a key column beside a value column, and
+    records [key][value] in one store."""
     from hyperdex_amd import RegionTable
     torch, dev = torch_dev
     n = 50_000_000
