@@ -97,6 +97,9 @@ __device__ __forceinline__ uint64_t hash_global(const uint8_t* p, uint32_t code,
     return hash_blk<false, false, true>(code, p, n, consume_any<true>(issue_any<true>(code, p, n)), bad);
 }
 
+// lane 0's offset (the group's first object)
+__device__ __forceinline__ uint64_t k0_of(uint64_t off) { return rl64(off, 0); }
+
 // copy [src, src + bytes) (src 16-byte aligned) to LDS dst: whole 16-byte
 // units by LDS DMA, the last partial unit as dwords (a dword never crosses a
 // page, so nothing past the span's last dword is read); ASM: inline-asm DMA
@@ -177,15 +180,17 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
     // block's adjacency; synth.make_encoded_device(layout="records")) is one
     // contiguous run of bytes per group: copied by one span DMA, keys and
     // values then both read from it.
-    const uint64_t ka = (uint64_t)(uintptr_t)(a.keys + koff), va = (uint64_t)(uintptr_t)(a.vals + voff);
-    const uint64_t ka_next = sh64(ka, (lane + 1) & 63);
-    const bool recs = RECS && __all((uint32_t)lane >= nobj ||
-                                    (va == ka + klen && ((uint32_t)lane + 1 >= nobj || ka_next == va + vlen)));
+    // (keys == vals, a wave-uniform test, gates the per-lane check: the other
+    // layouts pay one scalar compare)
     uint64_t rend = 0;
     bool rspan = false;
-    if (recs) {
-        rend = rl64(va + vlen, (int)nobj - 1);
-        rspan = rend - rl64(ka, 0) + (rl64(ka, 0) & 15) <= WB;
+    if (RECS && a.keys == a.vals) {
+        const uint64_t knx = sh64(koff, (lane + 1) & 63);
+        if (__all((uint32_t)lane >= nobj ||
+                  (voff == koff + klen && ((uint32_t)lane + 1 >= nobj || knx == voff + vlen)))) {
+            rend = rl64(voff + vlen, (int)nobj - 1);
+            rspan = rend - k0_of(koff) + ((uintptr_t)(a.keys + k0_of(koff)) & 15) <= WB;
+        }
     }
 
     // ---- else the keys, then the value span (whatever of it fits) -----------
@@ -201,10 +206,9 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
     const uint64_t v0 = rl64(voff, 0);
     uint32_t vlead = (uint32_t)((uintptr_t)(a.vals + v0) & 15), vheld = 0;
     if (rspan) {
-        const uint64_t ka0 = rl64(ka, 0);
         kspan = keys_in = true;  // kreg 0: the values lie in the same span
-        vlead = klead + (uint32_t)(rl64(va, 0) - ka0);
-        vheld = klead + (uint32_t)(rend - ka0);
+        vlead = klead + (uint32_t)(v0 - k0);
+        vheld = klead + (uint32_t)(rend - k0);
         copy_span<ASM>(a.keys + k0 - klead, win + kFrontS, vheld, lane);
     } else {
         if (kruns) {

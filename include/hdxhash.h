@@ -197,8 +197,10 @@ hdx_status hdx_hash_batch_device_multi(const uint32_t* types, uint32_t attrs_sz,
  * attributes lying inside its bytes gets zero coordinates (and version 0)
  * and (1u << HDX_E_BADENC) is ORed into status_dev (may be NULL).  The
  * reference's decode_value does not check that the last attribute ends
- * inside the value (:201-213); this does.  Device pointers, asynchronous;
- * attrs_sz <= 128. */
+ * inside the value (:201-213); this does.  Any placement of keys and values
+ * is exact; keys back to back, values back to back, or — keys == vals —
+ * records [key][value] back to back are read with coalesced span copies.
+ * Device pointers, asynchronous; attrs_sz <= 128. */
 hdx_status hdx_hash_encoded_device(const uint32_t* types, uint32_t attrs_sz,
                                    const uint8_t* keys, const uint64_t* key_off,
                                    const uint32_t* key_len, const uint8_t* vals,
