@@ -280,7 +280,8 @@ def run_rank(args):
         result["roofline"]["frac_of_probe"] = round(
             achieved / sp.get("read_write_mix_GBps", sp["read_write_1to8_GBps"]), 4)
     if cfg == "cfg5":
-        result["roofline"]["kernel"] = "void hdx::hash_sweep_wstage_kernel<2, 8704u, 6u, false, true, 0, 13, false, true, true, true>(hdx::EncodedArgs)"
+        result["roofline"]["kernel"] = ("void hdx::hash_sweep_wstage_kernel<2, 8704u, 6u, false, true, 0, 13, false, true, "
+                                        "true, %s>(hdx::EncodedArgs)" % ("true" if args.store_layout == "records" else "false"))
     if world > 1 and not args.no_allgather:
         result["allgather"] = time_allgather(coords, world, dev, backend, max_over_ranks)
         # hash phase then the coordinate exchange, back to back
