@@ -140,7 +140,7 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
 // SHAPE (debug forms 7 / 8, WRONG coordinates): 1 = no hash (a slot's
 // coordinate is its descriptor), 2 = no hash and no walk.
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
-          bool ASM = false, bool PU = true, bool BF = false, bool RECS = true>
+          bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true>
 __global__ void __launch_bounds__(256)
 hash_sweep_wstage_kernel(const EncodedArgs a) {
     constexpr uint32_t SL = NCH * 64;
@@ -205,6 +205,8 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
     bool keys_in = false, kspan = false;
     const uint64_t v0 = rl64(voff, 0);
     uint32_t vlead = (uint32_t)((uintptr_t)(a.vals + v0) & 15), vheld = 0;
+    const uint64_t kaddr = (uint64_t)(uintptr_t)(a.keys + koff);
+    uint32_t kU = 0;  // keys gathered as 16-byte units: units per key slot
     if (rspan) {
         kspan = keys_in = true;  // kreg 0: the values lie in the same span
         vlead = klead + (uint32_t)(v0 - k0);
@@ -220,7 +222,25 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
                 copy_span<ASM>(a.keys + k0 - klead, win + kFrontS, klead + (uint32_t)(kend - k0), lane);
             }
         }
-        if (!kspan) {
+        // keys in their own places, as whole 16-byte units: lane o*U + k copies
+        // unit k of key o (U = the most units a key of the group spans) with
+        // one LDS DMA; key o lands at 16*U*o + (its address & 15)
+        const uint32_t ku = (uint32_t)lane < nobj ? ((uint32_t)(kaddr & 15) + klen + 15) >> 4 : 0u;
+        if (!kspan && KUNITS) {
+            for (uint32_t o = 0; o < nobj; ++o) kU = std::max(kU, (uint32_t)__builtin_amdgcn_readlane(ku, (int)o));
+            if (kU && nobj * kU <= 64 && 16 * nobj * kU <= WB / 4) {
+                const uint32_t magic = (65536u + kU - 1) / kU;  // lane / kU for lane < 64, kU <= 64
+                const uint32_t o = ((uint32_t)lane * magic) >> 16, k = (uint32_t)lane - o * kU;
+                const uint64_t src = sh64(kaddr & ~15ull, (int)(o & 63)) + 16ull * k;
+                const uint32_t uo = (uint32_t)__shfl((int)ku, (int)(o & 63), 64);
+                if (o < nobj && k < uo) dma16<ASM>((const void*)(uintptr_t)src, win + kFrontS);
+                keys_in = true;
+                kreg = 16 * nobj * kU;
+            } else {
+                kU = 0;
+            }
+        }
+        if (!kspan && !kU) {
             // lane o < nobj: its key's dwords [kd, kd + kdw) from the key's dword floor
             const uint64_t kd = (uint64_t)(uintptr_t)(a.keys + koff) >> 2;
             const uint32_t kdw =
@@ -254,7 +274,9 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
     bool bad = false, ok = false;
     uint64_t my_version = 0;  // stored with the coordinates (a store here would stall the LDS atomics' waits)
     if ((uint32_t)lane < nobj) {
-        const uint32_t kw = kFrontS + (kspan ? klead + (uint32_t)(koff - k0) : 4 * kdx + (uint32_t)((uintptr_t)(a.keys + koff) & 3));
+        const uint32_t kw = kFrontS + (kspan ? klead + (uint32_t)(koff - k0)
+                                       : kU   ? 16 * kU * (uint32_t)lane + (uint32_t)(kaddr & 15)
+                                              : 4 * kdx + (uint32_t)(kaddr & 3));
         desc[lane * A] = keys_in ? ((uint64_t)kw | ((uint64_t)klen << 32)) : ((uint64_t)0 | ((uint64_t)(klen | kGlobal) << 32));
         const uint64_t vrel = voff - v0;
         const bool vin = voff >= v0 && vlead + vrel + vlen <= vheld;
@@ -386,14 +408,14 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
 }
 
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
-          bool ASM = false, bool PU = true, bool BF = false, bool RECS = true>
+          bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true>
 static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
     const uint32_t K = std::min<uint32_t>(64 * NCH / a.A, KCAP);
     if (K == 0) return hipErrorInvalidValue;
     const uint64_t waves = (a.n + K - 1) / K;
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU, BF, RECS>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU, BF, RECS, KUNITS>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -440,6 +462,7 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 15: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, false>(a, stream);  // the branchy class, guarded loads
         case 16: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false, true, true>(a, stream);  // without TNUM
         case 17: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false>(a, stream);  // without the record span
+        case 18: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, false>(a, stream);  // keys in place gathered by dwords (round 3)
         default: return hipErrorInvalidValue;
     }
 }
