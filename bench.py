@@ -242,7 +242,8 @@ def run_rank(args):
     else:  # payload + 4 B length + 8 B coordinate per attribute
         algo_bytes = payload + n * A * ALGO_EXTRA_PER_ATTR
     achieved = algo_bytes / (kernel_ms / 1e3) / 1e9
-    traffic, traffic_src = measured_traffic(args.traffic, cfg, n)
+    traffic_key = cfg + ({"keycol": "k", "records": "r"}.get(args.store_layout, "") if cfg == "cfg5" else "")
+    traffic, traffic_src = measured_traffic(args.traffic, traffic_key, n)
 
     result = {
         "metric": "hashed GiB/s (device-resident) + Mobjects/s, 16-attr×64B batches",

@@ -13,7 +13,7 @@
 #   ab=CFG:V1,V2[:R]   scripts/ab_variants.py, interleaved A/B of debug variants
 #   pmc=CFG:V1,V2[:SET] counter passes over scripts/run_kernel.py per variant (pmc_profile.sh),
 #                      summarised by pmc_summary.py; SET "lds" = the LDS / VALU / wait set
-#   profile            scripts/profile_r2.sh TAG (round evidence: traces + PMC traffic)
+#   profile[=MODE]     scripts/profile_r2.sh TAG MODE (round evidence: MODE trace | pmc | all)
 #   py=SCRIPT[,ARGS]   python SCRIPT ARGS (commas for spaces)
 #   sh=SCRIPT[,ARGS]   bash SCRIPT ARGS (commas for spaces)
 set -o pipefail
@@ -57,7 +57,7 @@ for STEP in "$@"; do
       done
       (exit $rc) ;;
     profile)
-      timeout -k 10 1100 bash scripts/profile_r2.sh "$TAG" > "$log" 2>&1 ;;
+      timeout -k 10 1150 bash scripts/profile_r2.sh "$TAG" "${arg:-all}" > "$log" 2>&1 ;;
     py)
       timeout -k 10 900 python -u ${arg//,/ } > "$log" 2> "$log.err" ;;
     sh)
