@@ -159,6 +159,14 @@ hdx_status bind_device(int want /* -1: current */) {
     return HDX_OK;
 }
 
+void release_thread_scratch() {
+    t_state.release();
+    if (t_state.tracked) {
+        untrack_scratch(&t_state);
+        t_state.tracked = false;
+    }
+}
+
 hdx_status thread_stream(hipStream_t* out) {
     hdx_status st = bind_device(-1);
     if (st != HDX_OK) return st;

@@ -33,6 +33,11 @@ void track_scratch(Scratch* s);
 void untrack_scratch(Scratch* s);
 // Binds the calling thread to `want` (-1: its current device) after checking it is gfx950.
 hdx_status bind_device(int want);
+// Frees the calling thread's library scratch now (streams, staging) and
+// unregisters it: a thread the library owns calls it as its last job, so no
+// HIP call runs in its thread-local destructors at exit (rocprofv3, among
+// others, has torn down its per-thread state by then).
+void release_thread_scratch();
 // The calling thread's library stream (created on first use).
 hdx_status thread_stream(hipStream_t* out);
 // The single-device host-resident pipeline (hdx_capi.cpp) on the calling

@@ -191,9 +191,13 @@ static DeviceSet* g_set = nullptr;
 
 static void destroy_set(DeviceSet* ds) {
     if (!ds) return;
-    // workers first: their thread-local scratch is released (and untracked)
-    // as they exit, before hdx_shutdown walks the scratch registry
-    for (auto& w : ds->workers) w->join();
+    // workers first: each frees its thread's scratch as its last job (not in
+    // a thread-local destructor at exit) before hdx_shutdown walks the
+    // scratch registry
+    for (auto& w : ds->workers) {
+        w->post([] { release_thread_scratch(); });
+        w->join();
+    }
     ds->workers.clear();
     for (size_t k = 0; k < ds->comms.size(); ++k) {
         (void)hipSetDevice(ds->devs[k]);
