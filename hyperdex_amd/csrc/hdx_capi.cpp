@@ -695,6 +695,7 @@ HDX_EXPORT hdx_status hdx_region_table_create(uint32_t dims, uint32_t regions, c
     std::vector<uint64_t> index;
     region_index_build(dims, regions, lower, upper, index, t->W);
     if (!index.empty() && !region_index_disabled()) {
+        t->h_index = index;
         t->index_words = (uint32_t)index.size();
         if (hipMalloc((void**)&t->d_index, index.size() * 8) != hipSuccess ||
             hipMemcpy(t->d_index, index.data(), index.size() * 8, hipMemcpyHostToDevice) != hipSuccess) {

@@ -96,13 +96,42 @@ struct hdx_region_table_s {
     uint64_t* d_index;  // interval index (NULL: lookups scan the boxes)
     uint32_t W, index_words;
     // host copies (the batcher's calling-thread lookups)
-    std::vector<uint64_t> h_lower, h_upper, h_ids;
+    std::vector<uint64_t> h_lower, h_upper, h_ids, h_index;
 };
 
 // configuration::lookup_region (common/configuration.cc:698-735) on the host:
 // the first region whose box holds hs[attrs[d]] on every dimension (bounds
-// inclusive), else 0 (region_id()).
+// inclusive), else 0 (region_id()).  Through the table's interval index when
+// it has one (hdx_region_lookup.h's lookup_indexed_fn, host form: per
+// dimension the top byte's bucket, a binary search, the interval's mask; the
+// lowest bit of the masks' AND), else the reference's scan.
 inline uint64_t region_lookup_host(const hdx_region_table_s* t, const uint64_t* hs) {
+    if (!t->h_index.empty()) {
+        const uint64_t* idx = t->h_index.data();
+        uint64_t acc[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+        for (uint32_t d = 0; d < t->D; ++d) {
+            const uint64_t hdr = idx[d];
+            const uint64_t* B = idx + ((hdr >> 16) & 0xffffff);
+            const uint64_t hv = hs[t->attrs[d]];
+            const uint16_t* start = reinterpret_cast<const uint16_t*>(B - 65 /* kIndexBucketWords */);
+            const uint32_t b = (uint32_t)(hv >> 56);
+            uint32_t pos = start[b], cnt = start[b + 1] - pos;
+            while (cnt) {
+                const uint32_t half = cnt >> 1;
+                if (B[pos + half] <= hv) {
+                    pos += half + 1;
+                    cnt -= half + 1;
+                } else {
+                    cnt = half;
+                }
+            }
+            const uint64_t* mask = idx + (hdr >> 40) + (size_t)pos * t->W;
+            for (uint32_t w = 0; w < t->W; ++w) acc[w] &= mask[w];
+        }
+        for (uint32_t w = 0; w < t->W; ++w)
+            if (acc[w]) return t->h_ids[64 * w + __builtin_ctzll(acc[w])];
+        return 0;
+    }
     for (uint32_t r = 0; r < t->R; ++r) {
         const uint64_t* lo = t->h_lower.data() + (size_t)r * t->D;
         const uint64_t* up = t->h_upper.data() + (size_t)r * t->D;
