@@ -99,6 +99,7 @@ SIGNATURES = [
 DEBUG_SIGNATURES = [
     ("hdxdbg_set_kernel_variant", _i32, [_i32]),
     ("hdxdbg_kernel_variant", _i32, []),
+    ("hdxdbg_init_devices", _i32, [_vp, _i32]),
 ]
 
 _LIB = None

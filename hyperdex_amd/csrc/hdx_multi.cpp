@@ -225,7 +225,7 @@ void device_set_teardown() {
 hdx_status device_set_create(uint64_t mask, const std::vector<int>& devs) {
     {
         std::lock_guard<std::mutex> lk(g_set_mu);
-        if (g_set && g_set->mask == mask) return HDX_OK;
+        if (g_set && g_set->mask == mask && g_set->devs == devs) return HDX_OK;
     }
     device_set_teardown();  // a different mask replaces the set (no call may be in progress)
     int cur = -1;
@@ -426,6 +426,10 @@ HDX_EXPORT hdx_status hdx_hash_batch_device_multi(const uint32_t* types, uint32_
         row += s.n;
     }
     if (gather) {
+        for (uint32_t k = 1; k < nshards; ++k)
+            for (uint32_t j = 0; j < k; ++j)
+                if (ds->devs[j] == ds->devs[k])  // hdxdbg_init_devices: no communicator over one GPU twice
+                    return fail(HDX_E_INVALID, "device %d twice in the set: no RCCL gather", ds->devs[k]);
         if (ds->comms.empty()) {
             ds->comms.resize(nshards);
             ncclResult_t r = ncclCommInitAll(ds->comms.data(), (int)nshards, ds->devs.data());
@@ -467,3 +471,19 @@ HDX_EXPORT hdx_status hdx_hash_batch_device_multi(const uint32_t* types, uint32_
     }
     return HDX_OK;
 }
+
+#if HDX_DEBUG_BUILD
+// Debug library only (include/hdxhash_debug.h): a device set of explicit
+// ordinals, repeats allowed, so the multi-device host path and ungathered
+// shards run at world 2, 3, ... on a one-GPU box (tests/test_multi.py).
+HDX_EXPORT hdx_status hdxdbg_init_devices(const int* devices, int n) {
+    if (!devices || n <= 0 || n > 64) return fail(HDX_E_INVALID, "1 <= n <= 64 devices");
+    const int nd = hdx_device_count();
+    std::vector<int> devs(devices, devices + n);
+    for (int d : devs)
+        if (d < 0 || d >= nd) return fail(HDX_E_INVALID, "device %d (count %d)", d, nd);
+    hdx_status st = bind_device(devs[0]);
+    if (st != HDX_OK) return st;
+    return device_set_create(1ull << 63, devs);  // mask bit 63: an explicit list
+}
+#endif

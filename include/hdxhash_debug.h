@@ -35,6 +35,10 @@ int hdxdbg_kernel_for(const uint32_t* types, uint32_t attrs_sz, uint64_t n, cons
  * 64-byte-attribute configs).  Asynchronous on `stream`.  bench.py reports the
  * rate as the practical ceiling beside the HBM3E spec. */
 int hdxdbg_stream_probe(const void* src, uint64_t bytes, uint64_t* sink, int write, void* stream);
+/* [debug library only] The device set of hdx_init_mask from an explicit list
+ * of HIP ordinals, repeats allowed (world 2+ on one GPU: host batches and
+ * ungathered shards; a gather over a repeated device returns HDX_E_INVALID). */
+int hdxdbg_init_devices(const int* devices, int n);
 /* Objects per scratch chunk of the regions entry points when the caller
  * wants no coordinates (n objects of attrs_sz attributes; hdx_regions.hip). */
 uint64_t hdxdbg_region_chunk_objects(uint64_t n, uint32_t attrs_sz);

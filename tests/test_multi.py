@@ -185,3 +185,75 @@ def test_cpp_daemon_uses_every_device():
     r = subprocess.run([MULTI_EXE, "200000"], capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "multi ok" in r.stdout, r.stdout
+
+
+# ---- world 2 and 3 on one GPU (debug library: a device set listing device 0 repeatedly) ----
+
+@pytest.fixture(params=[2, 3])
+def repeated_set(request):
+    """hdxdbg_init_devices([0] * world): `world` workers and streams on device 0,
+    so the multi-device cuts, the per-device workers and the shard plumbing
+    run at world > 1 on the one-GPU box."""
+    import torch
+    assert torch.cuda.is_available()
+    world = request.param
+    with _lib.debug_library() as dbg:
+        devs = (ctypes.c_int * world)(*([0] * world))
+        assert dbg.hdxdbg_init_devices(devs, world) == _lib.HDX_OK
+        assert hdx.device_set() == [0] * world
+        yield torch, world
+        hdx.shutdown()
+
+
+@pytest.mark.gpu
+def test_host_batch_split_over_repeated_set(oracle, repeated_set):
+    """hdx_hash_batch_host cut into `world` byte-balanced ranges, one per
+    worker: bit-exact, also for a multi-chunk batch and a bad size in the last
+    range (its error, after the other ranges ran)."""
+    torch, world = repeated_set
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 30_001, seed=61)
+    want, _ = oracle.hash_batch(types, blob, base, lens)
+    assert np.array_equal(hdx.hash_batch_host(types, blob, base, lens), want)
+    types, blob, base, lens = synth.make_batch_host("cfg3a", 300_000, seed=62)  # ~326 MB: chunks per range
+    got = hdx.hash_batch_host(types, blob, base, lens)
+    idx = np.sort(np.random.default_rng(3).choice(len(base), 3000, replace=False))
+    w2, _ = oracle.hash_batch(types, blob, base[idx], lens.reshape(len(base), -1)[idx].ravel())
+    assert np.array_equal(got[idx], w2)
+    types, blob, base, lens = synth.make_batch_host("cfg2", 60_000, seed=63)
+    lens = lens.copy()
+    lens[59_990 * len(types) + 1] = 3
+    out = np.zeros((len(base), len(types)), np.uint64)
+    with pytest.raises(hdx.HdxError) as e:
+        hdx.hash_batch_host(types, blob, base, lens, out=out)
+    assert e.value.status == _lib.HDX_E_BADSIZE
+    first = hashing.shard_ranges(lens, len(types), len(base), world)[0]
+    w3, _ = oracle.hash_batch(types, blob, base[:first[1]], lens[:first[1] * len(types)])
+    assert np.array_equal(out[:first[1]], w3.reshape(first[1], -1))  # range 0 ran to completion
+
+
+@pytest.mark.gpu
+def test_device_shards_over_repeated_set(oracle, repeated_set):
+    """hdx_hash_batch_device_multi with `world` shards cut by hdx_shard_ranges
+    (unequal counts), ungathered: every shard's rows bit-exact; a gather over
+    a repeated device is refused before RCCL is touched."""
+    torch, world = repeated_set
+    dev = torch.device("cuda", 0)
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 40_003, seed=64)
+    A = len(types)
+    want, _ = oracle.hash_batch(types, blob, base, lens)
+    ranges = hashing.shard_ranges(lens, A, len(base), world)
+    assert len(set(c for _, c in ranges)) > 1  # byte-balanced: unequal counts
+    shards = []
+    for f, c in ranges:
+        sb = base[f:f + c]
+        lo = int(sb[0])
+        hi = int(sb[-1] + lens[(f + c - 1) * A:(f + c) * A].astype(np.uint64).sum())
+        shards.append((torch.from_numpy(blob[lo:hi].copy()).to(dev),
+                       torch.from_numpy((sb - np.uint64(lo)).view(np.int64).copy()).to(dev),
+                       torch.from_numpy(lens[f * A:(f + c) * A].view(np.int32).copy()).to(dev)))
+    outs = hdx.hash_batch_device_multi(types, shards, gather=False)
+    for (f, c), o in zip(ranges, outs):
+        assert np.array_equal(o.cpu().numpy().view(np.uint64), want[f:f + c])
+    with pytest.raises(hdx.HdxError) as e:
+        hdx.hash_batch_device_multi(types, shards, gather=True)
+    assert e.value.status == _lib.HDX_E_INVALID
