@@ -318,7 +318,7 @@ hdx_status hash_host_set(const uint8_t* codes, uint32_t A, const uint8_t* blob, 
         if (cnt == 0) return HDX_OK;
         hdx_status s = bind_device(ds->devs[k]);
         if (s != HDX_OK) return s;
-        return hash_host(codes, A, blob, blob_bytes, obj_base, attr_len + f * A, cnt, coords + f * A);
+        return hash_host(codes, A, blob, blob_bytes, obj_base + f, attr_len + f * A, cnt, coords + f * A);
     });
 }
 
