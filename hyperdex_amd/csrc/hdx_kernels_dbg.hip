@@ -804,6 +804,7 @@ static bool known_variant(int v) {
         case 249:  // debug shape of 212: no funnel shifts on its LDS reads (WRONG coordinates)
         case 250:  // the product sweep (230) without the record span
         case 251:  // ... and with round 3's dword-by-dword key gather
+        case 252:  // debug shape of 250: no copy, no walk, the hash on made-up descriptors (WRONG coordinates)
         case 223: case 224: case 225: case 226: case 227:  // its debug shapes (WRONG coordinates)
         case 210: case 211:  // wave-staged, sorted over the workgroup
         case 40: case 41:

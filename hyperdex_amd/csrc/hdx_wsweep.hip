@@ -137,7 +137,8 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
 // GAP: the class straddling the pass boundary moves whole into the second
 // pass when pads allow (class_sort, hdx_regroup.h).
 // LOOP: hash_slot_window's; + 10: with TNUM.
-// SHAPE (debug forms 7 / 8, WRONG coordinates): 1 = no hash (a slot's
+// SHAPE (debug forms 7 / 8 / 19, WRONG coordinates): 3 = no copy and no walk,
+// the hash on made-up descriptors (the compute alone); 1 = no hash (a slot's
 // coordinate is its descriptor), 2 = no hash and no walk.
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
           bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true>
@@ -211,7 +212,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         kspan = keys_in = true;  // kreg 0: the values lie in the same span
         vlead = klead + (uint32_t)(v0 - k0);
         vheld = klead + (uint32_t)(rend - k0);
-        copy_span<ASM>(a.keys + k0 - klead, win + kFrontS, vheld, lane);
+        if (SHAPE != 3) copy_span<ASM>(a.keys + k0 - klead, win + kFrontS, vheld, lane);
     } else {
         if (kruns) {
             const uint64_t kend = rl64(koff + klen, (int)nobj - 1);
@@ -219,7 +220,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
             keys_in = kspan;
             if (kspan) {
                 kreg = (klead + (uint32_t)(kend - k0) + 15) & ~15u;
-                copy_span<ASM>(a.keys + k0 - klead, win + kFrontS, klead + (uint32_t)(kend - k0), lane);
+                if (SHAPE != 3) copy_span<ASM>(a.keys + k0 - klead, win + kFrontS, klead + (uint32_t)(kend - k0), lane);
             }
         }
         // keys in their own places, as whole 16-byte units: lane o*U + k copies
@@ -233,7 +234,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
                 const uint32_t o = ((uint32_t)lane * magic) >> 16, k = (uint32_t)lane - o * kU;
                 const uint64_t src = sh64(kaddr & ~15ull, (int)(o & 63)) + 16ull * k;
                 const uint32_t uo = (uint32_t)__shfl((int)ku, (int)(o & 63), 64);
-                if (o < nobj && k < uo) dma16<ASM>((const void*)(uintptr_t)src, win + kFrontS);
+                if (o < nobj && k < uo && SHAPE != 3) dma16<ASM>((const void*)(uintptr_t)src, win + kFrontS);
                 keys_in = true;
                 kreg = 16 * nobj * kU;
             } else {
@@ -265,7 +266,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         }
         const uint64_t vend = has_next ? rl64(voff, (int)nobj) : 0;
         vheld = has_next && vend >= v0 ? (uint32_t)std::min<uint64_t>(vlead + (vend - v0), WB - kreg) : 0u;
-        if (vheld) copy_span<ASM>(a.vals + v0 - vlead, win + kFrontS + kreg, vheld, lane);
+        if (vheld && SHAPE != 3) copy_span<ASM>(a.vals + v0 - vlead, win + kFrontS + kreg, vheld, lane);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the compiler does not order ds_read after LDS DMA
     wave_fence();
@@ -319,7 +320,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
             ok = vlen >= 10 && w_be16(lw, vw + 8) == A - 1;
             uint32_t pos = 10;
             uint64_t* dp = desc + lane * A + 1;
-            if (SHAPE == 2) {  // debug shape: no walk (descriptors of assorted lengths at the value's start)
+            if (SHAPE >= 2) {  // debug shapes: no walk (descriptors of assorted lengths at the value's start)
                 for (uint32_t k = 0; k + 1 < A; ++k) dp[k] = (uint64_t)(vw + 14) | ((uint64_t)((k * 37) & 127) << 32);
                 pos = vlen;
             } else
@@ -387,7 +388,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         uint64_t h = 0;
         if (s < ns && off != kZero) {
             if (ln & kGlobal) h = hash_global((j == 0 ? a.keys : a.vals) + ob + off, code, ln & ~kGlobal, bad);
-            else if (SHAPE) h = d ^ lw[off >> 2];
+            else if (SHAPE == 1 || SHAPE == 2) h = d ^ lw[off >> 2];
             else h = hash_slot_window<false, (LOOP >= 10 ? LOOP - 10 : LOOP), (LOOP >= 10)>(lw, code, off, ln, bad);
         }
         desc[s] = h;
@@ -463,6 +464,7 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 16: return launch_wsweep_t<2, 8704, 6, false, true, 0, 3, false, true, true>(a, stream);  // without TNUM
         case 17: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false>(a, stream);  // without the record span
         case 18: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, false>(a, stream);  // keys in place gathered by dwords (round 3)
+        case 19: return launch_wsweep_t<2, 8704, 6, false, true, 3, 13, false, true, true, false>(a, stream);  // debug shape: no copy, no walk, the hash
         default: return hipErrorInvalidValue;
     }
 }
