@@ -313,6 +313,11 @@ def run_rank(args):
     if args.config4_objects and cfg != "cfg5":
         result["config4"] = time_config4(args.config4_objects, world, rank, dev, stream, max_over_ranks,
                                          backend, gather=not args.no_allgather)
+        if world == 1:
+            # the same batch through the C-ABI device set: one process drives
+            # every visible device (what a C++ daemon links), RCCL gather in-process
+            torch.cuda.empty_cache()
+            result["config4_device_set"] = time_config4_device_set(args.config4_objects, dev, stream)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if cfg == "cfg5":
@@ -357,6 +362,71 @@ def time_allgather(coords, world, dev, backend, max_over_ranks, reps=3):
     res["d2h_local_shard_ms"] = round(d2h * 1e3, 3)
     res["d2h_GBps_per_gpu"] = round(coords.numel() * 8 / d2h / 1e9, 2)
     del host
+    return res
+
+
+def time_config4_device_set(n_total, dev0, stream, steps=3):
+    """Config 4 through the C-ABI device set (hdx_init_mask over every visible
+    device, hdx_hash_batch_device_multi): the batch cut as time_config4 cuts
+    it, shard k generated on device 0 and moved to device k, then the hash
+    phase (gather = 0) and hash + the in-process RCCL gather (gather = 1),
+    each a synchronous call timed on the host clock.  On a one-GPU box the set
+    is {0} and the gather a communicator of one."""
+    import torch
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import _lib, synth
+    from hyperdex_amd import dist as hdist
+    lib = _lib.lib()
+    ndev = max(1, lib.hdx_device_count())
+    rules = synth.CONFIGS["cfg3b"]
+    A = len(rules)
+    cr = synth.c_rules(rules)
+    sizes = torch.empty(n_total, dtype=torch.int64, device=dev0)
+    chunk = 8_000_000
+    tmp = torch.empty(chunk * A, dtype=torch.int32, device=dev0)
+    for f in range(0, n_total, chunk):
+        c = min(chunk, n_total - f)
+        _lib.check(lib.hdx_synth_lengths(cr, A, synth.SEED, f, c, tmp.data_ptr(), stream.cuda_stream))
+        sizes[f:f + c] = tmp[:c * A].view(c, A).to(torch.int64).sum(dim=1)
+    del tmp
+    ranges = hdist.shard_ranges(n_total, ndev, sizes, equal_count_tol=CONFIG4_EQUAL_COUNT_TOL)
+    shard0_bytes = int(sizes[:ranges[0][1]].sum().item())
+    del sizes
+    shards, full, own = [], [], []
+    for k, (f, c) in enumerate(ranges):
+        dk = torch.device("cuda", k)
+        types, blob, base, lens = synth.make_batch_device("cfg3b", c, first=f, device=dev0)
+        if k:
+            blob, base, lens = blob.to(dk), base.to(dk), lens.to(dk)
+        torch.cuda.synchronize(dev0)
+        shards.append((blob, base, lens))
+        full.append(torch.empty((n_total, A), dtype=torch.int64, device=dk))
+        own.append(full[-1][:c])  # gather = 0: each shard's own rows
+    hdx.init_mask((1 << ndev) - 1)
+    try:
+        def timed(gather, outs):
+            hdx.hash_batch_device_multi(types, shards, gather=gather, coords=outs)  # warm-up
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                hdx.hash_batch_device_multi(types, shards, gather=gather, coords=outs)
+            return (time.perf_counter() - t0) / steps * 1e3
+        hash_ms = timed(False, own)
+        both_ms = timed(True, full)
+    finally:
+        hdx.shutdown()
+    counts = [c for _, c in ranges]
+    res = {"workload": "config 4: %dM config-3b objects over the C-ABI device set of %d GPU(s)"
+                       % (n_total // 1_000_000, ndev),
+           "devices": ndev, "objects_per_device": counts, "hash_ms": round(hash_ms, 3),
+           "mobjects_per_s": round(n_total / (hash_ms / 1e3) / 1e6, 1),
+           "device0_roofline_frac": round((shard0_bytes + counts[0] * A * ALGO_EXTRA_PER_ATTR) /
+                                          (hash_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+           "hash_and_gather_ms": round(both_ms, 3),
+           "gather": "in-place ncclAllGather" if len(set(counts)) == 1 else "grouped in-place ncclBroadcast",
+           "timing": "host clock around synchronous hdx_hash_batch_device_multi calls"}
+    del shards, full, own
+    torch.cuda.empty_cache()
     return res
 
 
