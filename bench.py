@@ -38,6 +38,14 @@ import time
 import numpy as np
 
 
+def sweep_kernel_name(layout):
+    """The product sweep's kernel (hdx_wsweep.hip launch_hash_wsweep_product) as
+    rocprofv3 names it: the record instantiation when keys and values are one
+    store (layout "records"), else the other one."""
+    return ("void hdx::hash_sweep_wstage_kernel<2, 8704u, 6u, false, true, 0, 13, false, true, true, %s, true, "
+            "false>(hdx::EncodedArgs)" % ("true" if layout == "records" else "false"))
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -281,8 +289,7 @@ def run_rank(args):
         result["roofline"]["frac_of_probe"] = round(
             achieved / sp.get("read_write_mix_GBps", sp["read_write_1to8_GBps"]), 4)
     if cfg == "cfg5":
-        result["roofline"]["kernel"] = ("void hdx::hash_sweep_wstage_kernel<2, 8704u, 6u, false, true, 0, 13, false, true, "
-                                        "true, %s>(hdx::EncodedArgs)" % ("true" if args.store_layout == "records" else "false"))
+        result["roofline"]["kernel"] = sweep_kernel_name(args.store_layout)
     if world > 1 and not args.no_allgather:
         result["allgather"] = time_allgather(coords, world, dev, backend, max_over_ranks)
         # hash phase then the coordinate exchange, back to back

@@ -35,15 +35,100 @@ __device__ __forceinline__ ldsw_t as_ldsw(const void* p) { return (ldsw_t)p; }
 // kernels wait for them themselves (s_waitcnt vmcnt(0) before the window is
 // read).  Any wait the compiler emits for its own loads still covers them
 // (vmcnt counts in issue order), at worst waiting longer.
+// An SALU write of M0 needs one wait state before an LDS-DMA reads it (the
+// s_nop 0 the compiler puts after its own M0 writes).
+__device__ __forceinline__ uint32_t lds_addr_s(const void* p) {
+    return __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)p);
+}
 __device__ __forceinline__ void dma_x4_asm(const void* src, const void* dst) {
-    const uint32_t m0 =
-        __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)dst);
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds_addr_s(dst))
+                 : "memory", "m0");
 }
 __device__ __forceinline__ void dma_x1_asm(const void* src, const void* dst) {
-    const uint32_t m0 =
-        __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)dst);
-    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(lds_addr_s(dst))
+                 : "memory", "m0");
+}
+
+// round 3's span copy (debug forms): both addresses and the predicate per KiB
+template <bool ASM>
+__device__ __forceinline__ void dma_units16_loop(const uint8_t* src, void* dst, uint32_t units) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t u0 = 0; u0 < units; u0 += 64) {
+        const uint32_t u = u0 + lane;
+        if (u < units) {
+            if constexpr (ASM) dma_x4_asm(src + 16ull * u, (uint8_t*)dst + 16 * u0);
+            else __builtin_amdgcn_global_load_lds((const void*)(src + 16ull * u),
+                                                  (__attribute__((address_space(3))) void*)((uint8_t*)dst + 16 * u0), 16, 0, 0);
+        }
+    }
+}
+
+// A span copy: `units` 16-byte units from src (16-byte aligned) to LDS dst,
+// lane l copying units l, l + 64, ...  The instruction's immediate offset
+// applies to both the global and the LDS address, so one VGPR address and
+// one M0 serve four wave-instructions (4 KiB); only the last, partial 1 KiB
+// is predicated (round 3's loop recomputed both addresses and the predicate
+// for every KiB: ~6 VALU + ~8 SALU each).  ASM: inline asm (not seen by the
+// compiler's waits), else the builtin.
+template <bool ASM>
+__device__ __forceinline__ void dma_units16(const uint8_t* src, void* dst, uint32_t units) {
+#if defined(__HIP_DEVICE_COMPILE__)  // the host pass cannot instantiate the VGPR / SGPR constraints
+    const uint32_t lane = threadIdx.x & 63;
+    const uint8_t* p = src + 16 * lane;
+    uint32_t m0 = lds_addr_s(dst);
+    auto at = [&](uint32_t a) { return (__attribute__((address_space(3))) void*)(uintptr_t)a; };
+    uint32_t full = __builtin_amdgcn_readfirstlane(units >> 6);
+    for (; full >= 4; full -= 4) {
+        if constexpr (ASM)
+            asm volatile(
+                "s_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                "global_load_lds_dwordx4 %0, off\n\tglobal_load_lds_dwordx4 %0, off offset:1024\n\t"
+                "global_load_lds_dwordx4 %0, off offset:2048\n\tglobal_load_lds_dwordx4 %0, off offset:3072" ::"v"(p),
+                "s"(m0)
+                : "memory", "m0");
+        else {
+            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 1024, 0);
+            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 2048, 0);
+            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 3072, 0);
+        }
+        p += 4096;
+        m0 += 4096;
+    }
+    if (full) {
+        if constexpr (ASM) {
+            if (full == 1)
+                asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(m0)
+                             : "memory", "m0");
+            else if (full == 2)
+                asm volatile(
+                    "s_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                    "global_load_lds_dwordx4 %0, off\n\tglobal_load_lds_dwordx4 %0, off offset:1024" ::"v"(p),
+                    "s"(m0)
+                    : "memory", "m0");
+            else
+                asm volatile(
+                    "s_mov_b32 m0, %1\n\ts_nop 0\n\t"
+                    "global_load_lds_dwordx4 %0, off\n\tglobal_load_lds_dwordx4 %0, off offset:1024\n\t"
+                    "global_load_lds_dwordx4 %0, off offset:2048" ::"v"(p),
+                    "s"(m0)
+                    : "memory", "m0");
+        } else {
+            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 0, 0);
+            if (full >= 2) __builtin_amdgcn_global_load_lds(p, at(m0), 16, 1024, 0);
+            if (full >= 3) __builtin_amdgcn_global_load_lds(p, at(m0), 16, 2048, 0);
+        }
+        p += 1024 * full;
+        m0 += 1024 * full;
+    }
+    if (lane < (units & 63)) {
+        if constexpr (ASM)
+            asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(m0)
+                         : "memory", "m0");
+        else
+            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 0, 0);
+    }
+#endif
 }
 
 // 16 bytes at a dword-aligned LDS address as one ds_read_b128 (gfx950 serves
@@ -315,16 +400,18 @@ __device__ __forceinline__ uint64_t hash_string_window(ldsw_t w, uint32_t off, u
         }
         return mix16(u, v, mul);
     }
+    // one read serves both sides of the regime branch (a pass holding long and
+    // short strings runs both): s[n-64, n-32) over 64 bytes, else s[0, 32)
+    // (the back pad covers n < 32)
+    const Q32 h = lds_read32<W128>(w, n > 64 ? off + n - 64 : off);
     if (n > 64) {
-        const Q32 u = lds_read32<W128>(w, off + n - 64);
         Blk b;
-        b.v0 = u64x2{u.q0, u.q1};
-        b.v1 = u64x2{u.q2, u.q3};
+        b.v0 = u64x2{h.q0, h.q1};
+        b.v1 = u64x2{h.q2, h.q3};
         b.v2 = t01;
         b.v3 = t23;
         return city_gt64_lds<W128, (LOOP > 2 ? 2 : LOOP)>(w, off, n, b);
     }
-    const Q32 h = lds_read32<W128>(w, off);  // s[0, 32): the back pad covers n < 32
     const u64x2 h01 = {h.q0, h.q1};
     if (n > 32) return city_33to64(h01, u64x2{h.q2, h.q3}, t01, t23, n);
     if (n > 16) return city_17to32(h01, t23, n);
@@ -362,5 +449,6 @@ __device__ __forceinline__ uint64_t hash_slot_window(ldsw_t w, uint32_t code, ui
     }
     return hash_numeric(code, bits);
 }
+
 
 }  // namespace hdx

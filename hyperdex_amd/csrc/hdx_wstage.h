@@ -86,7 +86,7 @@ struct Group {
 // ADMA: the DMA as inline asm (dma_x4_asm), the code table loaded with the
 // bases and lengths and waited for before the DMA goes out — nothing in
 // phases 2-3 then waits for the DMA.
-template <int NCH, uint32_t WB, int SHAPE, int ORDER = 1, bool ADMA = false>
+template <int NCH, uint32_t WB, int SHAPE, int ORDER = 1, bool ADMA = false, bool DL = false>
 __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint64_t o0, uint8_t* win, uint32_t win_off,
                                                      uint64_t* desc) {
     const int lane = threadIdx.x & 63;
@@ -115,14 +115,11 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
     const uint64_t bnext = has_next ? readlane64(mybase, (int)g.nobj) : 0;
     const uint32_t lead = (uint32_t)((uintptr_t)(args.blob + b0) & 15);
     const uint8_t* s16 = args.blob + b0 - lead;
-    auto dma = [&](uint32_t units) {  // units 16-byte units from s16 -> win (units <= WB / 16)
-        for (uint32_t u0 = 0; u0 < units; u0 += 64) {
-            const uint32_t u = u0 + (uint32_t)lane;
-            if (u < units) {  // lanes past the span write nothing: the window need not be whole KiB
-                if constexpr (ADMA) dma_x4_asm(s16 + 16ull * u, win + 16 * u0);
-                else __builtin_amdgcn_global_load_lds((const void*)(s16 + 16ull * u), (lds_void_t)(win + 16 * u0), 16, 0, 0);
-            }
-        }
+    // units 16-byte units from s16 -> win (units <= WB / 16); lanes past the
+    // span write nothing: the window need not be whole KiB
+    auto dma = [&](uint32_t units) {
+        if constexpr (DL) dma_units16_loop<ADMA>(s16, win, units);
+        else dma_units16<ADMA>(s16, win, units);
     };
     // the span up to the next group's first object, before the lengths are back
     const bool early = has_next && bnext > b0 && lead + (bnext - b0) <= WB;
@@ -206,9 +203,10 @@ __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, 
 // up in the args.T region tables from their coordinates parked in LDS
 // (lookup_tables_wave), coordinates stored only when args.coords is set.
 // GAP: the class straddling the pass boundary moves whole into the second
-// pass when pads allow (class_sort, hdx_regroup.h).
+// pass when pads allow (class_sort, hdx_regroup.h).  DL (debug): round 3's
+// span copy, addresses and predicate per KiB (dma_units16_loop).
 template <int NCH, uint32_t WB, int SHAPE = 0, int HT = 0, int ORDER = 1, int W128 = 0, bool REGIONS = false,
-          bool GAP = false, bool ADMA = false, bool PU = true>
+          bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false>
 __global__ void __launch_bounds__(256)
 hash_wstage_kernel(const BatchArgs args) {
     static_assert(NCH >= 1 && NCH <= 4 && WB % 16 == 0, "slot indices are 8 bits; windows whole DMA units");
@@ -226,7 +224,7 @@ hash_wstage_kernel(const BatchArgs args) {
 
     const uint64_t o0 = ((uint64_t)blockIdx.x * 4 + w) * args.K;
     if (o0 >= args.n) return;  // no barrier anywhere: waves are independent
-    const Group<NCH> g = describe_group<NCH, WB, SHAPE, ORDER, ADMA>(args, o0, win, 0, desc);
+    const Group<NCH> g = describe_group<NCH, WB, SHAPE, ORDER, ADMA, DL>(args, o0, win, 0, desc);
 
     // ---- counting sort by work class (wave-local) --------------------------
     class_sort<NCH, GAP>(cnt, perm, g.cls, g.code, g.ns, wave_lds_fence);
@@ -260,7 +258,7 @@ hash_wstage_kernel(const BatchArgs args) {
 // Launch: K = floor(64 * NCH / A) whole objects per wave (at most 63), four
 // independent waves per 256-thread workgroup, no workgroup barrier.
 template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, int HT = 0, int ORDER = 1, int W128 = 0,
-          bool REGIONS = false, bool GAP = false, bool ADMA = false, bool PU = true>
+          bool REGIONS = false, bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false>
 static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     // lane o holds object o's base and lane K the next group's first: K <= 63
     args.K = std::min<uint32_t>(std::min<uint32_t>((uint32_t)(64 * NCH) / args.A, KCAP), 63u);
@@ -269,7 +267,7 @@ static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA, PU>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA, PU, DL>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
     return hipGetLastError();
 }
 

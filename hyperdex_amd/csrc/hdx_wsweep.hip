@@ -115,13 +115,11 @@ __device__ __forceinline__ void dma4(const void* src, void* dst) {
     if constexpr (ASM) dma_x1_asm(src, dst);
     else __builtin_amdgcn_global_load_lds(src, (lds_void_t)dst, 4, 0, 0);
 }
-template <bool ASM = false>
+template <bool ASM = false, bool DL = false>
 __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint32_t bytes, int lane) {
     const uint32_t units = bytes >> 4;
-    for (uint32_t u0 = 0; u0 < units; u0 += 64) {
-        const uint32_t u = u0 + (uint32_t)lane;
-        if (u < units) dma16<ASM>(src + 16ull * u, dst + 16 * u0);
-    }
+    if constexpr (DL) dma_units16_loop<ASM>(src, dst, units);
+    else dma_units16<ASM>(src, dst, units);
     const uint32_t tdw = ((bytes & 15) + 3) >> 2;
     if ((uint32_t)lane < tdw) dma4<ASM>(src + 16ull * units + 4 * lane, dst + 16 * units);
 }
@@ -141,7 +139,7 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
 // the hash on made-up descriptors (the compute alone); 1 = no hash (a slot's
 // coordinate is its descriptor), 2 = no hash and no walk.
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
-          bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true>
+          bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true, bool DL = false>
 __global__ void __launch_bounds__(256)
 hash_sweep_wstage_kernel(const EncodedArgs a) {
     constexpr uint32_t SL = NCH * 64;
@@ -212,7 +210,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         kspan = keys_in = true;  // kreg 0: the values lie in the same span
         vlead = klead + (uint32_t)(v0 - k0);
         vheld = klead + (uint32_t)(rend - k0);
-        if (SHAPE != 3) copy_span<ASM>(a.keys + k0 - klead, win + kFrontS, vheld, lane);
+        if (SHAPE != 3) copy_span<ASM, DL>(a.keys + k0 - klead, win + kFrontS, vheld, lane);
     } else {
         if (kruns) {
             const uint64_t kend = rl64(koff + klen, (int)nobj - 1);
@@ -220,7 +218,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
             keys_in = kspan;
             if (kspan) {
                 kreg = (klead + (uint32_t)(kend - k0) + 15) & ~15u;
-                if (SHAPE != 3) copy_span<ASM>(a.keys + k0 - klead, win + kFrontS, klead + (uint32_t)(kend - k0), lane);
+                if (SHAPE != 3) copy_span<ASM, DL>(a.keys + k0 - klead, win + kFrontS, klead + (uint32_t)(kend - k0), lane);
             }
         }
         // keys in their own places, as whole 16-byte units: lane o*U + k copies
@@ -266,7 +264,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         }
         const uint64_t vend = has_next ? rl64(voff, (int)nobj) : 0;
         vheld = has_next && vend >= v0 ? (uint32_t)std::min<uint64_t>(vlead + (vend - v0), WB - kreg) : 0u;
-        if (vheld && SHAPE != 3) copy_span<ASM>(a.vals + v0 - vlead, win + kFrontS + kreg, vheld, lane);
+        if (vheld && SHAPE != 3) copy_span<ASM, DL>(a.vals + v0 - vlead, win + kFrontS + kreg, vheld, lane);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the compiler does not order ds_read after LDS DMA
     wave_fence();
@@ -409,14 +407,14 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
 }
 
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
-          bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true>
+          bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true, bool DL = false>
 static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
     const uint32_t K = std::min<uint32_t>(64 * NCH / a.A, KCAP);
     if (K == 0) return hipErrorInvalidValue;
     const uint64_t waves = (a.n + K - 1) / K;
     const uint64_t blocks = (waves + 3) / 4;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU, BF, RECS, KUNITS>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU, BF, RECS, KUNITS, DL>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -465,6 +463,8 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 17: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false>(a, stream);  // without the record span
         case 18: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, false>(a, stream);  // keys in place gathered by dwords (round 3)
         case 19: return launch_wsweep_t<2, 8704, 6, false, true, 3, 13, false, true, true, false>(a, stream);  // debug shape: no copy, no walk, the hash
+        case 20: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, true, true>(a, stream);  // round 3's span copy (per KiB)
+        case 21: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, true, true, true>(a, stream);  // the record form, round 3's span copy
         default: return hipErrorInvalidValue;
     }
 }

@@ -61,6 +61,11 @@ CONFIGS = {
     "u8": [_s(8)] * 17, "u24": [_s(24)] * 17, "u48": [_s(48)] * 17, "u100": [_s(100)] * 17,
     "u150": [_s(150)] * 17, "u190": [_s(190)] * 17,
     "num": [_n(dt.HYPERDATATYPE_INT64)] * 17, "flt": [_n(dt.HYPERDATATYPE_FLOAT)] * 17,
+    # measurement-only: config 3b with its strings capped at 2 / 1 CityHash loop trips
+    "m3b192": ([_s(64)] + [Rule(dt.HYPERDATATYPE_STRING, UNIFORM, 0, 192)] * 10
+               + [_n(dt.HYPERDATATYPE_INT64)] * 3 + [_n(dt.HYPERDATATYPE_FLOAT)] * 3),
+    "m3b128": ([_s(64)] + [Rule(dt.HYPERDATATYPE_STRING, UNIFORM, 0, 128)] * 10
+               + [_n(dt.HYPERDATATYPE_INT64)] * 3 + [_n(dt.HYPERDATATYPE_FLOAT)] * 3),
 }
 
 

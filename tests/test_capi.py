@@ -157,6 +157,13 @@ def test_kernel_names_match_the_built_symbols():
         for n in (1000, 10_000_000):
             _, name = kernel_for(types, n)
             assert name in demangled, (name, sorted(demangled)[:5])
+    # bench.py's config-5 sweep names (both store layouts)
+    import bench
+    mangled = sorted(set(m.decode() for m in re.findall(rb"_ZN3hdx\w+kernel\w+EncodedArgsE", raw)))
+    demangled = set(subprocess.run(["c++filt"], input="\n".join(mangled), capture_output=True,
+                                   text=True).stdout.split("\n"))
+    for layout in ("records", "keycol", "columns"):
+        assert bench.sweep_kernel_name(layout) in demangled, bench.sweep_kernel_name(layout)
 
 
 def test_stream_probe_rejects_bad_sizes():
