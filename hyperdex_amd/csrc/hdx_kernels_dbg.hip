@@ -806,7 +806,7 @@ static bool known_variant(int v) {
         case 251:  // ... and with round 3's dword-by-dword key gather
         case 252:  // debug shape of 250: no copy, no walk, the hash on made-up descriptors (WRONG coordinates)
         case 253: case 254:  // the product sweep's non-record / record forms with round 3's per-KiB span copy
-        case 255:  // 212 with round 3's per-KiB span copy
+        case 255:  // 212 with round 3's per-KiB span copy; the sweep with round 3's walk reads
         case 223: case 224: case 225: case 226: case 227:  // its debug shapes (WRONG coordinates)
         case 210: case 211:  // wave-staged, sorted over the workgroup
         case 40: case 41:

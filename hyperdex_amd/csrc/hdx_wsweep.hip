@@ -73,11 +73,23 @@ __device__ __forceinline__ uint32_t g_be16(const uint8_t* p) {
     const uint16_t v = *(const __attribute__((address_space(1))) u16_u*)p;
     return (uint32_t)(uint16_t)((v >> 8) | (v << 8));
 }
-__device__ __forceinline__ uint32_t w_be32(ldsw_t w, uint32_t o) { return lds_be32(w, o); }
-__device__ __forceinline__ uint64_t w_be64(ldsw_t w, uint32_t o) {
-    return ((uint64_t)lds_be32(w, o) << 32) | lds_be32(w, o + 4);
+// The walk's big-endian reads at any byte offset: one misaligned ds_read_b32
+// each (gfx950 serves them, replaying the misaligned part; the walk runs on
+// 6 of 64 lanes, where that costs little, and saves the dword pair's address
+// and v_alignbyte — the hash's 64-lane reads keep the aligned form).  DW: the
+// dword pair + v_alignbyte (round 3; debug SHAPE 4).
+typedef const __attribute__((address_space(3))) uint32_t __attribute__((aligned(1))) lds_ua32_t;
+template <bool DW = false>
+__device__ __forceinline__ uint32_t w_be32(ldsw_t w, uint32_t o) {
+    if constexpr (DW) return lds_be32(w, o);
+    else return __builtin_bswap32(*(lds_ua32_t*)((const __attribute__((address_space(3))) uint8_t*)w + o));
 }
-__device__ __forceinline__ uint32_t w_be16(ldsw_t w, uint32_t o) { return lds_be32(w, o) >> 16; }
+template <bool DW = false>
+__device__ __forceinline__ uint64_t w_be64(ldsw_t w, uint32_t o) {
+    return ((uint64_t)w_be32<DW>(w, o) << 32) | w_be32<DW>(w, o + 4);
+}
+template <bool DW = false>
+__device__ __forceinline__ uint32_t w_be16(ldsw_t w, uint32_t o) { return w_be32<DW>(w, o) >> 16; }
 
 // Sort classes: class 7 = hashed from global memory; > 64-byte strings with
 // 3+ blocks share class 6; otherwise work_class<1>'s order (numerics and
@@ -137,7 +149,8 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
 // LOOP: hash_slot_window's; + 10: with TNUM.
 // SHAPE (debug forms 7 / 8 / 19, WRONG coordinates): 3 = no copy and no walk,
 // the hash on made-up descriptors (the compute alone); 1 = no hash (a slot's
-// coordinate is its descriptor), 2 = no hash and no walk.
+// coordinate is its descriptor), 2 = no hash and no walk.  SHAPE 4 (debug
+// form 22, correct coordinates): the walk's reads as round 3's dword pairs.
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
           bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true, bool DL = false>
 __global__ void __launch_bounds__(256)
@@ -314,17 +327,17 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
             // WB >= vlen: no wrap, and a clamped one still fails).  Steps past
             // a failure read garbage (or 0 past the LDS allocation) and their
             // descriptors are reset below.
-            version = w_be64(lw, vw);
-            ok = vlen >= 10 && w_be16(lw, vw + 8) == A - 1;
+            version = w_be64<SHAPE == 4>(lw, vw);
+            ok = vlen >= 10 && w_be16<SHAPE == 4>(lw, vw + 8) == A - 1;
             uint32_t pos = 10;
             uint64_t* dp = desc + lane * A + 1;
-            if (SHAPE >= 2) {  // debug shapes: no walk (descriptors of assorted lengths at the value's start)
+            if (SHAPE == 2 || SHAPE == 3) {  // debug shapes: no walk (descriptors of assorted lengths at the value's start)
                 for (uint32_t k = 0; k + 1 < A; ++k) dp[k] = (uint64_t)(vw + 14) | ((uint64_t)((k * 37) & 127) << 32);
                 pos = vlen;
             } else
 #pragma unroll 4
             for (uint32_t k = 0; k + 1 < A; ++k) {
-                const uint32_t len = std::min(w_be32(lw, vw + pos), WB);
+                const uint32_t len = std::min(w_be32<SHAPE == 4>(lw, vw + pos), WB);
                 dp[k] = (uint64_t)(vw + pos + 4) | ((uint64_t)len << 32);
                 pos += 4 + len;
             }
@@ -465,6 +478,7 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 19: return launch_wsweep_t<2, 8704, 6, false, true, 3, 13, false, true, true, false>(a, stream);  // debug shape: no copy, no walk, the hash
         case 20: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, true, true>(a, stream);  // round 3's span copy (per KiB)
         case 21: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, true, true, true>(a, stream);  // the record form, round 3's span copy
+        case 22: return launch_wsweep_t<2, 8704, 6, false, true, 4, 13, false, true, true, false>(a, stream);  // the walk's reads as dword pairs + v_alignbyte (round 3)
         default: return hipErrorInvalidValue;
     }
 }
