@@ -30,89 +30,12 @@
 #include <thread>
 #include <vector>
 
+#include "hdx_cuts.h"
 #include "hdx_host.h"
 
 namespace hdx {
 
-// ---- byte-balanced cuts (hyperdex_amd/dist.py:shard_ranges) ----------------
-//
-// Object sizes are the sums of their attribute lengths.  Every prefix is an
-// exact integer (< 2^53), so comparing it as a double against
-// total * k / world reproduces numpy's float64 searchsorted(side="left")
-// bit for bit.  The prefix at any object is a block prefix plus a scan of
-// at most one block, so the lengths are read once (in parallel by the
-// device workers when there are any) plus one block per cut.
-static constexpr uint64_t kCutBlock = 1ull << 16;  // objects per prefix block
-
-static uint64_t object_bytes(const uint32_t* attr_len, uint32_t A, uint64_t i) {
-    uint64_t s = 0;
-    const uint32_t* l = attr_len + i * A;
-    for (uint32_t j = 0; j < A; ++j) s += l[j];
-    return s;
-}
-
-static uint64_t block_bytes(const uint32_t* attr_len, uint32_t A, uint64_t n, uint64_t b) {
-    const uint64_t lo = b * kCutBlock, hi = std::min(n, lo + kCutBlock);
-    uint64_t s = 0;
-    for (uint64_t i = lo; i < hi; ++i) s += object_bytes(attr_len, A, i);
-    return s;
-}
-
-// bprefix[b] = bytes of objects [0, b * kCutBlock), b in [0, blocks]
-struct Prefix {
-    const uint32_t* attr_len;
-    uint32_t A;
-    uint64_t n;
-    std::vector<uint64_t> bprefix;
-    uint64_t at(uint64_t i) const {  // bytes of objects [0, i)
-        const uint64_t b = i / kCutBlock;
-        uint64_t s = bprefix[b];
-        for (uint64_t k = b * kCutBlock; k < i; ++k) s += object_bytes(attr_len, A, k);
-        return s;
-    }
-    // first i in [0, n] with prefix(i) >= target (numpy searchsorted, side="left")
-    uint64_t search(double target) const {
-        const uint64_t blocks = bprefix.size() - 1;
-        uint64_t lo = 0, hi = blocks;  // last block b with (double)bprefix[b] < target
-        if (!((double)bprefix[0] < target)) return 0;
-        while (lo < hi) {
-            const uint64_t mid = (lo + hi + 1) / 2;
-            if ((double)bprefix[mid] < target) lo = mid; else hi = mid - 1;
-        }
-        uint64_t i = lo * kCutBlock, s = bprefix[lo];
-        while (i < n && (double)s < target) s += object_bytes(attr_len, A, i++);
-        return (double)s < target ? n : i;
-    }
-};
-
-static void cuts_from_prefix(const Prefix& p, uint32_t world, double tol, uint64_t* first) {
-    const uint64_t n = p.n;
-    std::vector<uint64_t> even(world + 1);
-    for (uint32_t k = 0; k <= world; ++k) even[k] = (uint64_t)((unsigned __int128)n * k / world);
-    const uint64_t total = p.bprefix.back();
-    if (tol > 0) {  // dist._within: every equal-count shard within tol of the mean share
-        bool ok = true;
-        if (total > 0) {
-            const double share = (double)total / world;
-            uint64_t a = 0;
-            for (uint32_t k = 1; k <= world && ok; ++k) {
-                const uint64_t b = p.at(even[k]);
-                ok = std::abs((double)(b - a) - share) <= tol * share;
-                a = b;
-            }
-        }
-        if (ok) {
-            std::memcpy(first, even.data(), (world + 1) * sizeof(uint64_t));
-            return;
-        }
-    }
-    first[0] = 0;
-    for (uint32_t k = 1; k < world; ++k) {
-        const uint64_t c = p.search((double)total * k / world);
-        first[k] = std::min(std::max(c, first[k - 1]), n);
-    }
-    first[world] = n;
-}
+// ---- byte-balanced cuts: hdx_cuts.h ------------------------------------------
 
 // ---- worker threads ---------------------------------------------------------
 
@@ -333,15 +256,7 @@ HDX_EXPORT hdx_status hdx_shard_ranges(const uint32_t* attr_len, uint32_t attrs_
     if (!first || world == 0) return fail(HDX_E_INVALID, "first is NULL or world == 0");
     if (attr_len && (attrs_sz == 0 || attrs_sz > HDX_MAX_ATTRS))
         return fail(HDX_E_INVALID, "attrs_sz=%u outside [1, %d]", attrs_sz, HDX_MAX_ATTRS);
-    if (!attr_len) {  // no sizes: counts differ by at most one
-        for (uint32_t k = 0; k <= world; ++k) first[k] = (uint64_t)((unsigned __int128)n * k / world);
-        return HDX_OK;
-    }
-    Prefix p{attr_len, attrs_sz, n, {}};
-    const uint64_t blocks = (n + kCutBlock - 1) / kCutBlock;
-    p.bprefix.assign(blocks + 1, 0);
-    for (uint64_t b = 0; b < blocks; ++b) p.bprefix[b + 1] = p.bprefix[b] + block_bytes(attr_len, attrs_sz, n, b);
-    cuts_from_prefix(p, world, equal_count_tol, first);
+    shard_cuts(attr_len, attrs_sz, n, world, equal_count_tol, first);  // no sizes: counts differ by at most one
     return HDX_OK;
 }
 
