@@ -99,49 +99,11 @@ struct hdx_region_table_s {
     std::vector<uint64_t> h_lower, h_upper, h_ids, h_index;
 };
 
-// configuration::lookup_region (common/configuration.cc:698-735) on the host:
-// the first region whose box holds hs[attrs[d]] on every dimension (bounds
-// inclusive), else 0 (region_id()).  Through the table's interval index when
-// it has one (hdx_region_lookup.h's lookup_indexed_fn, host form: per
-// dimension the top byte's bucket, a binary search, the interval's mask; the
-// lowest bit of the masks' AND), else the reference's scan.
+// configuration::lookup_region (common/configuration.cc:698-735) on the host
+// (hdx_region_index.h): through the table's interval index when it has one,
+// else the reference's scan.
 inline uint64_t region_lookup_host(const hdx_region_table_s* t, const uint64_t* hs) {
-    if (!t->h_index.empty()) {
-        const uint64_t* idx = t->h_index.data();
-        uint64_t acc[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-        for (uint32_t d = 0; d < t->D; ++d) {
-            const uint64_t hdr = idx[d];
-            const uint64_t* B = idx + ((hdr >> 16) & 0xffffff);
-            const uint64_t hv = hs[t->attrs[d]];
-            const uint16_t* start = reinterpret_cast<const uint16_t*>(B - 65 /* kIndexBucketWords */);
-            const uint32_t b = (uint32_t)(hv >> 56);
-            uint32_t pos = start[b], cnt = start[b + 1] - pos;
-            while (cnt) {
-                const uint32_t half = cnt >> 1;
-                if (B[pos + half] <= hv) {
-                    pos += half + 1;
-                    cnt -= half + 1;
-                } else {
-                    cnt = half;
-                }
-            }
-            const uint64_t* mask = idx + (hdr >> 40) + (size_t)pos * t->W;
-            for (uint32_t w = 0; w < t->W; ++w) acc[w] &= mask[w];
-        }
-        for (uint32_t w = 0; w < t->W; ++w)
-            if (acc[w]) return t->h_ids[64 * w + __builtin_ctzll(acc[w])];
-        return 0;
-    }
-    for (uint32_t r = 0; r < t->R; ++r) {
-        const uint64_t* lo = t->h_lower.data() + (size_t)r * t->D;
-        const uint64_t* up = t->h_upper.data() + (size_t)r * t->D;
-        bool in = true;
-        for (uint32_t d = 0; in && d < t->D; ++d) {
-            const uint64_t h = hs[t->attrs[d]];
-            in = lo[d] <= h && h <= up[d];
-        }
-        if (in) return t->h_ids[r];
-    }
-    return 0;
+    return hdx::region_lookup_arrays(t->D, t->R, t->W, t->attrs, t->h_lower.data(), t->h_upper.data(), t->h_ids.data(),
+                                     t->h_index.empty() ? nullptr : t->h_index.data(), hs);
 }
 

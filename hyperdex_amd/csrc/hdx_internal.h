@@ -9,6 +9,7 @@
 
 #include "../../include/hdxhash.h"
 #include "hdx_host_common.h"
+#include "hdx_region_index.h"
 
 namespace hdx {
 
@@ -142,10 +143,7 @@ struct MultiRegionArgs {
 
 hipError_t launch_lookup_regions_multi(const MultiRegionArgs& a, hipStream_t stream);
 
-// Host: the interval index of a region table (empty when R > kIndexMaxRegions).
-constexpr uint32_t kIndexMaxRegions = 256;
-void region_index_build(uint32_t D, uint32_t R, const uint64_t* lower, const uint64_t* upper,
-                        std::vector<uint64_t>& index, uint32_t& W);
+// Host: the interval index of a region table, hdx_region_index.h.
 
 // Stored-object sweep (hdx_encoded.hip): device arrays.  T region tables
 // (hdx_hash_encoded_regions_device): table t's region id of object i goes to

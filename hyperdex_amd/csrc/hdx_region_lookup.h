@@ -7,13 +7,9 @@
 #include <stdint.h>
 
 #include "hdx_internal.h"
+#include "hdx_region_index.h"
 
 namespace hdx {
-
-constexpr uint32_t kMaxLookupDims = 16;
-// u64 words of a dimension's 257 u16 bucket starts (region_index_build),
-// stored just below its boundaries
-constexpr uint32_t kIndexBucketWords = 65;
 
 // Region id of coordinates hd(0..D) through the interval index idx (hd reads
 // one coordinate, so a caller holding them in LDS need not copy them out).

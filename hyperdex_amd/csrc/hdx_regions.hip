@@ -24,60 +24,7 @@
 
 namespace hdx {
 
-// ---------------------------------------------------------------------------
-// Interval index.  For every subspace dimension d the table's box edges
-// (lower[r][d] and upper[r][d] + 1) cut the u64 line into at most 2R+1
-// intervals, and every point of one interval lies in the same set of the
-// table's boxes on that dimension — a bit mask over the regions.  The first
-// region (in table order) whose box holds the coordinates is then the lowest
-// set bit of the AND of the D masks of the coordinates' intervals: exactly the
-// reference's first-match scan (configuration.cc:698-735), overlapping or
-// empty boxes included, at D binary searches instead of up to R*D compares.
-// Layout, u64 words: D headers (m | boundaries offset << 16 | masks offset
-// << 40), then per dimension: kIndexBucketWords words of u16 bucket starts
-// (start[b] = boundaries <= b << 56, b = 0..256, so a coordinate whose top
-// byte is b has its interval in [start[b], start[b + 1]]: the search is over
-// that range only — zero or one step for the reference's equal partitions),
-// its m sorted boundaries, and (m + 1) * W mask words.
-// ---------------------------------------------------------------------------
-void region_index_build(uint32_t D, uint32_t R, const uint64_t* lower, const uint64_t* upper,
-                        std::vector<uint64_t>& index, uint32_t& W) {
-    index.clear();
-    W = 0;
-    if (R == 0 || R > kIndexMaxRegions || D == 0 || D > kMaxLookupDims) return;
-    W = (R + 63) / 64;
-    index.assign(D, 0);
-    std::vector<uint64_t> pts;
-    for (uint32_t d = 0; d < D; ++d) {
-        pts.clear();
-        for (uint32_t r = 0; r < R; ++r) {
-            pts.push_back(lower[(size_t)r * D + d]);
-            if (upper[(size_t)r * D + d] != UINT64_MAX) pts.push_back(upper[(size_t)r * D + d] + 1);
-        }
-        std::sort(pts.begin(), pts.end());
-        pts.erase(std::unique(pts.begin(), pts.end()), pts.end());
-        const uint64_t m = pts.size();
-        uint16_t start[kIndexBucketWords * 4] = {};
-        for (uint32_t b = 0; b <= 256; ++b)
-            start[b] = (uint16_t)(b == 256 ? m
-                                           : std::upper_bound(pts.begin(), pts.end(), (uint64_t)b << 56) - pts.begin());
-        const size_t soff = index.size();
-        index.resize(soff + kIndexBucketWords);
-        std::memcpy(&index[soff], start, sizeof start);
-        const uint64_t boff = index.size();
-        index.insert(index.end(), pts.begin(), pts.end());
-        const uint64_t moff = index.size();
-        for (uint64_t i = 0; i <= m; ++i) {
-            const uint64_t x = i == 0 ? 0 : pts[i - 1];  // a point of interval i (interval 0 may be empty)
-            uint64_t mask[kIndexMaxRegions / 64] = {0, 0, 0, 0};
-            for (uint32_t r = 0; r < R; ++r)
-                if (lower[(size_t)r * D + d] <= x && x <= upper[(size_t)r * D + d]) mask[r >> 6] |= 1ull << (r & 63);
-            index.insert(index.end(), mask, mask + W);
-        }
-        index[d] = m | (boff << 16) | (moff << 40);
-    }
-}
-
+// The interval index (region_index_build) is built on the host: hdx_region_index.h.
 
 template <bool IN_LDS, bool INDEX = false>
 __global__ void __launch_bounds__(256)

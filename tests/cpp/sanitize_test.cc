@@ -6,7 +6,10 @@
 //     a read past a value's end is a reported error, against the oracle
 //     (oracle/hdx_oracle.c, test infrastructure);
 //   * the device set's byte-balanced cuts (hdx_cuts.h) against a direct
-//     restatement of dist.shard_ranges' rule.
+//     restatement of dist.shard_ranges' rule;
+//   * the region tables' interval index and host lookup (hdx_region_index.h,
+//     the batcher's calling-thread path) against the oracle's lookup_region,
+//     index and scan, with every table array in an exact-size buffer.
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -19,6 +22,7 @@
 
 #include "hdx_cuts.h"
 #include "hdx_host_common.h"
+#include "hdx_region_index.h"
 
 extern "C" {
 #include "hdx_oracle.h"
@@ -149,6 +153,65 @@ int main() {
         for (uint32_t k = 0; k <= world; ++k)
             CHECK(first[k] == want[k], "cuts rep %d (n %llu A %u world %u tol %g) k %u: %llu vs %llu", rep,
                   (unsigned long long)n, A, world, tol, k, (unsigned long long)first[k], (unsigned long long)want[k]);
+    }
+    // region tables: equal partitions (the reference's), random overlapping
+    // and empty boxes, full-range bounds; coordinates at and beside every edge
+    for (int rep = 0; rep < 300; ++rep) {
+        const uint32_t D = 1 + (uint32_t)(g() % 4), A = D + (uint32_t)(g() % 5);
+        const uint32_t R = rep % 10 == 0 ? 300 + (uint32_t)(g() % 40) : 1 + (uint32_t)(g() % 256);
+        std::unique_ptr<uint64_t[]> lower(new uint64_t[(size_t)R * D]), upper(new uint64_t[(size_t)R * D]),
+            ids(new uint64_t[R]);
+        std::unique_ptr<uint16_t[]> attrs(new uint16_t[D]);
+        for (uint32_t d = 0; d < D; ++d) attrs[d] = (uint16_t)((d * 7 + rep) % A);
+        const int kind = rep % 3;
+        for (uint32_t r = 0; r < R; ++r) {
+            ids[r] = 1000 + r;
+            for (uint32_t d = 0; d < D; ++d) {
+                uint64_t lo, up;
+                if (kind == 0) {  // equal partitions of the first dimension, others full
+                    lo = d == 0 ? (uint64_t)(((unsigned __int128)r << 64) / R) : 0;
+                    up = d == 0 ? (r + 1 == R ? UINT64_MAX : (uint64_t)(((unsigned __int128)(r + 1) << 64) / R) - 1)
+                                : UINT64_MAX;
+                } else {
+                    uint64_t a = g(), b = g();
+                    if (kind == 2) { a >>= 56; b >>= 56; a <<= 56; b <<= 56; }  // edges on bucket boundaries
+                    lo = std::min(a, b);
+                    up = std::max(a, b);
+                    if (g() % 16 == 0) std::swap(lo, up);  // an empty box
+                    if (g() % 16 == 0) up = UINT64_MAX;
+                }
+                lower[(size_t)r * D + d] = lo;
+                upper[(size_t)r * D + d] = up;
+            }
+        }
+        std::vector<uint64_t> index;
+        uint32_t W = 0;
+        hdx::region_index_build(D, R, lower.get(), upper.get(), index, W);
+        CHECK((R <= hdx::kIndexMaxRegions) == !index.empty(), "index presence R %u", R);
+        std::unique_ptr<uint64_t[]> idx(new uint64_t[index.size() ? index.size() : 1]);
+        if (!index.empty()) std::memcpy(idx.get(), index.data(), index.size() * 8);
+        const uint64_t n = 2000;
+        std::unique_ptr<uint64_t[]> hs(new uint64_t[n * A]), want(new uint64_t[n]);
+        for (uint64_t i = 0; i < n * A; ++i) {
+            const uint64_t e = lower[(g() % R) * D + g() % D];
+            switch (g() % 4) {
+                case 0: hs[i] = g(); break;
+                case 1: hs[i] = e; break;
+                case 2: hs[i] = e - 1; break;
+                default: hs[i] = upper[(g() % R) * D + g() % D] + (g() % 2); break;
+            }
+        }
+        hdxo_lookup_region(D, R, attrs.get(), lower.get(), upper.get(), ids.get(), hs.get(), A, n, want.get());
+        for (uint64_t i = 0; i < n; ++i) {
+            const uint64_t* row = hs.get() + i * A;
+            const uint64_t a = hdx::region_lookup_arrays(D, R, W, attrs.get(), lower.get(), upper.get(), ids.get(),
+                                                         index.empty() ? nullptr : idx.get(), row);
+            const uint64_t b = hdx::region_lookup_arrays(D, R, W, attrs.get(), lower.get(), upper.get(), ids.get(),
+                                                         nullptr, row);
+            CHECK(a == want[i] && b == want[i], "regions rep %d (D %u R %u kind %d) object %llu: %llu / %llu vs %llu",
+                  rep, D, R, kind, (unsigned long long)i, (unsigned long long)a, (unsigned long long)b,
+                  (unsigned long long)want[i]);
+        }
     }
     if (failures) {
         fprintf(stderr, "%d failures\n", failures);
