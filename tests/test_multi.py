@@ -187,9 +187,9 @@ def test_cpp_daemon_uses_every_device():
     assert "multi ok" in r.stdout, r.stdout
 
 
-# ---- world 2 and 3 on one GPU (debug library: a device set listing device 0 repeatedly) ----
+# ---- world 2, 3 and 8 on one GPU (debug library: a device set listing device 0 repeatedly) ----
 
-@pytest.fixture(params=[2, 3])
+@pytest.fixture(params=[2, 3, 8])
 def repeated_set(request):
     """hdxdbg_init_devices([0] * world): `world` workers and streams on device 0,
     so the multi-device cuts, the per-device workers and the shard plumbing
