@@ -1080,6 +1080,41 @@ def cgroup_cpu_quota():
         return None
 
 
+def verify_encoded_spread(types, enc, coords, oracle, sample=2048, seed=5):
+    """The sweep's coordinates of objects spread over the whole store (the last
+    64 and `sample` random ones) against the oracle, each object's key and
+    value bytes copied to the host on their own; returns the count checked."""
+    keys, key_off, key_len, vals, val_off, val_len = enc
+    n = val_off.numel()
+    if n == 0:
+        return 0
+    rng = np.random.default_rng(seed)
+    idx = np.unique(np.concatenate([rng.integers(0, n, min(sample, n)), np.arange(max(0, n - 64), n)]))
+    it = torch_index(idx, key_off.device)
+    ko = key_off[it].cpu().numpy().view(np.uint64)
+    kl = key_len[it].cpu().numpy().view(np.uint32)
+    vo = val_off[it].cpu().numpy().view(np.uint64)
+    vl = val_len[it].cpu().numpy().view(np.uint32)
+    kparts, vparts = [], []
+    for i in range(len(idx)):
+        kparts.append(keys[int(ko[i]):int(ko[i]) + int(kl[i])].cpu().numpy())
+        vparts.append(vals[int(vo[i]):int(vo[i]) + int(vl[i])].cpu().numpy())
+    nko = np.concatenate([[0], np.cumsum(kl.astype(np.uint64))[:-1]]).astype(np.uint64)
+    nvo = np.concatenate([[0], np.cumsum(vl.astype(np.uint64))[:-1]]).astype(np.uint64)
+    hk = np.concatenate(kparts) if kparts else np.zeros(0, np.uint8)
+    hv = np.concatenate(vparts) if vparts else np.zeros(0, np.uint8)
+    want, _, bad = oracle.hash_encoded(types, hk, nko, kl, hv, nvo, vl)
+    got = coords[it].cpu().numpy().view(np.uint64)
+    if bad.any() or not np.array_equal(got, want):
+        raise SystemExit("cpu_baseline: GPU coordinates of objects spread over the store differ from the oracle")
+    return len(idx)
+
+
+def torch_index(idx, device):
+    import torch
+    return torch.from_numpy(idx.astype(np.int64)).to(device)
+
+
 def cpu_baseline_encoded(types, enc, A, seconds, coords):
     """Config 5 CPU baseline: the oracle's decode_value + hash on the same
     cores as cpu_baseline (one oracle call per thread over its own chunk of a
@@ -1109,6 +1144,7 @@ def cpu_baseline_encoded(types, enc, A, seconds, coords):
         bad = np.concatenate([p[2] for p in parts])
         if bad.any() or not np.array_equal(coords[:ns].cpu().numpy().view(np.uint64), want):
             raise SystemExit("cpu_baseline: GPU coordinates differ from the oracle")
+        spread = verify_encoded_spread(types, enc, coords, oracle)
         nbytes = int(kl.sum()) + int(vl.sum())
         reps, t0 = 0, time.perf_counter()
         while True:
@@ -1120,7 +1156,8 @@ def cpu_baseline_encoded(types, enc, A, seconds, coords):
     return {"value": round(reps * nbytes / dt / 2**30, 3), "unit": "GiB/s", "cores": len(chunks),
             "kind": "port", "mobjects_per_s": round(reps * ns / dt / 1e6, 3),
             "sample": "%d stored objects (%.0f MB), %d passes, oracle hdxo_hash_encoded -O2, %d threads; "
-                      "verified equal to the GPU coords" % (ns, nbytes / 1e6, reps, len(chunks)),
+                      "verified equal to the GPU coords, and %d objects spread over the whole store (the last "
+                      "64 and random ones)" % (ns, nbytes / 1e6, reps, len(chunks), spread),
             **host_info(len(chunks), quota)}
 
 
