@@ -141,11 +141,11 @@ __device__ __forceinline__ void vm_wait_le(uint32_t n) {
 // batch is fixed and the kernel waits for its own with counted vm_wait_le.
 __device__ __forceinline__ void dma_x4(const void* src, const void* dst) {
     const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t)dst);
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
 }
 __device__ __forceinline__ void dma_x1(const void* src, const void* dst) {
     const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_void_t)dst);
-    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+    asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
 }
 
 }  // namespace
