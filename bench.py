@@ -870,15 +870,24 @@ def latest_traffic_file():
     return files[-1] if files else ""
 
 
+def product_sources():
+    """The product library's sources: SRCS and HDRS of hyperdex_amd/csrc/Makefile
+    (the debug library's extra kernels are not part of what the PMC counters
+    measured, so editing them leaves the digest alone)."""
+    names = []
+    for line in open(os.path.join(ROOT, "hyperdex_amd", "csrc", "Makefile")):
+        if line.startswith(("SRCS :=", "HDRS :=")):
+            names += line.split(":=", 1)[1].split()
+    return sorted(os.path.normpath(os.path.join(ROOT, "hyperdex_amd", "csrc", f)) for f in names)
+
+
 def source_digest():
-    """sha256 over the kernel and C-ABI sources (what the PMC counters measured):
-    a traffic.json recorded from other sources is not this build's traffic."""
-    import glob
+    """sha256 over the product's kernel and C-ABI sources (what the PMC counters
+    measured): a traffic.json recorded from other sources is not this build's
+    traffic."""
     import hashlib
     h = hashlib.sha256()
-    pats = ("hyperdex_amd/csrc/*.hip", "hyperdex_amd/csrc/*.h", "hyperdex_amd/csrc/*.cpp",
-            "hyperdex_amd/csrc/Makefile", "include/*.h")
-    for f in sorted(p for pat in pats for p in glob.glob(os.path.join(ROOT, pat))):
+    for f in product_sources():
         h.update(os.path.relpath(f, ROOT).encode())
         h.update(open(f, "rb").read())
     return h.hexdigest()[:16]

@@ -25,7 +25,7 @@ HDX_E_DEVICE = 3
 HDX_E_INVALID = 4
 HDX_E_NOMEM = 5
 HDX_E_BADENC = 6
-HDX_MAX_ATTRS = 256
+HDX_MAX_ATTRS = 65535
 
 STATUS_NAMES = {
     HDX_OK: "HDX_OK", HDX_E_BADTYPE: "HDX_E_BADTYPE", HDX_E_BADSIZE: "HDX_E_BADSIZE",
@@ -48,6 +48,12 @@ class Shard(ctypes.Structure):
                 ("status_dev", _vp)]
 
 
+class RegionShard(ctypes.Structure):
+    """struct hdx_region_shard (include/hdxhash.h): one device's shard, region-id form."""
+    _fields_ = [("blob", _vp), ("obj_base", _vp), ("attr_len", _vp), ("n", _u64), ("region_ids", _vp),
+                ("coords", _vp), ("status_dev", _vp)]
+
+
 SIGNATURES = [
     ("hdx_abi_version", _i32, []),
     ("hdx_version", _cp, []),
@@ -57,6 +63,12 @@ SIGNATURES = [
     ("hdx_device_set", _i32, [_vp, _i32]),
     ("hdx_shard_ranges", _i32, [_vp, _u32, _u64, _u32, ctypes.c_double, _vp]),
     ("hdx_hash_batch_device_multi", _i32, [_vp, _u32, ctypes.POINTER(Shard), _u32, _i32]),
+    ("hdx_hash_batch_regions_device_multi", _i32, [_vp, _u32, ctypes.POINTER(RegionShard), _u32, _vp, _u32,
+                                                   _i32]),
+    ("hdx_hash_batch_regions_host", _i32, [_vp, _u32, _vp, _u64, _vp, _vp, _u64, _vp, _u32, _vp, _vp]),
+    ("hdx_hash_encoded_host", _i32, [_vp, _u32, _vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp, _u64, _vp, _vp]),
+    ("hdx_hash_encoded_regions_host", _i32, [_vp, _u32, _vp, _u64, _vp, _vp, _vp, _u64, _vp, _vp, _u64, _vp,
+                                             _u32, _vp, _vp, _vp]),
     ("hdx_device_count", _i32, []),
     ("hdx_last_error", _cp, []),
     ("hdx_sync", _i32, [_vp]),

@@ -101,8 +101,9 @@ struct Slot {
 struct hdx_batcher_s {
     int device = -1;
     uint32_t A = 0;
-    uint8_t codes[HDX_MAX_ATTRS];
-    uint32_t types[HDX_MAX_ATTRS];
+    std::vector<uint8_t> codes;
+    std::vector<uint32_t> types;
+    const uint8_t* codes_dev = nullptr;  // A > 128: the wide kernels' device copy (set_codes)
     uint64_t host_max_bytes = 0;  // 0 with HDX_BATCHER_DEVICE_ONLY
     uint32_t max_obj = 0;
     uint64_t max_bytes = 0;
@@ -228,7 +229,8 @@ hipError_t ship(hdx_batcher_s* b, Slot& s) {
     a.status = s.d_status;
     a.n = n;
     a.A = b->A;
-    std::memcpy(a.codes, b->codes, b->A);
+    std::memcpy(a.codes, b->codes.data(), std::min(b->A, kKernargCodes));
+    a.codes_dev = b->codes_dev;
     finalize_args(a);
     const size_t region_base = (size_t)s.cap_obj * b->A;
     if (!b->tables.empty() && b->tables.size() <= kMaxSweepTables && b->A <= 128) {
@@ -410,8 +412,8 @@ HDX_EXPORT hdx_status hdx_batcher_create(const uint32_t* types, uint32_t attrs_s
     *out = nullptr;
     hdx_batcher_config c{};
     if (cfg) c = *cfg;
-    uint8_t codes[HDX_MAX_ATTRS];
-    hdx_status st = check_schema(types, attrs_sz, codes);
+    std::vector<uint8_t> codes(attrs_sz ? attrs_sz : 1);
+    hdx_status st = check_schema(types, attrs_sz, codes.data());
     if (st != HDX_OK) return st;
     if (c.ntables > 16) return fail(HDX_E_INVALID, "ntables=%u > 16", c.ntables);
     if (c.ntables && !c.tables) return fail(HDX_E_INVALID, "tables is NULL");
@@ -421,12 +423,20 @@ HDX_EXPORT hdx_status hdx_batcher_create(const uint32_t* types, uint32_t attrs_s
     auto* b = new hdx_batcher_s();
     b->device = dev;
     b->A = attrs_sz;
-    std::memcpy(b->codes, codes, attrs_sz);
+    b->codes.assign(codes.begin(), codes.begin() + attrs_sz);
+    {
+        BatchArgs tmp{};
+        if ((st = set_codes(tmp, codes.data(), attrs_sz)) != HDX_OK) {
+            delete b;
+            return st;
+        }
+        b->codes_dev = tmp.codes_dev;
+    }
     b->max_obj = c.max_objects ? c.max_objects : 4096;
     b->max_bytes = c.max_bytes ? c.max_bytes : (8ull << 20);
     b->delay = std::chrono::microseconds(c.max_delay_us ? c.max_delay_us : 50);
     b->stage_device = (c.flags & HDX_BATCHER_STAGE_DEVICE) != 0;
-    std::memcpy(b->types, types, attrs_sz * sizeof(uint32_t));
+    b->types.assign(types, types + attrs_sz);
     b->host_max_bytes = (c.flags & HDX_BATCHER_DEVICE_ONLY) ? 0 : c.host_max_bytes ? c.host_max_bytes : UINT64_MAX;
     const uint32_t nslots = c.slots ? std::max(c.slots, 2u) : 4;
     for (uint32_t t = 0; t < c.ntables; ++t) {
@@ -535,7 +545,7 @@ HDX_EXPORT hdx_status hdx_batcher_hash_object(hdx_batcher b, const uint8_t* key,
     }
     if (b->host_max_bytes && total <= b->host_max_bytes) {
         // the calling thread: the per-object CPU path and host lookups
-        hdx_status st = hdx_hash_object(b->types, b->A, key, key_len, values, value_lens, hs);
+        hdx_status st = hdx_hash_object(b->types.data(), b->A, key, key_len, values, value_lens, hs);
         if (st != HDX_OK) return st;
         if (region_ids)
             for (size_t t = 0; t < b->tables.size(); ++t) region_ids[t] = region_lookup_host(b->tables[t], hs);

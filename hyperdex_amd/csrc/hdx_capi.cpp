@@ -11,6 +11,8 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <functional>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -40,7 +42,7 @@ hdx_status fail(hdx_status s, const char* fmt, ...) {
 }
 
 hdx_status hip_fail(hipError_t e, const char* what) {
-    return fail(HDX_E_DEVICE, "%s: %s", what, hipGetErrorString(e));
+    return fail(e == hipErrorOutOfMemory ? HDX_E_NOMEM : HDX_E_DEVICE, "%s: %s", what, hipGetErrorString(e));
 }
 
 
@@ -56,6 +58,45 @@ hdx_status check_schema(const uint32_t* types, uint32_t A, uint8_t* codes_out) {
         if (codes_out) codes_out[j] = (uint8_t)c;
     }
     return HDX_OK;
+}
+
+// Attribute classes in device memory for the wide kernels (A > 128,
+// hdx_wide.hip): one copy per (device, schema), kept for the process's life
+// (a few bytes per attribute; an asynchronous launch may still read it when
+// hdx_shutdown runs).  On the calling thread's current device.
+static hdx_status device_codes(const uint8_t* codes, uint32_t A, const uint8_t** out) {
+    static std::mutex mu;
+    static std::map<std::pair<int, std::string>, uint8_t*>* cache = new std::map<std::pair<int, std::string>, uint8_t*>();
+    int dev = -1;
+    HIP_TRY(hipGetDevice(&dev));
+    std::pair<int, std::string> key(dev, std::string((const char*)codes, A));
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache->find(key);
+    if (it != cache->end()) {
+        *out = it->second;
+        return HDX_OK;
+    }
+    uint8_t* d = nullptr;
+    if (hipMalloc((void**)&d, A) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(HDX_E_NOMEM, "hipMalloc(%u) for the attribute classes", A);
+    }
+    HIP_TRY(hipMemcpy(d, codes, A, hipMemcpyHostToDevice));
+    (*cache)[key] = d;
+    *out = d;
+    return HDX_OK;
+}
+
+hdx_status set_codes(BatchArgs& args, const uint8_t* codes, uint32_t A) {
+    std::memcpy(args.codes, codes, std::min(A, kKernargCodes));
+    args.codes_dev = nullptr;
+    return A > 128 ? device_codes(codes, A, &args.codes_dev) : HDX_OK;
+}
+
+hdx_status set_codes(EncodedArgs& a, const uint8_t* codes, uint32_t A) {
+    std::memcpy(a.codes, codes, std::min(A, kKernargCodes));
+    a.codes_dev = nullptr;
+    return A > kWsweepMaxAttrs ? device_codes(codes, A, &a.codes_dev) : HDX_OK;
 }
 
 // ---- device binding -------------------------------------------------------
@@ -94,44 +135,77 @@ void untrack_scratch(Scratch* s) {
     g_scratch.erase(std::remove(g_scratch.begin(), g_scratch.end(), s), g_scratch.end());
 }
 
+// Scratch of threads that exited.  A thread-local destructor makes no HIP
+// call: at thread (or process) exit the runtime, or a profiler's per-thread
+// state (rocprofv3), may already be gone, and a HIP call there aborted the
+// process (round 4).  The destructor parks the frees here instead; the next
+// hdx_shutdown, or the next thread that binds a device, runs them.  Whatever
+// is still parked when the process exits is released with the process.
+// Leaked on purpose: thread-local destructors may run after static ones.
+struct Orphans {
+    std::mutex mu;
+    std::vector<std::function<void()>> frees;
+    std::atomic<size_t> count{0};
+};
+static Orphans& orphans() {
+    static Orphans* o = new Orphans();
+    return *o;
+}
+
+void park_orphan(std::function<void()> free_fn) {
+    Orphans& o = orphans();
+    std::lock_guard<std::mutex> lk(o.mu);
+    o.frees.push_back(std::move(free_fn));
+    o.count.store(o.frees.size(), std::memory_order_release);
+}
+
+// Runs the parked frees on the calling thread; restores its HIP device.
+static void reap_orphans() {
+    Orphans& o = orphans();
+    if (o.count.load(std::memory_order_acquire) == 0) return;
+    std::vector<std::function<void()>> todo;
+    {
+        std::lock_guard<std::mutex> lk(o.mu);
+        todo.swap(o.frees);
+        o.count.store(0, std::memory_order_release);
+    }
+    int dev = -1;
+    const bool had = hipGetDevice(&dev) == hipSuccess;
+    for (auto& f : todo) f();
+    if (had && dev >= 0) (void)hipSetDevice(dev);
+    (void)hipGetLastError();
+}
+
 struct ThreadState : Scratch {
     int device = -1;
     bool tracked = false;
     hipStream_t stream = nullptr;
-    // host-path pipeline: two slots, each with device + pinned staging
-    struct Slot {
-        hipStream_t s = nullptr;
-        uint8_t* d_blob = nullptr; size_t cap_blob = 0;
-        uint64_t* d_base = nullptr; uint32_t* d_len = nullptr; uint64_t* d_coords = nullptr;
-        size_t cap_obj = 0, cap_attr = 0, cap_coords = 0;
-        uint64_t* h_base = nullptr; size_t cap_hbase = 0;
-        uint8_t* h_blob = nullptr; size_t cap_hblob = 0;    // only for pageable inputs
-        uint64_t* h_coords = nullptr; size_t cap_hcoords = 0;
-        uint32_t* h_len = nullptr; size_t cap_hlen = 0;
-    } slot[2];
-    // Frees everything and unbinds the thread (it rebinds lazily on its next call).
-    void release() override {
-        if (device < 0) return;
-        (void)hipSetDevice(device);
-        for (auto& s : slot) {
-            if (s.s) (void)hipStreamSynchronize(s.s);
-            (void)hipFree(s.d_blob); (void)hipFree(s.d_base); (void)hipFree(s.d_len);
-            (void)hipFree(s.d_coords);
-            (void)hipHostFree(s.h_base); (void)hipHostFree(s.h_blob);
-            (void)hipHostFree(s.h_coords); (void)hipHostFree(s.h_len);
-            if (s.s) (void)hipStreamDestroy(s.s);
-            s = Slot{};
-        }
-        if (stream) {
-            (void)hipStreamSynchronize(stream);
-            (void)hipStreamDestroy(stream);
-        }
+    HostSlot slot[2];  // the host-resident pipelines (hdx_hostpath.cpp)
+    // The frees of everything held, as one job (empty when nothing is held);
+    // leaves the state unbound (the thread rebinds lazily on its next call).
+    std::function<void()> detach() {
+        if (device < 0) return {};
+        const int dev = device;
+        HostSlot held[2] = {slot[0], slot[1]};
+        hipStream_t st = stream;
+        for (auto& s : slot) s = HostSlot{};
         stream = nullptr;
         device = -1;
+        return [dev, held, st]() mutable {
+            (void)hipSetDevice(dev);
+            for (auto& s : held) free_host_slot(s);
+            if (st) {
+                (void)hipStreamSynchronize(st);
+                (void)hipStreamDestroy(st);
+            }
+        };
     }
-    ~ThreadState() {
+    void release() override {
+        if (auto f = detach()) f();
+    }
+    ~ThreadState() {  // no HIP call here: park the frees (reap_orphans)
         if (tracked) untrack_scratch(this);
-        release();
+        if (auto f = detach()) park_orphan(std::move(f));
     }
 };
 static thread_local ThreadState t_state;
@@ -150,6 +224,7 @@ hdx_status bind_device(int want /* -1: current */) {
     if (t_state.device != dev) {
         if (t_state.device >= 0)
             return fail(HDX_E_INVALID, "thread already bound to device %d", t_state.device);
+        reap_orphans();  // exited threads' scratch (restores the current device)
         t_state.device = dev;
         if (!t_state.tracked) {
             track_scratch(&t_state);
@@ -175,137 +250,24 @@ hdx_status thread_stream(hipStream_t* out) {
     return HDX_OK;
 }
 
-static bool is_pinned(const void* p) {
+int thread_device() { return t_state.device; }
+
+hdx_status thread_slots(HostSlot** out) {
+    hdx_status st = bind_device(-1);
+    if (st != HDX_OK) return st;
+    for (auto& s : t_state.slot)
+        if (!s.s) HIP_TRY(hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking));
+    *out = t_state.slot;
+    return HDX_OK;
+}
+
+bool is_pinned(const void* p) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
         (void)hipGetLastError();
         return false;
     }
     return a.type == hipMemoryTypeHost;
-}
-
-static bool is_numeric_code(uint8_t c) { return c >= CODE_INT64; }
-
-// ---- host-resident pipeline ------------------------------------------------
-
-static constexpr uint64_t kChunkBytes = 128ull << 20;  // blob bytes per in-flight chunk
-
-hdx_status hash_host(const uint8_t* codes, uint32_t A, const uint8_t* blob,
-                     uint64_t blob_bytes, const uint64_t* obj_base,
-                     const uint32_t* attr_len, uint64_t n, uint64_t* coords) {
-    hdx_status st = bind_device(-1);
-    if (st != HDX_OK) return st;
-    ThreadState& ts = t_state;
-
-    // Host-side validation (the reference asserts here) and the object's byte
-    // extent, done chunk by chunk as the pipeline below reaches each object, so
-    // the first copies start after one chunk's validation, not the batch's.
-    auto extent = [&](uint64_t i, uint64_t* out) -> hdx_status {
-        uint64_t s = 0;
-        for (uint32_t j = 0; j < A; ++j) {
-            const uint32_t L = attr_len[i * A + j];
-            if (is_numeric_code(codes[j]) && L != 0 && L != 8)
-                return fail(HDX_E_BADSIZE, "object %llu attribute %u: numeric value of %u bytes",
-                            (unsigned long long)i, j, L);
-            s += L;
-        }
-        if (s >= (1ull << 32))
-            return fail(HDX_E_INVALID, "object %llu is %llu bytes (limit 4 GiB)",
-                        (unsigned long long)i, (unsigned long long)s);
-        if (obj_base[i] > blob_bytes || s > blob_bytes - obj_base[i])
-            return fail(HDX_E_INVALID, "object %llu [%llu,+%llu) outside blob of %llu bytes",
-                        (unsigned long long)i, (unsigned long long)obj_base[i],
-                        (unsigned long long)s, (unsigned long long)blob_bytes);
-        *out = s;
-        return HDX_OK;
-    };
-
-    const bool blob_pinned = is_pinned(blob);
-    const bool len_pinned = is_pinned(attr_len);
-    const bool coords_pinned = is_pinned(coords);
-    for (auto& s : ts.slot)
-        if (!s.s) HIP_TRY(hipStreamCreateWithFlags(&s.s, hipStreamNonBlocking));
-
-    BatchArgs args{};
-    args.A = A;
-    std::memcpy(args.codes, codes, A);
-    finalize_args(args);
-
-    struct Pending { uint64_t first = 0, cnt = 0; bool live = false; } pend[2];
-    auto finish = [&](int k) -> hdx_status {
-        auto& sl = ts.slot[k];
-        if (!pend[k].live) return HDX_OK;
-        HIP_TRY(hipStreamSynchronize(sl.s));
-        if (!coords_pinned)
-            std::memcpy(coords + pend[k].first * A, sl.h_coords, pend[k].cnt * A * sizeof(uint64_t));
-        pend[k].live = false;
-        return HDX_OK;
-    };
-
-    uint64_t i = 0, next_size = 0;
-    int k = 0;
-    if ((st = extent(0, &next_size)) != HDX_OK) return st;
-    auto drain = [&](hdx_status err) {  // an invalid object: let the copies in flight land
-        (void)finish(0);
-        (void)finish(1);
-        return err;
-    };
-    while (i < n) {
-        // Grow the chunk while its byte extent stays under kChunkBytes; an
-        // object that does not fit starts the next chunk (its extent is kept).
-        uint64_t lo = obj_base[i], hi = obj_base[i] + next_size, e = i + 1;
-        while (e < n) {
-            if ((st = extent(e, &next_size)) != HDX_OK) return drain(st);
-            const uint64_t nlo = std::min(lo, obj_base[e]);
-            const uint64_t nhi = std::max(hi, obj_base[e] + next_size);
-            if (nhi - nlo > kChunkBytes) break;
-            lo = nlo; hi = nhi; ++e;
-        }
-        const uint64_t cnt = e - i, bytes = hi - lo;
-        auto& sl = ts.slot[k];
-        if ((st = finish(k)) != HDX_OK) return st;
-        if ((st = grow_dev(&sl.d_blob, &sl.cap_blob, std::max<uint64_t>(bytes, 1))) != HDX_OK) return st;
-        if ((st = grow_dev(&sl.d_base, &sl.cap_obj, cnt)) != HDX_OK) return st;
-        if ((st = grow_dev(&sl.d_len, &sl.cap_attr, cnt * A)) != HDX_OK) return st;
-        if ((st = grow_dev(&sl.d_coords, &sl.cap_coords, cnt * A)) != HDX_OK) return st;
-        if ((st = grow_pinned(&sl.h_base, &sl.cap_hbase, cnt)) != HDX_OK) return st;
-        for (uint64_t t = 0; t < cnt; ++t) sl.h_base[t] = obj_base[i + t] - lo;
-
-        const uint8_t* src_blob = blob + lo;
-        if (!blob_pinned) {
-            if ((st = grow_pinned(&sl.h_blob, &sl.cap_hblob, std::max<uint64_t>(bytes, 1))) != HDX_OK)
-                return st;
-            std::memcpy(sl.h_blob, blob + lo, bytes);
-            src_blob = sl.h_blob;
-        }
-        const uint32_t* src_len = attr_len + i * A;
-        if (!len_pinned) {
-            if ((st = grow_pinned(&sl.h_len, &sl.cap_hlen, cnt * A)) != HDX_OK) return st;
-            std::memcpy(sl.h_len, attr_len + i * A, cnt * A * sizeof(uint32_t));
-            src_len = sl.h_len;
-        }
-        HIP_TRY(hipMemcpyAsync(sl.d_blob, src_blob, bytes, hipMemcpyHostToDevice, sl.s));
-        HIP_TRY(hipMemcpyAsync(sl.d_base, sl.h_base, cnt * 8, hipMemcpyHostToDevice, sl.s));
-        HIP_TRY(hipMemcpyAsync(sl.d_len, src_len, cnt * A * 4, hipMemcpyHostToDevice, sl.s));
-        args.blob = sl.d_blob;
-        args.obj_base = sl.d_base;
-        args.attr_len = sl.d_len;
-        args.coords = sl.d_coords;
-        args.status = nullptr;  // sizes validated above
-        args.n = cnt;
-        HIP_TRY(launch_hash_batch(args, sl.s));
-        uint64_t* dst = coords + i * A;
-        if (!coords_pinned) {
-            if ((st = grow_pinned(&sl.h_coords, &sl.cap_hcoords, cnt * A)) != HDX_OK) return st;
-            dst = sl.h_coords;
-        }
-        HIP_TRY(hipMemcpyAsync(dst, sl.d_coords, cnt * A * 8, hipMemcpyDeviceToHost, sl.s));
-        pend[k] = {i, cnt, true};
-        i = e;
-        k ^= 1;
-    }
-    if ((st = finish(k)) != HDX_OK) return st;
-    return finish(k ^ 1);
 }
 
 }  // namespace hdx
@@ -356,6 +318,7 @@ HDX_EXPORT hdx_status hdx_shutdown(void) {
     // do); then each remaining release() binds its scratch's device and the
     // caller's current device is restored, so its lazy rebind returns to it
     device_set_teardown();
+    reap_orphans();
     int dev = -1;
     const bool had = hipGetDevice(&dev) == hipSuccess;
     {
@@ -387,12 +350,14 @@ HDX_EXPORT hdx_status hdx_hash_batch_device(const uint32_t* types, uint32_t attr
                                             uint64_t* coords, uint32_t* status_dev,
                                             hdx_stream stream) {
     BatchArgs args{};
-    hdx_status st = check_schema(types, attrs_sz, args.codes);
+    std::vector<uint8_t> codes(attrs_sz ? attrs_sz : 1);
+    hdx_status st = check_schema(types, attrs_sz, codes.data());
     if (st != HDX_OK) return st;
     if (n == 0) return HDX_OK;
     if (!blob || !obj_base || !attr_len || !coords)
         return fail(HDX_E_INVALID, "NULL device pointer");
     if ((st = bind_device(-1)) != HDX_OK) return st;
+    if ((st = set_codes(args, codes.data(), attrs_sz)) != HDX_OK) return st;
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
     args.blob = blob;
     args.obj_base = obj_base;
@@ -406,15 +371,50 @@ HDX_EXPORT hdx_status hdx_hash_batch_device(const uint32_t* types, uint32_t attr
     return HDX_OK;
 }
 
-// Region tables live on the device they were created on; a fused launch on
-// another device would read that device's memory (the batcher checks the same).
-static hdx_status check_table_devices(const hdx_region_table* tables, uint32_t ntables) {
-    for (uint32_t t = 0; t < ntables; ++t)
-        if (tables[t]->device != t_state.device)
-            return fail(HDX_E_INVALID, "region table %u was created on device %d, the call runs on device %d", t,
-                        tables[t]->device, t_state.device);
+namespace hdx {
+hdx_status fill_sweep_table(SweepTable& st, hdx_region_table_s* t, int dev, uint64_t* out) {
+    st = SweepTable{};
+    st.lower = t->d_lower;
+    st.upper = t->d_upper;
+    st.ids = t->d_ids;
+    st.index = t->d_index;
+    if (dev != t->device) {
+        std::lock_guard<std::mutex> lk(t->rep_mu);
+        const hdx_region_table_s::Replica* r = nullptr;
+        for (const auto& x : t->replicas)
+            if (x.device == dev) r = &x;
+        if (!r) {
+            hdx_region_table_s::Replica c{dev, nullptr, nullptr, nullptr, nullptr};
+            const size_t box = t->h_lower.size() * 8;
+            auto up = [](uint64_t** d, const std::vector<uint64_t>& h, size_t extra) {
+                if (hipMalloc((void**)d, h.size() * 8 + extra) != hipSuccess) return false;
+                return h.empty() || hipMemcpy(*d, h.data(), h.size() * 8, hipMemcpyHostToDevice) == hipSuccess;
+            };
+            const bool ok = up(&c.lower, t->h_lower, 8) && up(&c.upper, t->h_upper, 8) && up(&c.ids, t->h_ids, 8) &&
+                            (t->h_index.empty() || !t->d_index || up(&c.index, t->h_index, 0));
+            (void)box;
+            if (!ok) {
+                (void)hipGetLastError();
+                (void)hipFree(c.lower); (void)hipFree(c.upper); (void)hipFree(c.ids); (void)hipFree(c.index);
+                return fail(HDX_E_NOMEM, "region table replica on device %d", dev);
+            }
+            t->replicas.push_back(c);
+            r = &t->replicas.back();
+        }
+        st.lower = r->lower;
+        st.upper = r->upper;
+        st.ids = r->ids;
+        st.index = r->index;
+    }
+    st.out = out;
+    st.W = t->W;
+    st.D = t->D;
+    st.R = t->R;
+    st.index_words = t->index_words;
+    std::memcpy(st.attrs, t->attrs, sizeof st.attrs);
     return HDX_OK;
 }
+}  // namespace hdx
 
 static hdx_status hash_encoded(const uint32_t* types, uint32_t attrs_sz, const uint8_t* keys,
                                const uint64_t* key_off, const uint32_t* key_len, const uint8_t* vals,
@@ -422,38 +422,18 @@ static hdx_status hash_encoded(const uint32_t* types, uint32_t attrs_sz, const u
                                const hdx_region_table* tables, uint32_t ntables, uint64_t* region_ids,
                                uint64_t* coords, uint64_t* versions, uint32_t* status_dev, hdx_stream stream) {
     EncodedArgs a{};
-    hdx_status st = check_schema(types, attrs_sz, a.codes);
+    std::vector<uint8_t> codes(attrs_sz ? attrs_sz : 1);
+    hdx_status st = check_schema(types, attrs_sz, codes.data());
     if (st != HDX_OK) return st;
-    if (attrs_sz > 128) return fail(HDX_E_INVALID, "attrs_sz=%u > 128 for stored objects", attrs_sz);
-    if (ntables > kMaxSweepTables) return fail(HDX_E_INVALID, "%u region tables (at most %u)", ntables,
-                                               kMaxSweepTables);
-    if (ntables && (!tables || !region_ids)) return fail(HDX_E_INVALID, "NULL tables / region_ids");
-    for (uint32_t t = 0; t < ntables; ++t) {
-        if (!tables[t]) return fail(HDX_E_INVALID, "NULL table %u", t);
-        for (uint32_t d = 0; d < tables[t]->D; ++d)
-            if (tables[t]->attrs[d] >= attrs_sz)
-                return fail(HDX_E_INVALID, "table %u: subspace attribute %u >= attrs_sz %u", t,
-                            tables[t]->attrs[d], attrs_sz);
-    }
+    if ((st = check_tables(tables, ntables, attrs_sz, region_ids)) != HDX_OK) return st;
     if (n == 0) return HDX_OK;
     if (!keys || !key_off || !key_len || !vals || !val_off || !val_len || (!coords && !ntables))
         return fail(HDX_E_INVALID, "NULL device pointer");
     if ((st = bind_device(-1)) != HDX_OK) return st;
-    if ((st = check_table_devices(tables, ntables)) != HDX_OK) return st;
+    if ((st = set_codes(a, codes.data(), attrs_sz)) != HDX_OK) return st;
     a.T = ntables;
-    for (uint32_t t = 0; t < ntables; ++t) {
-        const hdx_region_table tb = tables[t];
-        a.t[t].index = tb->d_index;
-        a.t[t].lower = tb->d_lower;
-        a.t[t].upper = tb->d_upper;
-        a.t[t].ids = tb->d_ids;
-        a.t[t].out = region_ids + (size_t)t * n;
-        a.t[t].W = tb->W;
-        a.t[t].D = tb->D;
-        a.t[t].R = tb->R;
-        a.t[t].index_words = tb->index_words;
-        std::memcpy(a.t[t].attrs, tb->attrs, sizeof a.t[t].attrs);
-    }
+    for (uint32_t t = 0; t < ntables; ++t)
+        if ((st = fill_sweep_table(a.t[t], tables[t], t_state.device, region_ids + (size_t)t * n)) != HDX_OK) return st;
     a.keys = keys;
     a.key_off = key_off;
     a.key_len = key_len;
@@ -492,6 +472,42 @@ HDX_EXPORT hdx_status hdx_hash_encoded_regions_device(const uint32_t* types, uin
                         region_ids, coords, versions, status_dev, stream);
 }
 
+namespace hdx {
+hdx_status check_tables(const hdx_region_table* tables, uint32_t ntables, uint32_t A, const uint64_t* region_ids) {
+    if (ntables > kMaxSweepTables)
+        return fail(HDX_E_INVALID, "%u region tables (at most %u)", ntables, kMaxSweepTables);
+    if (ntables && (!tables || !region_ids)) return fail(HDX_E_INVALID, "NULL tables / region_ids");
+    for (uint32_t t = 0; t < ntables; ++t) {
+        if (!tables[t]) return fail(HDX_E_INVALID, "NULL table %u", t);
+        for (uint32_t d = 0; d < tables[t]->D; ++d)
+            if (tables[t]->attrs[d] >= A)
+                return fail(HDX_E_INVALID, "table %u: subspace attribute %u >= attrs_sz %u", t, tables[t]->attrs[d], A);
+    }
+    return HDX_OK;
+}
+
+hdx_status batch_args(BatchArgs& args, const uint8_t* codes, uint32_t A, const uint8_t* blob,
+                      const uint64_t* obj_base, const uint32_t* attr_len, uint64_t n, uint64_t* coords,
+                      uint32_t* status, const hdx_region_table* tables, uint32_t T, uint64_t* ids,
+                      uint64_t ids_stride, int dev) {
+    args = BatchArgs{};
+    hdx_status st = set_codes(args, codes, A);
+    if (st != HDX_OK) return st;
+    args.blob = blob;
+    args.obj_base = obj_base;
+    args.attr_len = attr_len;
+    args.coords = coords;
+    args.status = status;
+    args.n = n;
+    args.A = A;
+    finalize_args(args);
+    args.T = T;
+    for (uint32_t t = 0; t < T; ++t)
+        if ((st = fill_sweep_table(args.t[t], tables[t], dev, ids + t * ids_stride)) != HDX_OK) return st;
+    return HDX_OK;
+}
+}  // namespace hdx
+
 HDX_EXPORT hdx_status hdx_hash_batch_regions_device(const uint32_t* types, uint32_t attrs_sz, const uint8_t* blob,
                                                     const uint64_t* obj_base, const uint32_t* attr_len, uint64_t n,
                                                     const hdx_region_table* tables, uint32_t ntables,
@@ -499,65 +515,21 @@ HDX_EXPORT hdx_status hdx_hash_batch_regions_device(const uint32_t* types, uint3
                                                     hdx_stream stream) {
     if (ntables == 0) return fail(HDX_E_INVALID, "no region tables");
     if (n && !attr_len) return fail(HDX_E_INVALID, "NULL device pointer");
-    BatchArgs args{};
-    hdx_status st = check_schema(types, attrs_sz, args.codes);
+    std::vector<uint8_t> codes(attrs_sz ? attrs_sz : 1);
+    hdx_status st = check_schema(types, attrs_sz, codes.data());
     if (st != HDX_OK) return st;
-    if (attrs_sz > 128) return fail(HDX_E_INVALID, "attrs_sz=%u > 128 for the fused lookup", attrs_sz);
-    if (ntables > kMaxSweepTables)
-        return fail(HDX_E_INVALID, "%u region tables (at most %u)", ntables, kMaxSweepTables);
-    if (!tables || !region_ids) return fail(HDX_E_INVALID, "NULL tables / region_ids");
-    for (uint32_t t = 0; t < ntables; ++t) {
-        if (!tables[t]) return fail(HDX_E_INVALID, "NULL table %u", t);
-        for (uint32_t d = 0; d < tables[t]->D; ++d)
-            if (tables[t]->attrs[d] >= attrs_sz)
-                return fail(HDX_E_INVALID, "table %u: subspace attribute %u >= attrs_sz %u", t, tables[t]->attrs[d],
-                            attrs_sz);
-    }
+    if ((st = check_tables(tables, ntables, attrs_sz, region_ids)) != HDX_OK) return st;
     if (n == 0) return HDX_OK;
     if (!blob || !obj_base) return fail(HDX_E_INVALID, "NULL device pointer");
     if ((st = bind_device(-1)) != HDX_OK) return st;
-    if ((st = check_table_devices(tables, ntables)) != HDX_OK) return st;
-    args.blob = blob;
-    args.obj_base = obj_base;
-    args.attr_len = attr_len;
-    args.coords = coords;
-    args.status = status_dev;
-    args.n = n;
-    args.A = attrs_sz;
-    finalize_args(args);
-    args.T = ntables;
-    for (uint32_t t = 0; t < ntables; ++t) {
-        const hdx_region_table tb = tables[t];
-        args.t[t].index = tb->d_index;
-        args.t[t].lower = tb->d_lower;
-        args.t[t].upper = tb->d_upper;
-        args.t[t].ids = tb->d_ids;
-        args.t[t].out = region_ids + (size_t)t * n;
-        args.t[t].W = tb->W;
-        args.t[t].D = tb->D;
-        args.t[t].R = tb->R;
-        args.t[t].index_words = tb->index_words;
-        std::memcpy(args.t[t].attrs, tb->attrs, sizeof args.t[t].attrs);
-    }
+    BatchArgs args;
+    if ((st = batch_args(args, codes.data(), attrs_sz, blob, obj_base, attr_len, n, coords, status_dev, tables,
+                         ntables, region_ids, n, t_state.device)) != HDX_OK)
+        return st;
     HIP_TRY(launch_hash_batch_regions(args, (hipStream_t)stream));
     return HDX_OK;
 }
 
-HDX_EXPORT hdx_status hdx_hash_batch_host(const uint32_t* types, uint32_t attrs_sz,
-                                          const uint8_t* blob, uint64_t blob_bytes,
-                                          const uint64_t* obj_base, const uint32_t* attr_len,
-                                          uint64_t n, uint64_t* coords) {
-    uint8_t codes[HDX_MAX_ATTRS];
-    hdx_status st = check_schema(types, attrs_sz, codes);
-    if (st != HDX_OK) return st;
-    if (n == 0) return HDX_OK;
-    if (!obj_base || !attr_len || !coords || (!blob && blob_bytes))
-        return fail(HDX_E_INVALID, "NULL host pointer");
-    static const uint8_t one = 0;
-    if (host_batch_uses_set())  // hdx_init_mask: split over its devices (hdx_multi.cpp)
-        return hash_host_set(codes, attrs_sz, blob ? blob : &one, blob_bytes, obj_base, attr_len, n, coords);
-    return hash_host(codes, attrs_sz, blob ? blob : &one, blob_bytes, obj_base, attr_len, n, coords);
-}
 
 // hdx_hash_value / hdx_hash_key / hdx_hash_object: the per-object entry points
 // run on the host CPU (hdx_cpu.cpp).
@@ -714,6 +686,12 @@ HDX_EXPORT hdx_status hdx_region_table_destroy(hdx_region_table t) {
     (void)hipFree(t->d_upper);
     (void)hipFree(t->d_ids);
     (void)hipFree(t->d_index);
+    for (const auto& r : t->replicas) {
+        (void)hipFree(r.lower);
+        (void)hipFree(r.upper);
+        (void)hipFree(r.ids);
+        (void)hipFree(r.index);
+    }
     delete t;
     return HDX_OK;
 }
@@ -729,12 +707,13 @@ HDX_EXPORT hdx_status hdx_lookup_region_device(hdx_region_table t, const uint64_
             return fail(HDX_E_INVALID, "subspace attribute %u >= attrs_sz %u", t->attrs[d], attrs_sz);
     hdx_status st = bind_device(-1);
     if (st != HDX_OK) return st;
-    if ((st = check_table_devices(&t, 1)) != HDX_OK) return st;
+    SweepTable tb;
+    if ((st = fill_sweep_table(tb, t, t_state.device, region_ids)) != HDX_OK) return st;
     RegionArgs a{};
-    a.lower = t->d_lower;
-    a.upper = t->d_upper;
-    a.ids = t->d_ids;
-    a.index = t->d_index;
+    a.lower = tb.lower;
+    a.upper = tb.upper;
+    a.ids = tb.ids;
+    a.index = tb.index;
     a.W = t->W;
     a.index_words = t->index_words;
     a.coords = coords;

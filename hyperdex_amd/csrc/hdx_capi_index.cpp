@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstring>
+#include <functional>
 #include <vector>
 
 #include "hdx_host.h"
@@ -31,18 +32,25 @@ struct SearchStage : Scratch {
     uint8_t* host = nullptr;
     uint8_t* dev = nullptr;
     size_t cap = 0;
-    void release() override {
-        if (device < 0) return;
-        (void)hipSetDevice(device);
-        (void)hipHostFree(host);
-        (void)hipFree(dev);
+    std::function<void()> detach() {
+        if (device < 0) return {};
+        const int d = device;
+        uint8_t *h = host, *g = dev;
         host = dev = nullptr;
         cap = 0;
         device = -1;
+        return [d, h, g] {
+            (void)hipSetDevice(d);
+            (void)hipHostFree(h);
+            (void)hipFree(g);
+        };
     }
-    ~SearchStage() {
+    void release() override {
+        if (auto f = detach()) f();
+    }
+    ~SearchStage() {  // no HIP call at thread exit (hdx_capi.cpp, park_orphan)
         if (tracked) untrack_scratch(this);
-        release();
+        if (auto f = detach()) park_orphan(std::move(f));
     }
 };
 thread_local SearchStage t_search;

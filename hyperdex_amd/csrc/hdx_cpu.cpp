@@ -231,7 +231,6 @@ HDX_EXPORT hdx_status hdx_hash_object(const uint32_t* types, uint32_t attrs_sz, 
         return fail(HDX_E_INVALID, "NULL pointer");
     // the reference asserts on the first bad attribute (hash.cc:38, :233/:204);
     // here nothing is written unless the whole object hashes
-    uint8_t codes[HDX_MAX_ATTRS];
     for (uint32_t j = 0; j < attrs_sz; ++j) {
         const int code = type_code(types[j]);
         if (code < 0) return fail(HDX_E_BADTYPE, "attribute %u: unknown hyperdatatype %u", j, types[j]);
@@ -241,9 +240,9 @@ HDX_EXPORT hdx_status hdx_hash_object(const uint32_t* types, uint32_t attrs_sz, 
             return fail(HDX_E_BADSIZE, "key: numeric value of %zu bytes", n);
         }
         if (j > 0 && !values[j - 1] && n) return fail(HDX_E_INVALID, "value %u is NULL", j - 1);
-        codes[j] = (uint8_t)code;
     }
-    (void)cpu::hash_code(codes[0], key, key_len, &hs[0]);
-    for (uint32_t j = 1; j < attrs_sz; ++j) (void)cpu::hash_code(codes[j], values[j - 1], value_lens[j - 1], &hs[j]);
+    (void)cpu::hash_code(type_code(types[0]), key, key_len, &hs[0]);
+    for (uint32_t j = 1; j < attrs_sz; ++j)
+        (void)cpu::hash_code(type_code(types[j]), values[j - 1], value_lens[j - 1], &hs[j]);
     return HDX_OK;
 }

@@ -1,6 +1,7 @@
 // hdx_cuts.h — byte-balanced contiguous object ranges for the device set
 // (hdx_multi.cpp: hdx_shard_ranges, hdx_hash_batch_host over the set), the
-// rule of hyperdex_amd/dist.py:shard_ranges restated in C++.  Host-only, no
+// rule of hyperdex_amd/dist.py:shard_ranges restated in C++, over a packed
+// batch's attribute lengths or stored objects' key + value lengths.  Host-only, no
 // HIP: tests/cpp/sanitize_test.cc builds it under ASan/UBSan.
 #pragma once
 
@@ -28,23 +29,40 @@ inline uint64_t object_bytes(const uint32_t* attr_len, uint32_t A, uint64_t i) {
     return s;
 }
 
-inline uint64_t block_bytes(const uint32_t* attr_len, uint32_t A, uint64_t n, uint64_t b) {
+// Object sizes of a packed batch: the sums of its attribute lengths.
+struct PackedSizes {
+    const uint32_t* attr_len;
+    uint32_t A;
+    uint64_t operator()(uint64_t i) const { return object_bytes(attr_len, A, i); }
+};
+// Object sizes of stored objects (hdx_hash_encoded_host): key + value bytes.
+struct StoredSizes {
+    const uint32_t* key_len;
+    const uint32_t* val_len;
+    uint64_t operator()(uint64_t i) const { return (uint64_t)key_len[i] + val_len[i]; }
+};
+
+template <typename Sizes>
+inline uint64_t block_bytes(const Sizes& size, uint64_t n, uint64_t b) {
     const uint64_t lo = b * kCutBlock, hi = std::min(n, lo + kCutBlock);
     uint64_t s = 0;
-    for (uint64_t i = lo; i < hi; ++i) s += object_bytes(attr_len, A, i);
+    for (uint64_t i = lo; i < hi; ++i) s += size(i);
     return s;
+}
+inline uint64_t block_bytes(const uint32_t* attr_len, uint32_t A, uint64_t n, uint64_t b) {
+    return block_bytes(PackedSizes{attr_len, A}, n, b);
 }
 
 // bprefix[b] = bytes of objects [0, b * kCutBlock), b in [0, blocks]
-struct Prefix {
-    const uint32_t* attr_len;
-    uint32_t A;
+template <typename Sizes>
+struct PrefixOf {
+    Sizes size;
     uint64_t n;
     std::vector<uint64_t> bprefix;
     uint64_t at(uint64_t i) const {  // bytes of objects [0, i)
         const uint64_t b = i / kCutBlock;
         uint64_t s = bprefix[b];
-        for (uint64_t k = b * kCutBlock; k < i; ++k) s += object_bytes(attr_len, A, k);
+        for (uint64_t k = b * kCutBlock; k < i; ++k) s += size(k);
         return s;
     }
     // first i in [0, n] with prefix(i) >= target (numpy searchsorted, side="left")
@@ -57,12 +75,14 @@ struct Prefix {
             if ((double)bprefix[mid] < target) lo = mid; else hi = mid - 1;
         }
         uint64_t i = lo * kCutBlock, s = bprefix[lo];
-        while (i < n && (double)s < target) s += object_bytes(attr_len, A, i++);
+        while (i < n && (double)s < target) s += size(i++);
         return (double)s < target ? n : i;
     }
 };
+using Prefix = PrefixOf<PackedSizes>;
 
-inline void cuts_from_prefix(const Prefix& p, uint32_t world, double tol, uint64_t* first) {
+template <typename Sizes>
+inline void cuts_from_prefix(const PrefixOf<Sizes>& p, uint32_t world, double tol, uint64_t* first) {
     const uint64_t n = p.n;
     std::vector<uint64_t> even(world + 1);
     for (uint32_t k = 0; k <= world; ++k) even[k] = (uint64_t)((unsigned __int128)n * k / world);
@@ -91,18 +111,25 @@ inline void cuts_from_prefix(const Prefix& p, uint32_t world, double tol, uint64
     first[world] = n;
 }
 
-// The cuts of n objects over world ranges: first[k] = range k's first object,
-// first[world] = n.  attr_len NULL: counts that differ by at most one.
+// The cuts of n objects of sizes size(i) over world ranges: first[k] = range
+// k's first object, first[world] = n.
+template <typename Sizes>
+inline void shard_cuts_of(const Sizes& size, uint64_t n, uint32_t world, double tol, uint64_t* first) {
+    PrefixOf<Sizes> p{size, n, {}};
+    const uint64_t blocks = (n + kCutBlock - 1) / kCutBlock;
+    p.bprefix.assign(blocks + 1, 0);
+    for (uint64_t b = 0; b < blocks; ++b) p.bprefix[b + 1] = p.bprefix[b] + block_bytes(size, n, b);
+    cuts_from_prefix(p, world, tol, first);
+}
+
+// The same over a packed batch's attribute lengths; attr_len NULL: counts
+// that differ by at most one.
 inline void shard_cuts(const uint32_t* attr_len, uint32_t A, uint64_t n, uint32_t world, double tol, uint64_t* first) {
     if (!attr_len) {
         for (uint32_t k = 0; k <= world; ++k) first[k] = (uint64_t)((unsigned __int128)n * k / world);
         return;
     }
-    Prefix p{attr_len, A, n, {}};
-    const uint64_t blocks = (n + kCutBlock - 1) / kCutBlock;
-    p.bprefix.assign(blocks + 1, 0);
-    for (uint64_t b = 0; b < blocks; ++b) p.bprefix[b + 1] = p.bprefix[b] + block_bytes(attr_len, A, n, b);
-    cuts_from_prefix(p, world, tol, first);
+    shard_cuts_of(PackedSizes{attr_len, A}, n, world, tol, first);
 }
 
 }  // namespace hdx

@@ -367,6 +367,26 @@ static hipError_t launch_encoded(const EncodedArgs& a_in, hipStream_t stream) {
 hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
     if (a_in.n == 0) return hipSuccess;
     EncodedArgs a = a_in;
+    if (a.A > kWsweepMaxAttrs) {
+        // wide schemas (hdx_wide.hip): the wide sweep, then one lookup launch
+        // per table
+        const RegionHashFn hash = [&](uint64_t first, uint64_t count, uint64_t* c) {
+            EncodedArgs b = a;
+            b.key_off += first;
+            b.key_len += first;
+            b.val_off += first;
+            b.val_len += first;
+            if (b.versions) b.versions += first;
+            b.n = count;
+            b.coords = c;
+            b.T = 0;
+            return launch_hash_sweep_wide(b, stream);
+        };
+        if (!a.T) return launch_hash_sweep_wide(a, stream);
+        bool no_scratch = false;
+        const hipError_t e = regions_by_lookup(a.n, a.A, a.t, a.T, a.coords, hash, stream, &no_scratch);
+        return no_scratch ? hipErrorOutOfMemory : e;
+    }
     a.a_magic = (uint32_t)(((1ull << 31) + a.A - 1) / a.A);
     // default: dword-aligned loads (5.49 vs 6.14 ms per 10 M config-3b objects,
     // profiles/r1/ab_a4_cfg5.jsonl), 32 objects per wave (5.05 vs 5.31 ms for
@@ -441,13 +461,6 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
         case 173: return launch_encoded<false, true, 0, 32, false, true, true>(a, stream);
         case 174: return launch_encoded<false, true, 0, 64, false, true, true>(a, stream);
         case 48: return launch_encoded<false, true, 0, 16>(a, stream);
-        // LDS-staged (hdx_encoded_staged.hip): 95 G=7 sorted 10 KiB, 96 G=11 sorted 14 KiB,
-        // 97 G=3 sorted 5 KiB, 98 G=4 unsorted 6 KiB, 99 G=15 sorted 20 KiB
-        case 95: if (a.A <= 32) return launch_hash_encoded_staged(a, 7, 10240, true, stream); break;
-        case 96: if (a.A <= 32) return launch_hash_encoded_staged(a, 11, 14336, true, stream); break;
-        case 97: if (a.A <= 32) return launch_hash_encoded_staged(a, 3, 5120, true, stream); break;
-        case 98: if (a.A <= 32) return launch_hash_encoded_staged(a, 4, 6144, false, stream); break;
-        case 99: if (a.A <= 32) return launch_hash_encoded_staged(a, 15, 20480, true, stream); break;
         // wave-staged (hdx_wsweep.hip): 230 6 objects / 2 passes, 231 7 objects, 232 11 objects / 3 passes,
         // 236 = 230 without the pass-boundary gap, 237 / 238 its debug shapes (no hash / no hash, no walk),
         // 239 = 230 with the one-block > 64-byte loop, 242 without the shared final mix16,

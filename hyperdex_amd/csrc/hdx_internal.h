@@ -15,7 +15,11 @@ namespace hdx {
 
 
 // Kernel arguments, passed by value (kernarg segment).  codes[] holds the
-// per-attribute dispatch class (hdx_device_hash.h CODE_*).
+// per-attribute dispatch class (hdx_device_hash.h CODE_*) for schemas of up
+// to kKernargCodes attributes; wider schemas (up to HDX_MAX_ATTRS, the
+// reference's u16 attrs_sz) run the wide kernels (hdx_wide.hip), which read
+// the classes from codes_dev, a device copy (device_codes, hdx_capi.cpp).
+constexpr uint32_t kKernargCodes = 256;
 constexpr uint32_t kMaxSweepTables = 4;
 struct SweepTable {
     const uint64_t* index;  // interval index (NULL: scan lower/upper)
@@ -40,7 +44,8 @@ struct BatchArgs {
     double inv_A;           // 1.0 / A                       (finalize_args)
     uint32_t a_magic;       // ceil(2^31 / A): t / A == (t * a_magic) >> 31 for t * A < 2^31
     uint32_t pad_;
-    uint8_t codes[HDX_MAX_ATTRS];
+    const uint8_t* codes_dev;  // A > 128: the classes in device memory (the wide kernels)
+    uint8_t codes[kKernargCodes];
     // fused region lookup (hash_regroup_regions_kernel): T tables, K whole
     // objects per wave, lds_tables u64 words of LDS table copies per workgroup
     uint32_t T, K, lds_tables, win_bytes;  // win_bytes: the staged kernels' LDS window (hdx_staged.hip)
@@ -48,9 +53,6 @@ struct BatchArgs {
 };
 
 hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream);
-// LDS-staged hashing of packed batches (hdx_staged.hip): K = slots / A objects
-// per wave, a win_bytes window (multiple of 1 KiB, <= 64 KiB); A <= 64.
-hipError_t launch_hash_staged(const BatchArgs& args, hipStream_t stream, uint32_t slots, uint32_t win_bytes);
 // Wave-staged hash (hdx_wstage.hip): K whole objects per wave copied into an
 // LDS window by DMA and hashed from LDS; form = passes / window size.
 hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int form);  // debug library
@@ -58,12 +60,17 @@ hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int for
 // A <= 128 (else hipErrorInvalidValue).
 hipError_t launch_hash_wstage_product(const BatchArgs& args, hipStream_t stream);
 hipError_t launch_hash_wstage_regions(const BatchArgs& args, hipStream_t stream);  // + args.T tables
-// Streamed hash (hdx_stream.hip): one persistent workgroup per CU walks its
-// objects in batches staged in LDS by DMA a batch ahead, slots class-sorted
-// over the workgroup; A <= 64 (else hipErrorInvalidValue).
-hipError_t launch_hash_stream(const BatchArgs& args, hipStream_t stream, int form);
-// hash + lookup_region in one launch (args.T tables in args.t, A <= 128)
+// hash + lookup_region (args.T tables in args.t): one fused launch for A <=
+// 128 below kRegionLookupMinObjects, else the hash and one lookup launch per
+// table (hipErrorOutOfMemory when A > 128, coords is NULL and no scratch can
+// be allocated)
 hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream);
+// The wide kernels (hdx_wide.hip): any A (args.codes_dev set).  Packed
+// batches (the policy takes them for A > kKernargCodes) and stored objects
+// (A > kWsweepMaxAttrs; coords != NULL).
+hipError_t launch_hash_wide(const BatchArgs& args, hipStream_t stream);
+struct EncodedArgs;
+hipError_t launch_hash_sweep_wide(const EncodedArgs& a, hipStream_t stream);
 // Fills args.uniform_code from args.codes[0..A), and inv_A / a_magic from A.
 void finalize_args(BatchArgs& args);
 // Kernel variants (hdx_kernels.hip, variant_kernel_name): the automatic policy's
@@ -163,17 +170,15 @@ struct EncodedArgs {
     uint32_t a_magic;  // ceil(2^31 / A) (launch_hash_encoded fills it)
     uint32_t T, lds_tables;  // lds_tables: u64 words of the workgroup's table copies
     SweepTable t[kMaxSweepTables];
-    uint8_t codes[HDX_MAX_ATTRS];
+    const uint8_t* codes_dev;  // A > 128: the classes in device memory (the wide sweep)
+    uint8_t codes[kKernargCodes];
     // numeric walk (launch_hash_encoded fills them): the attributes left to the
     // hash passes — the key and every STRING value attribute — in order
-    uint8_t p2[HDX_MAX_ATTRS];
+    uint8_t p2[kKernargCodes];
     uint32_t S, s_magic;  // how many; ceil(2^31 / S)
 };
 
 hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream);
-// The sweep with each group of G objects staged in LDS (hdx_encoded_staged.hip):
-// G objects per wave, A <= 32, an LDS window of WB bytes, class-sorted passes.
-hipError_t launch_hash_encoded_staged(const EncodedArgs& a, int G, uint32_t WB, bool sort, hipStream_t stream);
 // The wave-staged sweep (hdx_wsweep.hip): K objects per wave, keys and values
 // copied into LDS by DMA, the walk and the hashing from LDS; coords != NULL,
 // A <= 64 * passes (else hipErrorInvalidValue).  The product form, and (debug

@@ -40,6 +40,7 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         case 44: return launch_regroup<2, true, true, true, true, false, true, 1>(args, stream);
         case 46: return launch_regroup<8, true, true, true, false, false, true, 1>(args, stream);
         case 212: return launch_hash_wstage_product(args, stream);  // hdx_wstage.hip
+        case 300: return launch_hash_wide(args, stream);            // hdx_wide.hip
         default:
 #if HDX_DEBUG_BUILD
             return launch_debug_variant(args, stream, variant);  // hdx_kernels_dbg.hip
@@ -63,6 +64,22 @@ static int auto_variant(const BatchArgs& args);
 // profiles/r2/ab_fused.jsonl).  A <= 128 (checked by the caller).
 hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream) {
     if (args.n == 0) return hipSuccess;
+    if (args.A > 128) {
+        // wide schemas: the batch policy's hash (44, or the wide kernel above
+        // 256 attributes), then one lookup launch per table
+        const RegionHashFn hash = [&](uint64_t first, uint64_t count, uint64_t* c) {
+            BatchArgs b = args;
+            b.obj_base += first;
+            b.attr_len += first * args.A;
+            b.n = count;
+            b.coords = c;
+            b.T = 0;
+            return launch_hash_batch(b, stream);
+        };
+        bool no_scratch = false;
+        const hipError_t e = regions_by_lookup(args.n, args.A, args.t, args.T, args.coords, hash, stream, &no_scratch);
+        return no_scratch ? hipErrorOutOfMemory : e;
+    }
 #if HDX_DEBUG_BUILD
     const int v = hash_variant();
     if (v >= 100 && v < 120) return launch_fused_debug(args, stream, v);  // hdx_kernels_dbg.hip
@@ -120,8 +137,11 @@ hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream) 
 //    class sort over 2 chunks with dword-aligned loads (3.37 vs 3.43 ms in
 //    ORDER 0 (38) and 4.22 for the chunk kernel — byte-misaligned 16-byte
 //    loads had made the texture-address unit the bound).
-//    Schemas of more than 128 attributes keep 44.
+//    Schemas of 129-256 attributes keep 44; wider ones (up to the reference's
+//    65535) take the wide kernel (300, hdx_wide.hip), whose attribute classes
+//    come from device memory.
 static int auto_variant(const BatchArgs& args) {
+    if (args.A > kKernargCodes) return 300;  // hdx_wide.hip
     uint32_t numeric = 0;
     bool complex_types = false;
     for (uint32_t j = 0; j < args.A; ++j) {
@@ -150,7 +170,7 @@ void finalize_args(BatchArgs& args) {
     args.inv_A = 1.0 / (double)args.A;
     args.a_magic = (uint32_t)(((1ull << 31) + args.A - 1) / args.A);
     args.uniform_code = args.codes[0];
-    for (uint32_t j = 1; j < args.A; ++j)
+    for (uint32_t j = 1; j < std::min(args.A, kKernargCodes); ++j)
         if (args.codes[j] != args.codes[0]) args.uniform_code = 0xffu;
 }
 
@@ -183,6 +203,7 @@ const char* variant_kernel_name(int v) {
         case 44: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true, 1>(hdx::BatchArgs)";
         case 45: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true, 2>(hdx::BatchArgs)";
         case 46: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, true, 1>(hdx::BatchArgs)";
+        case 300: return "hdx::hash_wide_kernel(hdx::BatchArgs)";
         case 212: return "void hdx::hash_wstage_kernel<2, 8832u, 0, 5, 4, 0, false, true, true, true, false>(hdx::BatchArgs)";
         default: return "";
     }

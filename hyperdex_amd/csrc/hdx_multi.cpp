@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "hdx_cuts.h"
+#include "hdx_exchange.h"
 #include "hdx_host.h"
 
 namespace hdx {
@@ -42,12 +43,15 @@ namespace hdx {
 class Worker {
 public:
     Worker() : th_([this] { run(); }) {}
-    void post(std::function<void()> job) {
+    // false once join() has begun: the job will never run
+    bool post(std::function<void()> job) {
         {
             std::lock_guard<std::mutex> lk(mu_);
+            if (stop_) return false;
             q_.push_back(std::move(job));
         }
         cv_.notify_one();
+        return true;
     }
     void join() {
         {
@@ -102,15 +106,50 @@ private:
 
 struct DeviceSet {
     uint64_t mask = 0;
-    std::vector<int> devs;                        // ascending HIP ordinals
+    std::vector<int> devs;                        // ascending HIP ordinals (debug: any list)
     std::vector<std::unique_ptr<Worker>> workers;  // one per device: the host path
     std::vector<hipStream_t> streams;             // one per device: device-resident shards
     std::vector<ncclComm_t> comms;                // created on the first gather
     std::mutex call_mu;                           // one device-resident multi call at a time
+    // calls in progress (SetRef): teardown waits for them, so hdx_init_mask /
+    // hdx_shutdown from another thread never frees a set in use
+    std::mutex ref_mu;
+    std::condition_variable ref_cv;
+    uint64_t inflight = 0;
 };
 
 static std::mutex g_set_mu;
-static DeviceSet* g_set = nullptr;
+static std::shared_ptr<DeviceSet> g_set;
+
+// A call's hold on the set (empty without one).
+class SetRef {
+public:
+    SetRef() = default;
+    explicit SetRef(std::shared_ptr<DeviceSet> d) : ds_(std::move(d)) {
+        if (ds_) {
+            std::lock_guard<std::mutex> lk(ds_->ref_mu);
+            ++ds_->inflight;
+        }
+    }
+    SetRef(const SetRef&) = delete;
+    SetRef& operator=(const SetRef&) = delete;
+    ~SetRef() {
+        if (!ds_) return;
+        std::lock_guard<std::mutex> lk(ds_->ref_mu);
+        if (--ds_->inflight == 0) ds_->ref_cv.notify_all();
+    }
+    DeviceSet* get() const { return ds_.get(); }
+    DeviceSet* operator->() const { return ds_.get(); }
+    explicit operator bool() const { return (bool)ds_; }
+
+private:
+    std::shared_ptr<DeviceSet> ds_;
+};
+
+static std::unique_ptr<SetRef> acquire_set() {
+    std::lock_guard<std::mutex> lk(g_set_mu);  // the count is taken before teardown can see the set go
+    return std::unique_ptr<SetRef>(new SetRef(g_set));
+}
 
 static void destroy_set(DeviceSet* ds) {
     if (!ds) return;
@@ -126,23 +165,28 @@ static void destroy_set(DeviceSet* ds) {
         (void)hipSetDevice(ds->devs[k]);
         (void)ncclCommDestroy(ds->comms[k]);
     }
+    ds->comms.clear();
     for (size_t k = 0; k < ds->streams.size(); ++k) {
         if (!ds->streams[k]) continue;
         (void)hipSetDevice(ds->devs[k]);
         (void)hipStreamSynchronize(ds->streams[k]);
         (void)hipStreamDestroy(ds->streams[k]);
     }
-    delete ds;
+    ds->streams.clear();
 }
 
 void device_set_teardown() {
-    DeviceSet* ds;
+    std::shared_ptr<DeviceSet> ds;
     {
         std::lock_guard<std::mutex> lk(g_set_mu);
-        ds = g_set;
-        g_set = nullptr;
+        ds.swap(g_set);
     }
-    destroy_set(ds);
+    if (!ds) return;
+    {
+        std::unique_lock<std::mutex> lk(ds->ref_mu);
+        ds->ref_cv.wait(lk, [&] { return ds->inflight == 0; });
+    }
+    destroy_set(ds.get());
 }
 
 hdx_status device_set_create(uint64_t mask, const std::vector<int>& devs) {
@@ -150,10 +194,10 @@ hdx_status device_set_create(uint64_t mask, const std::vector<int>& devs) {
         std::lock_guard<std::mutex> lk(g_set_mu);
         if (g_set && g_set->mask == mask && g_set->devs == devs) return HDX_OK;
     }
-    device_set_teardown();  // a different mask replaces the set (no call may be in progress)
+    device_set_teardown();  // a different mask replaces the set (after the calls in progress)
     int cur = -1;
     const bool had = hipGetDevice(&cur) == hipSuccess;
-    auto* ds = new DeviceSet();
+    auto ds = std::make_shared<DeviceSet>();
     ds->mask = mask;
     ds->devs = devs;
     ds->streams.assign(devs.size(), nullptr);
@@ -161,7 +205,7 @@ hdx_status device_set_create(uint64_t mask, const std::vector<int>& devs) {
         if (hipSetDevice(devs[k]) != hipSuccess ||
             hipStreamCreateWithFlags(&ds->streams[k], hipStreamNonBlocking) != hipSuccess) {
             const hipError_t e = hipGetLastError();
-            destroy_set(ds);
+            destroy_set(ds.get());
             if (had) (void)hipSetDevice(cur);
             return fail(HDX_E_DEVICE, "device %d: stream creation failed: %s", devs[k], hipGetErrorString(e));
         }
@@ -171,11 +215,6 @@ hdx_status device_set_create(uint64_t mask, const std::vector<int>& devs) {
     std::lock_guard<std::mutex> lk(g_set_mu);
     g_set = ds;
     return HDX_OK;
-}
-
-static DeviceSet* current_set() {
-    std::lock_guard<std::mutex> lk(g_set_mu);
-    return g_set;
 }
 
 // Restores the caller's HIP device on scope exit.
@@ -189,21 +228,48 @@ struct DeviceGuard {
     }
 };
 
-// ---- host-resident batch over the set ------------------------------------------
+// ---- host-resident calls over the set ---------------------------------------------
 
-// Runs one job per device on the workers; returns the first failing device's
-// status (in device order) with that worker's message.
-static hdx_status run_on_workers(DeviceSet* ds, const std::function<hdx_status(size_t k)>& job) {
+// The set index whose device the calling thread is bound to (or, unbound,
+// would bind to: its current HIP device), else -1.
+static int caller_slot(const DeviceSet* ds) {
+    int d = thread_device();
+    if (d < 0 && hipGetDevice(&d) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1;
+    }
+    for (size_t k = 0; k < ds->devs.size(); ++k)
+        if (ds->devs[k] == d) return (int)k;
+    return -1;
+}
+
+// Runs job(k) for every device of the set: the calling thread runs its own
+// device's share itself (no hand-off, and concurrent callers keep
+// their own pipelines), the workers the others.  Returns the first failing
+// device's status (in device order) with that device named.
+static hdx_status run_on_set(DeviceSet* ds, const std::function<hdx_status(size_t k)>& job) {
     const size_t nd = ds->devs.size();
     std::vector<hdx_status> st(nd, HDX_OK);
     std::vector<std::string> msg(nd);
-    Latch latch(nd);
+    const int mine = caller_slot(ds);
+    Latch latch(nd - (mine >= 0 ? 1 : 0));
     for (size_t k = 0; k < nd; ++k) {
-        ds->workers[k]->post([&, k] {
+        if ((int)k == mine) continue;
+        const bool posted = ds->workers[k]->post([&, k] {
             st[k] = job(k);
             if (st[k] != HDX_OK) msg[k] = hdx_last_error();
             latch.done();
         });
+        if (!posted) {
+            st[k] = HDX_E_DEVICE;
+            msg[k] = "the device set is being torn down";
+            latch.done();
+        }
+    }
+    if (mine >= 0) {
+        DeviceGuard guard;
+        st[mine] = job((size_t)mine);
+        if (st[mine] != HDX_OK) msg[mine] = hdx_last_error();
     }
     latch.wait();
     for (size_t k = 0; k < nd; ++k)
@@ -211,37 +277,93 @@ static hdx_status run_on_workers(DeviceSet* ds, const std::function<hdx_status(s
     return HDX_OK;
 }
 
-bool host_batch_uses_set() { return current_set() != nullptr; }
-
-hdx_status hash_host_set(const uint8_t* codes, uint32_t A, const uint8_t* blob, uint64_t blob_bytes,
-                         const uint64_t* obj_base, const uint32_t* attr_len, uint64_t n, uint64_t* coords) {
-    DeviceSet* ds = current_set();
-    if (!ds) return fail(HDX_E_INVALID, "no device set (hdx_init_mask)");
+// Byte-balanced cuts of n objects over the set (hdx_cuts.h), the block sums
+// of the prefix computed by the set's threads in parallel.
+template <typename Sizes>
+static hdx_status set_cuts(DeviceSet* ds, const Sizes& size, uint64_t n, std::vector<uint64_t>& first) {
     const uint32_t world = (uint32_t)ds->devs.size();
-    std::vector<uint64_t> first(world + 1);
-    if (world == 1) {
-        first[0] = 0;
-        first[1] = n;
-    } else {
-        Prefix p{attr_len, A, n, {}};
-        const uint64_t blocks = (n + kCutBlock - 1) / kCutBlock;
-        std::vector<uint64_t> bsum(blocks);
-        hdx_status st = run_on_workers(ds, [&](size_t k) {
-            for (uint64_t b = blocks * k / world; b < blocks * (k + 1) / world; ++b)
-                bsum[b] = block_bytes(attr_len, A, n, b);
-            return HDX_OK;
-        });
-        if (st != HDX_OK) return st;
-        p.bprefix.assign(blocks + 1, 0);
-        for (uint64_t b = 0; b < blocks; ++b) p.bprefix[b + 1] = p.bprefix[b] + bsum[b];
-        cuts_from_prefix(p, world, 0.0, first.data());
-    }
-    return run_on_workers(ds, [&](size_t k) -> hdx_status {
+    first.assign(world + 1, 0);
+    first[world] = n;
+    if (world == 1) return HDX_OK;
+    PrefixOf<Sizes> p{size, n, {}};
+    const uint64_t blocks = (n + kCutBlock - 1) / kCutBlock;
+    std::vector<uint64_t> bsum(blocks);
+    hdx_status st = run_on_set(ds, [&](size_t k) {
+        for (uint64_t b = blocks * k / world; b < blocks * (k + 1) / world; ++b) bsum[b] = block_bytes(size, n, b);
+        return HDX_OK;
+    });
+    if (st != HDX_OK) return st;
+    p.bprefix.assign(blocks + 1, 0);
+    for (uint64_t b = 0; b < blocks; ++b) p.bprefix[b + 1] = p.bprefix[b] + bsum[b];
+    cuts_from_prefix(p, world, 0.0, first.data());
+    return HDX_OK;
+}
+
+static HostRegions range_regions(const HostRegions* R, uint64_t f) {
+    return R ? HostRegions{R->tables, R->T, R->ids + f, R->stride} : HostRegions{nullptr, 0, nullptr, 0};
+}
+
+hdx_status hash_host_any(const uint8_t* codes, uint32_t A, const uint8_t* blob, uint64_t blob_bytes,
+                         const uint64_t* obj_base, const uint32_t* attr_len, uint64_t n, uint64_t* coords,
+                         const HostRegions* R) {
+    std::unique_ptr<SetRef> ref = acquire_set();
+    DeviceSet* ds = ref->get();
+    if (!ds) return hash_host(codes, A, blob, blob_bytes, obj_base, attr_len, n, coords, R);
+    std::vector<uint64_t> first;
+    hdx_status st = set_cuts(ds, PackedSizes{attr_len, A}, n, first);
+    if (st != HDX_OK) return st;
+    return run_on_set(ds, [&](size_t k) -> hdx_status {
         const uint64_t f = first[k], cnt = first[k + 1] - first[k];
         if (cnt == 0) return HDX_OK;
         hdx_status s = bind_device(ds->devs[k]);
         if (s != HDX_OK) return s;
-        return hash_host(codes, A, blob, blob_bytes, obj_base + f, attr_len + f * A, cnt, coords + f * A);
+        const HostRegions Rk = range_regions(R, f);
+        return hash_host(codes, A, blob, blob_bytes, obj_base + f, attr_len + f * A, cnt,
+                         coords ? coords + f * A : nullptr, R ? &Rk : nullptr);
+    });
+}
+
+// One range of stored objects: the pipeline, then its status words as a
+// status (a mis-sized numeric before an undecodable value: the reference
+// asserts on the former).
+static hdx_status encoded_range(const uint8_t* codes, uint32_t A, const uint8_t* keys, uint64_t keys_bytes,
+                                const uint64_t* key_off, const uint32_t* key_len, const uint8_t* vals,
+                                uint64_t vals_bytes, const uint64_t* val_off, const uint32_t* val_len, uint64_t f,
+                                uint64_t cnt, uint64_t* coords, uint64_t* versions, const HostRegions* R) {
+    uint32_t bits = 0;
+    const HostRegions Rk = range_regions(R, f);
+    hdx_status st = hash_encoded_host(codes, A, keys, keys_bytes, key_off + f, key_len + f, vals, vals_bytes,
+                                      val_off + f, val_len + f, cnt, coords ? coords + f * A : nullptr,
+                                      versions ? versions + f : nullptr, R ? &Rk : nullptr, &bits);
+    if (st != HDX_OK) return st;
+    if (bits & (1u << HDX_E_BADSIZE))
+        return fail(HDX_E_BADSIZE, "objects [%llu, %llu): a numeric value of neither 0 nor 8 bytes (coordinate 0)",
+                    (unsigned long long)f, (unsigned long long)(f + cnt));
+    if (bits & (1u << HDX_E_BADENC))
+        return fail(HDX_E_BADENC, "objects [%llu, %llu): a value does not decode (zero coordinates, version 0)",
+                    (unsigned long long)f, (unsigned long long)(f + cnt));
+    return HDX_OK;
+}
+
+hdx_status hash_encoded_host_any(const uint8_t* codes, uint32_t A, const uint8_t* keys, uint64_t keys_bytes,
+                                 const uint64_t* key_off, const uint32_t* key_len, const uint8_t* vals,
+                                 uint64_t vals_bytes, const uint64_t* val_off, const uint32_t* val_len, uint64_t n,
+                                 uint64_t* coords, uint64_t* versions, const HostRegions* R) {
+    std::unique_ptr<SetRef> ref = acquire_set();
+    DeviceSet* ds = ref->get();
+    if (!ds)
+        return encoded_range(codes, A, keys, keys_bytes, key_off, key_len, vals, vals_bytes, val_off, val_len, 0, n,
+                             coords, versions, R);
+    std::vector<uint64_t> first;
+    hdx_status st = set_cuts(ds, StoredSizes{key_len, val_len}, n, first);
+    if (st != HDX_OK) return st;
+    return run_on_set(ds, [&](size_t k) -> hdx_status {
+        const uint64_t f = first[k], cnt = first[k + 1] - first[k];
+        if (cnt == 0) return HDX_OK;
+        hdx_status s = bind_device(ds->devs[k]);
+        if (s != HDX_OK) return s;
+        return encoded_range(codes, A, keys, keys_bytes, key_off, key_len, vals, vals_bytes, val_off, val_len, f, cnt,
+                             coords, versions, R);
     });
 }
 
@@ -261,7 +383,8 @@ HDX_EXPORT hdx_status hdx_shard_ranges(const uint32_t* attr_len, uint32_t attrs_
 }
 
 HDX_EXPORT int hdx_device_set(int* devices, int max_devices) {
-    DeviceSet* ds = current_set();
+    std::unique_ptr<SetRef> ref = acquire_set();
+    DeviceSet* ds = ref->get();
     if (!ds) return 0;
     const int nd = (int)ds->devs.size();
     for (int k = 0; k < nd && k < max_devices && devices; ++k) devices[k] = ds->devs[k];
@@ -269,12 +392,6 @@ HDX_EXPORT int hdx_device_set(int* devices, int max_devices) {
 }
 
 static const char* nccl_text(ncclResult_t r) { return ncclGetErrorString(r); }
-
-#define NCCL_TRY(expr)                                                             \
-    do {                                                                           \
-        ncclResult_t r_ = (expr);                                                  \
-        if (r_ != ncclSuccess) return fail(HDX_E_DEVICE, "%s: %s", #expr, nccl_text(r_)); \
-    } while (0)
 
 // A device pointer must live on the device its shard runs on (a kernel on
 // another device would read through the fabric or fault).  Host (pinned)
@@ -292,99 +409,151 @@ static hdx_status check_on_device(const void* p, int dev, uint32_t k, const char
     return HDX_OK;
 }
 
-HDX_EXPORT hdx_status hdx_hash_batch_device_multi(const uint32_t* types, uint32_t attrs_sz, const hdx_shard* shards,
-                                                  uint32_t nshards, int gather) {
-    uint8_t codes[HDX_MAX_ATTRS];
-    hdx_status st = check_schema(types, attrs_sz, codes);
+namespace {
+// One device's shard as the core below takes it (hdx_shard / hdx_region_shard).
+struct MultiShard {
+    const uint8_t* blob;
+    const uint64_t* obj_base;
+    const uint32_t* attr_len;
+    uint64_t n;
+    uint64_t* coords;  // the gathered matrix (T == 0, gather) or this shard's rows; may be NULL when T > 0
+    uint64_t* ids;     // T > 0: T sections of N (gather) or of n region ids
+    uint32_t* status;
+};
+}  // namespace
+
+// hdx_hash_batch_device_multi (T == 0) and hdx_hash_batch_regions_device_multi:
+// every argument validated, the communicator created and the kernel
+// arguments (replicas, code tables) prepared before the first launch; after
+// it, any failure waits for every device's stream before returning (ADVICE
+// r4), so no kernel or collective still writes the caller's memory.
+static hdx_status device_multi(const uint32_t* types, uint32_t A, const std::vector<MultiShard>& sh,
+                               const hdx_region_table* tables, uint32_t T, int gather) {
+    std::vector<uint8_t> codes(A ? A : 1);
+    hdx_status st = check_schema(types, A, codes.data());
     if (st != HDX_OK) return st;
-    DeviceSet* ds = current_set();
+    // the tables (each shard's region_ids pointer is checked with the shard)
+    if ((st = check_tables(tables, T, A, T ? (const uint64_t*)&T : nullptr)) != HDX_OK) return st;
+    std::unique_ptr<SetRef> ref = acquire_set();
+    DeviceSet* ds = ref->get();
     if (!ds) return fail(HDX_E_INVALID, "no device set: call hdx_init_mask first");
-    if (!shards || nshards != ds->devs.size())
-        return fail(HDX_E_INVALID, "%u shards for a device set of %zu devices", nshards, ds->devs.size());
+    const uint32_t world = (uint32_t)ds->devs.size();
+    if (sh.size() != world) return fail(HDX_E_INVALID, "%zu shards for a device set of %u devices", sh.size(), world);
     uint64_t total = 0;
-    for (uint32_t k = 0; k < nshards; ++k) total += shards[k].n;
+    std::vector<uint64_t> counts(world);
+    for (uint32_t k = 0; k < world; ++k) total += counts[k] = sh[k].n;
     if (total == 0) return HDX_OK;
-    for (uint32_t k = 0; k < nshards; ++k) {
-        const hdx_shard& s = shards[k];
-        if (s.n && (!s.blob || !s.obj_base || !s.attr_len || !s.coords))
+    for (uint32_t k = 0; k < world; ++k) {
+        const MultiShard& s = sh[k];
+        if (s.n && (!s.blob || !s.obj_base || !s.attr_len || (!T && !s.coords) || (T && !s.ids)))
             return fail(HDX_E_INVALID, "shard %u: NULL device pointer", k);
-        if (gather && !s.coords) return fail(HDX_E_INVALID, "shard %u: NULL coords", k);
+        if (gather && !(T ? s.ids : s.coords)) return fail(HDX_E_INVALID, "shard %u: NULL %s", k, T ? "region_ids" : "coords");
         const int dev = ds->devs[k];
         if ((st = check_on_device(s.blob, dev, k, "blob")) != HDX_OK ||
             (st = check_on_device(s.obj_base, dev, k, "obj_base")) != HDX_OK ||
             (st = check_on_device(s.attr_len, dev, k, "attr_len")) != HDX_OK ||
             (st = check_on_device(s.coords, dev, k, "coords")) != HDX_OK ||
-            (st = check_on_device(s.status_dev, dev, k, "status_dev")) != HDX_OK)
+            (st = check_on_device(s.ids, dev, k, "region_ids")) != HDX_OK ||
+            (st = check_on_device(s.status, dev, k, "status_dev")) != HDX_OK)
             return st;
     }
-    DeviceGuard guard;
-    std::lock_guard<std::mutex> call(ds->call_mu);
-    // hash: each shard into its rows of its device's matrix (gather) or into
-    // its own coords (no gather)
-    uint64_t row = 0;
-    for (uint32_t k = 0; k < nshards; ++k) {
-        const hdx_shard& s = shards[k];
-        if (s.n) {
-            HIP_TRY(hipSetDevice(ds->devs[k]));
-            BatchArgs args{};
-            std::memcpy(args.codes, codes, attrs_sz);
-            args.blob = s.blob;
-            args.obj_base = s.obj_base;
-            args.attr_len = s.attr_len;
-            args.coords = s.coords + (gather ? row * attrs_sz : 0);
-            args.status = s.status_dev;
-            args.n = s.n;
-            args.A = attrs_sz;
-            finalize_args(args);
-            HIP_TRY(launch_hash_batch(args, ds->streams[k]));
-        }
-        row += s.n;
-    }
-    if (gather) {
-        for (uint32_t k = 1; k < nshards; ++k)
+    if (gather)
+        for (uint32_t k = 1; k < world; ++k)
             for (uint32_t j = 0; j < k; ++j)
                 if (ds->devs[j] == ds->devs[k])  // hdxdbg_init_devices: no communicator over one GPU twice
                     return fail(HDX_E_INVALID, "device %d twice in the set: no RCCL gather", ds->devs[k]);
-        if (ds->comms.empty()) {
-            ds->comms.resize(nshards);
-            ncclResult_t r = ncclCommInitAll(ds->comms.data(), (int)nshards, ds->devs.data());
-            if (r != ncclSuccess) {
-                ds->comms.clear();
-                return fail(HDX_E_DEVICE, "ncclCommInitAll over %u devices: %s", nshards, nccl_text(r));
+    DeviceGuard guard;
+    std::lock_guard<std::mutex> call(ds->call_mu);
+    if (gather && ds->comms.empty()) {
+        ds->comms.resize(world);
+        const ncclResult_t r = ncclCommInitAll(ds->comms.data(), (int)world, ds->devs.data());
+        if (r != ncclSuccess) {
+            ds->comms.clear();
+            return fail(HDX_E_DEVICE, "ncclCommInitAll over %u devices: %s", world, nccl_text(r));
+        }
+    }
+    // kernel arguments: shard k's rows [first_k, first_k + n_k) of its
+    // device's matrix (gather), else its own rows
+    std::vector<BatchArgs> args(world);
+    uint64_t row = 0;
+    for (uint32_t k = 0; k < world; ++k) {
+        const MultiShard& s = sh[k];
+        if (s.n) {
+            if (hipSetDevice(ds->devs[k]) != hipSuccess) return hip_fail(hipGetLastError(), "hipSetDevice");
+            uint64_t* coords = s.coords ? s.coords + (gather && !T ? row * A : 0) : nullptr;
+            uint64_t* ids = T ? s.ids + (gather ? row : 0) : nullptr;
+            if ((st = batch_args(args[k], codes.data(), A, s.blob, s.obj_base, s.attr_len, s.n, coords, s.status,
+                                 tables, T, ids, gather ? total : s.n, ds->devs[k])) != HDX_OK)
+                return st;
+        }
+        row += s.n;
+    }
+    auto sync_all = [&]() {
+        hipError_t first_err = hipSuccess;
+        for (uint32_t k = 0; k < world; ++k) {
+            const hipError_t e = hipSetDevice(ds->devs[k]) == hipSuccess ? hipStreamSynchronize(ds->streams[k])
+                                                                         : hipGetLastError();
+            if (first_err == hipSuccess) first_err = e;
+        }
+        return first_err;
+    };
+    for (uint32_t k = 0; k < world; ++k) {
+        if (!sh[k].n) continue;
+        hipError_t e = hipSetDevice(ds->devs[k]);
+        if (e == hipSuccess)
+            e = T ? launch_hash_batch_regions(args[k], ds->streams[k]) : launch_hash_batch(args[k], ds->streams[k]);
+        if (e != hipSuccess) {
+            (void)sync_all();
+            return hip_fail(e, T ? "launch_hash_batch_regions" : "launch_hash_batch");
+        }
+    }
+    if (gather) {
+        // the exchange (hdx_exchange.h): coordinates are one section of N * A
+        // elements, region ids one section of N per table
+        const std::vector<ExchangeOp> plan =
+            T ? exchange_plan(counts.data(), world, 1, T, total) : exchange_plan(counts.data(), world, A, 1, total * A);
+        ncclResult_t r = ncclGroupStart();
+        const ncclResult_t r0 = r;
+        for (const ExchangeOp& op : plan) {
+            for (uint32_t k = 0; k < world && r == ncclSuccess; ++k) {
+                uint64_t* m = (T ? sh[k].ids : sh[k].coords) + op.offset;
+                r = op.kind == ExchangeOp::kAllGather
+                        ? ncclAllGather(m + (size_t)k * op.count, m, op.count, ncclUint64, ds->comms[k], ds->streams[k])
+                        : ncclBroadcast(m, m, op.count, ncclUint64, (int)op.root, ds->comms[k], ds->streams[k]);
             }
         }
-        bool equal = true;
-        for (uint32_t k = 1; k < nshards; ++k) equal = equal && shards[k].n == shards[0].n;
-        // one RCCL group: an in-place all-gather for equal counts, else one
-        // in-place broadcast per shard (no staging matrix; hyperdex_amd/dist.py
-        // pads instead because torch has no grouped broadcast over unequal rows)
-        NCCL_TRY(ncclGroupStart());
-        ncclResult_t r = ncclSuccess;  // the group is closed whatever happens inside it
-        if (equal) {
-            const size_t cnt = (size_t)shards[0].n * attrs_sz;
-            for (uint32_t k = 0; k < nshards && r == ncclSuccess; ++k)
-                r = ncclAllGather(shards[k].coords + (size_t)k * cnt, shards[k].coords, cnt, ncclUint64,
-                                  ds->comms[k], ds->streams[k]);
-        } else {
-            uint64_t first = 0;
-            for (uint32_t src = 0; src < nshards && r == ncclSuccess; ++src) {
-                const size_t cnt = (size_t)shards[src].n * attrs_sz;
-                for (uint32_t k = 0; cnt && k < nshards && r == ncclSuccess; ++k) {
-                    uint64_t* rows = shards[k].coords + first * attrs_sz;
-                    r = ncclBroadcast(rows, rows, cnt, ncclUint64, (int)src, ds->comms[k], ds->streams[k]);
-                }
-                first += shards[src].n;
-            }
+        const ncclResult_t e = r0 == ncclSuccess ? ncclGroupEnd() : r0;  // the group is closed whatever happened in it
+        if (r != ncclSuccess || e != ncclSuccess) {
+            (void)sync_all();
+            return fail(HDX_E_DEVICE, "RCCL gather: %s", nccl_text(r != ncclSuccess ? r : e));
         }
-        const ncclResult_t e = ncclGroupEnd();
-        if (r != ncclSuccess) return fail(HDX_E_DEVICE, "RCCL gather: %s", nccl_text(r));
-        if (e != ncclSuccess) return fail(HDX_E_DEVICE, "ncclGroupEnd: %s", nccl_text(e));
     }
-    for (uint32_t k = 0; k < nshards; ++k) {
-        HIP_TRY(hipSetDevice(ds->devs[k]));
-        HIP_TRY(hipStreamSynchronize(ds->streams[k]));
-    }
+    const hipError_t e = sync_all();
+    if (e != hipSuccess) return hip_fail(e, "hipStreamSynchronize");
     return HDX_OK;
+}
+
+HDX_EXPORT hdx_status hdx_hash_batch_device_multi(const uint32_t* types, uint32_t attrs_sz, const hdx_shard* shards,
+                                                  uint32_t nshards, int gather) {
+    if (!shards && nshards) return fail(HDX_E_INVALID, "shards is NULL");
+    std::vector<MultiShard> sh(nshards);
+    for (uint32_t k = 0; k < nshards; ++k)
+        sh[k] = {shards[k].blob, shards[k].obj_base, shards[k].attr_len, shards[k].n, shards[k].coords, nullptr,
+                 shards[k].status_dev};
+    return device_multi(types, attrs_sz, sh, nullptr, 0, gather);
+}
+
+HDX_EXPORT hdx_status hdx_hash_batch_regions_device_multi(const uint32_t* types, uint32_t attrs_sz,
+                                                          const hdx_region_shard* shards, uint32_t nshards,
+                                                          const hdx_region_table* tables, uint32_t ntables,
+                                                          int gather) {
+    if (ntables == 0) return fail(HDX_E_INVALID, "no region tables");
+    if (!shards && nshards) return fail(HDX_E_INVALID, "shards is NULL");
+    std::vector<MultiShard> sh(nshards);
+    for (uint32_t k = 0; k < nshards; ++k)
+        sh[k] = {shards[k].blob, shards[k].obj_base, shards[k].attr_len, shards[k].n, shards[k].coords,
+                 shards[k].region_ids, shards[k].status_dev};
+    return device_multi(types, attrs_sz, sh, tables, ntables, gather);
 }
 
 #if HDX_DEBUG_BUILD

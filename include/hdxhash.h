@@ -27,7 +27,8 @@
  *   attr_len[n*A]   u32 length of attribute j of object i at [i*A + j]
  *   coords[n*A]     u64 output, row-major: coords[i*A + j] = hash of attr j
  *                   (= hs[j] of the reference's whole-object hash)
- * Limits: 1 <= A <= HDX_MAX_ATTRS; each object's attributes total < 4 GiB.
+ * Limits: 1 <= A <= HDX_MAX_ATTRS (65535, the reference's u16 attrs_sz);
+ * each object's attributes total < 4 GiB.
  *
  * Errors: the reference asserts on an unknown type (hash.cc:38) and on an
  * int64/float/timestamp value whose size is not 0 or 8
@@ -56,8 +57,9 @@
 extern "C" {
 #endif
 
-#define HDX_ABI_VERSION 3
-#define HDX_MAX_ATTRS 256
+#define HDX_ABI_VERSION 4
+/* The reference's schema::attrs_sz is a u16 (common/schema.h:49). */
+#define HDX_MAX_ATTRS 65535
 
 typedef enum hdx_status {
     HDX_OK = 0,
@@ -71,6 +73,8 @@ typedef enum hdx_status {
 
 /* An opaque hipStream_t.  NULL is the HIP null (default) stream. */
 typedef void* hdx_stream;
+/* A subspace's region table (hdx_region_table_create, below). */
+typedef struct hdx_region_table_s* hdx_region_table;
 
 /* ---- library state ---------------------------------------------------- */
 
@@ -133,7 +137,8 @@ hdx_status hdx_hash_batch_device(const uint32_t* types, uint32_t attrs_sz,
                                  hdx_stream stream);
 
 /* Same batch with every array in HOST memory (pageable or pinned).
- * Synchronous.  The library streams the batch through the device in chunks,
+ * Synchronous.  Any thread; the calling thread runs its own device's share
+ * itself.  The library streams the batch through the device in chunks,
  * overlapping H2D copies, kernels and D2H copies on two streams, and
  * validates numeric sizes and object extents on the host chunk by chunk
  * ahead of the copies.  blob_bytes is the size of the blob allocation (every
@@ -149,6 +154,20 @@ hdx_status hdx_hash_batch_host(const uint32_t* types, uint32_t attrs_sz,
                                const uint8_t* blob, uint64_t blob_bytes,
                                const uint64_t* obj_base, const uint32_t* attr_len,
                                uint64_t n, uint64_t* coords);
+
+/* The same host-resident batch for the ingest path: every object's region in
+ * ntables (1..4) subspaces, region_ids[t*n + i] = lookup_region(tables[t],
+ * hash(schema, key, value) of object i) — the values hdx_lookup_region_device
+ * gives on hdx_hash_batch_host's coordinates — with only 8 bytes per table
+ * per object crossing PCIe back (key_state::hash_objects consumes only
+ * regions, daemon/key_state.cc:1482-1534).  coords (host, may be NULL) also
+ * receives the coordinates.  Split over the device set like
+ * hdx_hash_batch_host; the tables are replicated to each device on first use.
+ * Synchronous. */
+hdx_status hdx_hash_batch_regions_host(const uint32_t* types, uint32_t attrs_sz, const uint8_t* blob,
+                                       uint64_t blob_bytes, const uint64_t* obj_base, const uint32_t* attr_len,
+                                       uint64_t n, const hdx_region_table* tables, uint32_t ntables,
+                                       uint64_t* region_ids, uint64_t* coords);
 
 /* ---- multi-device (the device set of hdx_init_mask) ---------------------- */
 
@@ -186,6 +205,26 @@ typedef struct hdx_shard {
 hdx_status hdx_hash_batch_device_multi(const uint32_t* types, uint32_t attrs_sz, const hdx_shard* shards,
                                        uint32_t nshards, int gather);
 
+/* The region-id form of the same: each shard is hashed and
+ * looked up in ntables (1..4) region tables on its device; with gather, ONLY
+ * the region ids are exchanged — 8 bytes per table per object instead of the
+ * 8 * attrs_sz of the coordinates (config 3b: 16 vs 136 bytes with two
+ * tables).  The tables are replicated to each device on first use. */
+typedef struct hdx_region_shard {
+    const uint8_t* blob;
+    const uint64_t* obj_base;
+    const uint32_t* attr_len;
+    uint64_t n;
+    uint64_t* region_ids;       /* gather: ntables x N on this device, table t's id of object i at
+                                   [t*N + i] (N = the shards' total); else ntables x n, [t*n + i] */
+    uint64_t* coords;           /* may be NULL: this shard's own (n x attrs_sz) coordinates,
+                                   never exchanged */
+    uint32_t* status_dev;       /* may be NULL; as hdx_hash_batch_device */
+} hdx_region_shard;
+hdx_status hdx_hash_batch_regions_device_multi(const uint32_t* types, uint32_t attrs_sz,
+                                               const hdx_region_shard* shards, uint32_t nshards,
+                                               const hdx_region_table* tables, uint32_t ntables, int gather);
+
 /* Reindex sweep over stored objects: value i is
  * vals[val_off[i], +val_len[i]) in the daemon's on-disk encoding
  * [u64 BE version][u16 BE count]{[u32 BE len][bytes]}*count
@@ -200,13 +239,42 @@ hdx_status hdx_hash_batch_device_multi(const uint32_t* types, uint32_t attrs_sz,
  * inside the value (:201-213); this does.  Any placement of keys and values
  * is exact; keys back to back, values back to back, or — keys == vals —
  * records [key][value] back to back are read with coalesced span copies.
- * Device pointers, asynchronous; attrs_sz <= 128. */
+ * Device pointers, asynchronous.  Any attrs_sz up to HDX_MAX_ATTRS (above 128
+ * a wave per object, hdx_wide.hip). */
 hdx_status hdx_hash_encoded_device(const uint32_t* types, uint32_t attrs_sz,
                                    const uint8_t* keys, const uint64_t* key_off,
                                    const uint32_t* key_len, const uint8_t* vals,
                                    const uint64_t* val_off, const uint32_t* val_len,
                                    uint64_t n, uint64_t* coords, uint64_t* versions,
                                    uint32_t* status_dev, hdx_stream stream);
+
+/* The reindex sweep from HOST memory (datalayer::indexer_thread reads the
+ * region's stored objects from LevelDB into host buffers, daemon/
+ * datalayer_indexer_thread.cc:161-176, daemon/datalayer.cc:853-882): the
+ * arrays of hdx_hash_encoded_device, all in host memory (pageable or pinned),
+ * keys_bytes / vals_bytes the sizes of the two stores (keys == vals: records
+ * [key][value] in one store).  The call is cut into contiguous object ranges
+ * balanced by key + value bytes, one per device of the set (the calling
+ * thread's device without one); each device pipelines its range through PCIe
+ * in 128 MiB chunks (H2D of each chunk's key and value spans, the sweep, D2H
+ * of its coordinates and versions) into the caller's arrays.  versions may be
+ * NULL.  Synchronous.  Returns HDX_E_BADENC when a value does not decode
+ * (those objects get zero coordinates and version 0, every other object is
+ * hashed) and HDX_E_BADSIZE for a numeric value of neither 0 nor 8 bytes
+ * (coordinate 0), naming the device and the object range; HDX_E_INVALID for
+ * a key or value outside its store, before anything of its chunk is copied. */
+hdx_status hdx_hash_encoded_host(const uint32_t* types, uint32_t attrs_sz, const uint8_t* keys,
+                                 uint64_t keys_bytes, const uint64_t* key_off, const uint32_t* key_len,
+                                 const uint8_t* vals, uint64_t vals_bytes, const uint64_t* val_off,
+                                 const uint32_t* val_len, uint64_t n, uint64_t* coords, uint64_t* versions);
+/* ... and each object's region under ntables (1..4) subspaces (the
+ * indexer's purpose), region_ids[t*n + i], host memory; coords may be NULL. */
+hdx_status hdx_hash_encoded_regions_host(const uint32_t* types, uint32_t attrs_sz, const uint8_t* keys,
+                                         uint64_t keys_bytes, const uint64_t* key_off, const uint32_t* key_len,
+                                         const uint8_t* vals, uint64_t vals_bytes, const uint64_t* val_off,
+                                         const uint32_t* val_len, uint64_t n, const hdx_region_table* tables,
+                                         uint32_t ntables, uint64_t* region_ids, uint64_t* coords,
+                                         uint64_t* versions);
 
 /* ---- per-value / per-object (the reference signatures, C form) ---------- */
 
@@ -229,7 +297,6 @@ hdx_status hdx_hash_object(const uint32_t* types, uint32_t attrs_sz,
  * (common/hyperspace.h:99-113), lower/upper[regions*dims] the boxes and
  * ids[regions] the region ids (region.id, common/hyperspace.h:122-137), all
  * host arrays, copied at creation. */
-typedef struct hdx_region_table_s* hdx_region_table;
 hdx_status hdx_region_table_create(uint32_t dims, uint32_t regions, const uint16_t* attrs,
                                    const uint64_t* lower, const uint64_t* upper,
                                    const uint64_t* ids, hdx_region_table* out);
@@ -250,7 +317,7 @@ hdx_status hdx_lookup_region_device(hdx_region_table table, const uint64_t* coor
  * hdx_lookup_region_device would give on the coordinates hdx_hash_encoded_device
  * computes (an undecodable object's are zero).  coords may be NULL.  The
  * tables' subspace attributes must be < attrs_sz.  Device pointers,
- * asynchronous; attrs_sz <= 128.
+ * asynchronous; any attrs_sz (above 128 always hash + lookups).
  * Implementation note: below 2^20 objects this is one fused launch; from
  * 2^20 on, the hash and one lookup launch per table (faster there: the hash
  * kernels are VALU-bound), and with coords NULL the coordinates then pass
@@ -271,7 +338,9 @@ hdx_status hdx_hash_encoded_regions_device(const uint32_t* types, uint32_t attrs
  * hdx_lookup_region_device gives on hdx_hash_batch_device's coordinates.
  * coords may be NULL (the ingest path key_state::hash_objects -> point_leader
  * / lookup_region needs only the region).  Device pointers, asynchronous;
- * attrs_sz <= 128; status_dev (may be NULL) gets HDX_E_BADSIZE's bit for a
+ * any attrs_sz (above 128: hash + lookups, and with coords NULL the
+ * coordinates' scratch is required: HDX_E_NOMEM without it); status_dev
+ * (may be NULL) gets HDX_E_BADSIZE's bit for a
  * numeric value not 0 or 8 bytes long.  Mixed string / numeric schemas from
  * 2^20 objects on take hash + per-table lookups, with the scratch of
  * hdx_hash_encoded_regions_device's note when coords is NULL. */

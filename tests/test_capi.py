@@ -60,7 +60,7 @@ def test_product_library_has_no_knobs_or_debug_kernels():
 
 
 def test_version_and_abi():
-    assert hdx.lib().hdx_abi_version() == 3
+    assert hdx.lib().hdx_abi_version() == 4
     assert b"gfx950" in hdx.lib().hdx_version()
 
 
