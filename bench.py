@@ -284,6 +284,9 @@ def run_rank(args):
                      "kernel": hdx.hashing.kernel_for(types, n)[1]},
     }
 
+    valu = measured_valu(args.traffic, traffic_key, n, kernel_ms)
+    if valu is not None:
+        result["roofline"]["valu"] = valu
     if sp is not None:
         result["roofline"]["stream_probe"] = sp
         result["roofline"]["frac_of_probe"] = round(
@@ -309,8 +312,12 @@ def run_rank(args):
                 types, (keys, key_off, key_len, vals, val_off, val_len), n, A, dev, stream, max_over_ranks,
                 result["roofline"]["kernel_ms"], result["regions"]["lookup_ms"])
 
-    if not args.no_host_path and rank == 0 and world == 1 and cfg != "cfg5":
-        result["host_path"] = time_host_path(types, blob, base, lens, A)
+    if not args.no_host_path and rank == 0 and world == 1:
+        if cfg == "cfg5":
+            result["host_path"] = time_host_sweep(types, (keys, key_off, key_len, vals, val_off, val_len), A,
+                                                  args.store_layout, coords)
+        else:
+            result["host_path"] = time_host_path(types, blob, base, lens, A)
 
     if rank == 0 and world == 1 and cfg == "cfg3a" and not args.no_secondary:
         # BASELINE's third config with its mixed attribute types, measured the
@@ -803,6 +810,9 @@ def time_config(cfg, n, dev, stream, steps=10, warmup=2, warmup_ms=150.0):
            "GiB_s": round(payload / (ms / 1e3) / 2**30, 3), "mobjects_per_s": round(n / (ms / 1e3) / 1e6, 2),
            "kernel_ms": round(ms, 4), "roofline_frac": round(algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
            "kernel": hdx.hashing.kernel_for(types, n)[1]}
+    valu = measured_valu(latest_traffic_file(), cfg, n, ms)
+    if valu is not None:
+        res["valu"] = valu
     del blob, base, lens, coords
     torch.cuda.empty_cache()
     return res
@@ -893,6 +903,31 @@ def source_digest():
     return h.hexdigest()[:16]
 
 
+def measured_valu(path, cfg, n, kernel_ms):
+    """The VALU-issue roofline of the launch from the same
+    digest-matched PMC summary as `traffic`: SQ_INSTS_VALU per launch (scaled
+    to n) x 4 cycles (a wave64 vector instruction's issue cost on one SIMD,
+    MI355X_MICROARCH.md constants table) / (1024 SIMDs x the effective clock
+    of the PMC pass x this run's kernel time).  None when the summary has no
+    VALU record or measured other sources."""
+    try:
+        doc = json.load(open(path))
+        rec = doc[cfg]
+    except (OSError, KeyError, ValueError):
+        return None
+    if doc.get("source_digest") != source_digest() or "valu_insts" not in rec:
+        return None
+    scale = n / rec.get("objects", 10_000_000)
+    valu = rec["valu_insts"] * scale
+    clock = rec["effective_clock_ghz"] * 1e9
+    cycles = 1024 * clock * kernel_ms / 1e3
+    return {"valu_frac": round(valu * 4 / cycles, 4),
+            "valu_insts_per_launch": int(valu), "salu_insts_per_launch": int(rec["salu_insts"] * scale),
+            "valu_per_wave": round(rec["valu_per_wave"], 1), "salu_per_wave": round(rec["salu_per_wave"], 1),
+            "effective_clock_ghz": round(rec["effective_clock_ghz"], 3),
+            "convention": "SQ_INSTS_VALU x 4 cycles / (256 CUs x 4 SIMDs x effective clock x kernel time)"}
+
+
 def measured_traffic(path, cfg, n):
     """HBM bytes per launch for this config from the committed PMC summary
     (scripts/profile_r2.sh -> scripts/traffic_from_pmc.py), scaled to n, or
@@ -950,6 +985,73 @@ def time_host_path(types, blob, base, lens, A, n_host=2_000_000):
             "path": "hdx_init_mask(all visible devices) + hdx_hash_batch_host: pinned H2D, kernel, D2H"}
 
 
+def time_host_sweep(types, enc, A, layout, coords, n_host=1_000_000):
+    """Config 5 from host memory (hdx_hash_encoded_host, the indexer's entry
+    point): a pinned host copy of the first n_host objects per device of the
+    store (keys, values, offsets, lengths), swept over the device set of every
+    visible device (cut byte-balanced, one 128 MiB-chunk PCIe pipeline per
+    device), coordinates and versions back into pinned host arrays.  The
+    host coordinates are checked equal to the device-resident sweep's."""
+    import ctypes
+
+    import hyperdex_amd as hdx
+    lib = hdx.lib()
+    ndev = max(1, lib.hdx_device_count())
+    hdx.init_mask((1 << ndev) - 1)
+    devices = hdx.device_set()
+    keys, key_off, key_len, vals, val_off, val_len = enc
+    n = min(n_host * len(devices), val_off.numel())
+    ko = key_off[:n].cpu().numpy().view(np.uint64)
+    kl = key_len[:n].cpu().numpy().view(np.uint32)
+    vo = val_off[:n].cpu().numpy().view(np.uint64)
+    vl = val_len[:n].cpu().numpy().view(np.uint32)
+    kend = int((ko + kl).max())
+    vend = int((vo + vl).max())
+    records = layout == "records"
+    ptrs = {}
+    sizes = {"keys": kend, "vals": 0 if records else vend, "ko": n * 8, "kl": n * 4, "vo": n * 8, "vl": n * 4,
+             "out": n * A * 8, "ver": n * 8}
+    if records:
+        sizes["keys"] = max(kend, vend)
+    for name, nbytes in sizes.items():
+        if nbytes == 0:
+            continue
+        p = ctypes.c_void_p()
+        hdx._lib.check(lib.hdx_alloc_pinned(nbytes, ctypes.byref(p)))
+        ptrs[name] = p.value
+    srcs = [("keys", keys[:sizes["keys"]]), ("ko", ko), ("kl", kl), ("vo", vo), ("vl", vl)]
+    if not records:
+        srcs.append(("vals", vals[:vend]))
+    for name, src in srcs:
+        host = src.cpu().numpy() if hasattr(src, "cpu") else src
+        ctypes.memmove(ptrs[name], host.ctypes.data, host.nbytes)
+        del host
+    vptr, vbytes = (ptrs["keys"], sizes["keys"]) if records else (ptrs["vals"], vend)
+    t = np.array(types, np.uint32)
+
+    def call():
+        hdx._lib.check(lib.hdx_hash_encoded_host(t.ctypes.data, A, ptrs["keys"], sizes["keys"], ptrs["ko"], ptrs["kl"],
+                                                 vptr, vbytes, ptrs["vo"], ptrs["vl"], n, ptrs["out"], ptrs["ver"]))
+    call()
+    got = np.ctypeslib.as_array((ctypes.c_uint64 * (n * A)).from_address(ptrs["out"])).reshape(n, A)
+    if not np.array_equal(got, coords[:n].cpu().numpy().view(np.uint64)):
+        raise SystemExit("host_path: hdx_hash_encoded_host coordinates differ from the device-resident sweep's")
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        call()
+    dt = (time.perf_counter() - t0) / reps
+    for p in ptrs.values():
+        lib.hdx_free_pinned(p)
+    hdx.shutdown()
+    nb = int(kl.astype(np.uint64).sum()) + int(vl.astype(np.uint64).sum())
+    return {"objects": n, "devices": len(devices), "ms": round(dt * 1e3, 3),
+            "GiB_s": round(nb / dt / 2**30, 3), "GiB_s_per_device": round(nb / dt / 2**30 / len(devices), 3),
+            "mobjects_per_s": round(n / dt / 1e6, 2), "store_layout": layout,
+            "path": "hdx_init_mask(all visible devices) + hdx_hash_encoded_host: pinned H2D of key / value spans, "
+                    "sweep, D2H of coordinates and versions; equal to the device-resident sweep's coordinates"}
+
+
 def cpu_threads():
     """Every core this process may use: the affinity set, capped by the cgroup's
     CPU quota (on the GPU box 256 logical CPUs are visible but cpu.max allows
@@ -975,10 +1077,74 @@ def host_info(threads, quota):
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
+def pinned_passes(work, seconds, passes=3):
+    """Times `work` (one (prepare, run, nbytes, nobj) per thread) on threads
+    pinned one per CPU of this process's affinity set.  Each thread first
+    touches its own copy of its chunk (prepare(), on that thread: its pages
+    land on its NUMA node), then in each of `passes` passes of seconds /
+    passes every thread runs its chunk until the pass's deadline.  Returns the
+    per-pass (bytes/s, objects/s) list and the median pass.  ctypes drops the
+    GIL for each oracle call, so the threads run in parallel."""
+    import threading
+    cpus = sorted(os.sched_getaffinity(0))
+    n = len(work)
+    start = threading.Barrier(n + 1)
+    done = threading.Barrier(n + 1)
+    reps = [[0] * passes for _ in range(n)]
+    deadline = [0.0]
+    errors = []
+
+    def worker(k):
+        try:
+            os.sched_setaffinity(0, {cpus[k % len(cpus)]})  # this thread only (Linux: pid 0 = the caller)
+        except OSError:
+            pass
+        try:
+            prepare, run, _, _ = work[k]
+            state = prepare()
+            run(state)  # warm: first-call page faults and allocations stay out of the passes
+            for p in range(passes):
+                start.wait()
+                while time.perf_counter() < deadline[0]:
+                    run(state)
+                    reps[k][p] += 1
+                done.wait()
+        except threading.BrokenBarrierError:
+            pass
+        except Exception as e:  # noqa: BLE001 — re-raised on the main thread
+            errors.append(e)
+            start.abort()
+            done.abort()
+    ths = [threading.Thread(target=worker, args=(k,), daemon=True) for k in range(n)]
+    for th in ths:
+        th.start()
+    rates = []
+    try:
+        for p in range(passes):
+            deadline[0] = time.perf_counter() + seconds / passes
+            t0 = time.perf_counter()
+            start.wait()
+            done.wait()
+            dt = time.perf_counter() - t0
+            nb = sum(reps[k][p] * work[k][2] for k in range(n))
+            no = sum(reps[k][p] * work[k][3] for k in range(n))
+            rates.append((nb / dt, no / dt))
+    except threading.BrokenBarrierError:
+        pass
+    for th in ths:
+        th.join()
+    if errors:
+        raise errors[0]
+    med = sorted(rates)[len(rates) // 2]
+    return rates, med, sum(sum(r) for r in reps)
+
+
 def cpu_baseline(types, blob, base, lens, A, seconds, coords):
     """The oracle (C restatement of common/hash.cc, -O2) on this host's cores,
-    on a bounded sample of the same batch.  Also verifies the sample's GPU
-    coordinates against it (a failed check aborts the bench)."""
+    on a bounded sample of the same batch: one pinned thread per core, each
+    over its own first-touched copy of a contiguous chunk (pinned_passes),
+    median of 3 passes.  Also verifies the sample's GPU coordinates against
+    it (a failed check aborts the bench)."""
     from oracle import oracle
     threads, quota = cpu_threads()
     ns = min(200_000, base.numel())
@@ -990,24 +1156,29 @@ def cpu_baseline(types, blob, base, lens, A, seconds, coords):
     got = coords[:ns].cpu().numpy().view(np.uint64)
     if err or not np.array_equal(got, want):
         raise SystemExit("cpu_baseline: GPU coordinates differ from the oracle")
+    sizes = hl.reshape(ns, A).astype(np.uint64).sum(axis=1)
+    cuts = np.linspace(0, ns, threads + 1).astype(np.int64)
 
-    def rate(nthreads, budget):
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            oracle.hash_batch(types, hb, ho, hl, nthreads=nthreads)
-            reps += 1
-            dt = time.perf_counter() - t0
-            if dt >= budget:
-                return reps * nb / dt, reps * ns / dt, reps
+    def job(c0, c1):
+        lo, hi = int(ho[c0]), int(ho[c1 - 1] + sizes[c1 - 1])
 
-    multi_b, multi_o, reps = rate(threads, seconds)
-    one_b, one_o, _ = rate(1, max(2.0, seconds / 5))
-    return {"value": round(multi_b / 2**30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "mobjects_per_s": round(multi_o / 1e6, 3),
-            "single_thread_GiB_s": round(one_b / 2**30, 3),
-            "sample": "%d objects (%.0f MB) of the same batch, %d passes, oracle/hdx_oracle.c -O2 "
-                      "pthreads; verified equal to the GPU coords" % (ns, nb / 1e6, reps),
-            **host_info(threads, quota)}
+        def prepare():  # this thread's compact copy of its objects
+            return (hb[lo:hi].copy(), (ho[c0:c1] - np.uint64(lo)).copy(), hl[c0 * A:c1 * A].copy())
+
+        def run(st):
+            oracle.hash_batch(types, st[0], st[1], st[2], nthreads=1)
+        return prepare, run, hi - lo, c1 - c0
+    work = [job(int(c0), int(c1)) for c0, c1 in zip(cuts[:-1], cuts[1:]) if c1 > c0]
+    rates, (mb, mo), reps = pinned_passes(work, seconds)
+    one, (ob, _), _ = pinned_passes(work[:1], max(1.5, seconds / 5), passes=1)
+    return {"value": round(mb / 2**30, 3), "unit": "GiB/s", "cores": len(work), "kind": "port",
+            "mobjects_per_s": round(mo / 1e6, 3),
+            "passes_GiB_s": [round(r[0] / 2**30, 3) for r in rates],
+            "single_thread_GiB_s": round(ob / 2**30, 3),
+            "sample": "%d objects (%.0f MB) of the same batch, oracle/hdx_oracle.c -O2, one pinned thread per core "
+                      "over its own first-touched copy of a contiguous chunk, median of 3 passes (%d chunk passes); "
+                      "verified equal to the GPU coords" % (ns, nb / 1e6, reps),
+            **host_info(len(work), quota)}
 
 
 def cpu_per_object(types, blob, base, lens, coords, seconds, label):
@@ -1125,11 +1296,12 @@ def torch_index(idx, device):
 
 
 def cpu_baseline_encoded(types, enc, A, seconds, coords):
-    """Config 5 CPU baseline: the oracle's decode_value + hash on the same
-    cores as cpu_baseline (one oracle call per thread over its own chunk of a
-    20 k-objects-per-thread sample; ctypes drops the GIL for each call)."""
-    from concurrent.futures import ThreadPoolExecutor
-
+    """Config 5 CPU baseline: the oracle's decode_value + hash, one pinned
+    thread per core as cpu_baseline, each over its own first-touched compact
+    copy (keys back to back, values back to back) of a 20 k-object chunk, so
+    every store layout times the same work; median of 3 passes.  The
+    sample's GPU coordinates, and those of objects spread over the whole
+    store, are checked against the oracle first."""
     from oracle import oracle
     threads, quota = cpu_threads()
     keys, key_off, key_len, vals, val_off, val_len = enc
@@ -1141,33 +1313,42 @@ def cpu_baseline_encoded(types, enc, A, seconds, coords):
     kend = int((ko.astype(np.uint64) + kl).max())
     vend = int((vo.astype(np.uint64) + vl).max())
     hk, hv = keys[:kend].cpu().numpy(), vals[:vend].cpu().numpy()
+    want, _, bad = oracle.hash_encoded(types, hk, ko, kl, hv, vo, vl)
+    if bad.any() or not np.array_equal(coords[:ns].cpu().numpy().view(np.uint64), want):
+        raise SystemExit("cpu_baseline: GPU coordinates differ from the oracle")
+    spread = verify_encoded_spread(types, enc, coords, oracle)
     cuts = np.linspace(0, ns, threads + 1).astype(np.int64)
-    chunks = [(ko[c0:c1], kl[c0:c1], vo[c0:c1], vl[c0:c1]) for c0, c1 in zip(cuts[:-1], cuts[1:]) if c1 > c0]
 
-    def one(ch):
-        return oracle.hash_encoded(types, hk, ch[0], ch[1], hv, ch[2], ch[3])
+    def compact(buf, off, ln):
+        out = np.empty(int(ln.astype(np.uint64).sum()), np.uint8)
+        noff = np.zeros(len(off), np.uint64)
+        if len(off) > 1:
+            noff[1:] = np.cumsum(ln[:-1].astype(np.uint64))
+        for i in range(len(off)):
+            out[int(noff[i]):int(noff[i]) + int(ln[i])] = buf[int(off[i]):int(off[i]) + int(ln[i])]
+        return out, noff
 
-    with ThreadPoolExecutor(len(chunks)) as pool:
-        parts = list(pool.map(one, chunks))
-        want = np.concatenate([p[0] for p in parts])
-        bad = np.concatenate([p[2] for p in parts])
-        if bad.any() or not np.array_equal(coords[:ns].cpu().numpy().view(np.uint64), want):
-            raise SystemExit("cpu_baseline: GPU coordinates differ from the oracle")
-        spread = verify_encoded_spread(types, enc, coords, oracle)
-        nbytes = int(kl.sum()) + int(vl.sum())
-        reps, t0 = 0, time.perf_counter()
-        while True:
-            list(pool.map(one, chunks))
-            reps += 1
-            dt = time.perf_counter() - t0
-            if dt >= seconds:
-                break
-    return {"value": round(reps * nbytes / dt / 2**30, 3), "unit": "GiB/s", "cores": len(chunks),
-            "kind": "port", "mobjects_per_s": round(reps * ns / dt / 1e6, 3),
-            "sample": "%d stored objects (%.0f MB), %d passes, oracle hdxo_hash_encoded -O2, %d threads; "
-                      "verified equal to the GPU coords, and %d objects spread over the whole store (the last "
-                      "64 and random ones)" % (ns, nbytes / 1e6, reps, len(chunks), spread),
-            **host_info(len(chunks), quota)}
+    def job(c0, c1):
+        def prepare():  # this thread's compact copy of its objects
+            k, nko = compact(hk, ko[c0:c1], kl[c0:c1])
+            v, nvo = compact(hv, vo[c0:c1], vl[c0:c1])
+            return k, nko, kl[c0:c1].copy(), v, nvo, vl[c0:c1].copy()
+
+        def run(st):
+            oracle.hash_encoded(types, *st)
+        return prepare, run, int(kl[c0:c1].sum()) + int(vl[c0:c1].sum()), c1 - c0
+    work = [job(int(c0), int(c1)) for c0, c1 in zip(cuts[:-1], cuts[1:]) if c1 > c0]
+    rates, (mb, mo), reps = pinned_passes(work, seconds)
+    nbytes = int(kl.sum()) + int(vl.sum())
+    return {"value": round(mb / 2**30, 3), "unit": "GiB/s", "cores": len(work), "kind": "port",
+            "mobjects_per_s": round(mo / 1e6, 3),
+            "passes_GiB_s": [round(r[0] / 2**30, 3) for r in rates],
+            "sample": "%d stored objects (%.0f MB), oracle hdxo_hash_encoded -O2, one pinned thread per core over its "
+                      "own first-touched compact copy (keys and values back to back, whatever the store's layout) "
+                      "of a contiguous chunk, median of 3 passes (%d chunk passes); verified equal to the GPU coords, "
+                      "and %d objects spread over the whole store (the last 64 and random ones)"
+                      % (ns, nbytes / 1e6, reps, spread),
+            **host_info(len(work), quota)}
 
 
 if __name__ == "__main__":

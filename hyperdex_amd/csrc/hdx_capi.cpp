@@ -87,16 +87,17 @@ static hdx_status device_codes(const uint8_t* codes, uint32_t A, const uint8_t**
     return HDX_OK;
 }
 
+// (debug library: variants 300 / 301 force the wide kernels at any A)
 hdx_status set_codes(BatchArgs& args, const uint8_t* codes, uint32_t A) {
     std::memcpy(args.codes, codes, std::min(A, kKernargCodes));
     args.codes_dev = nullptr;
-    return A > 128 ? device_codes(codes, A, &args.codes_dev) : HDX_OK;
+    return A > 128 || hash_variant() == 300 ? device_codes(codes, A, &args.codes_dev) : HDX_OK;
 }
 
 hdx_status set_codes(EncodedArgs& a, const uint8_t* codes, uint32_t A) {
     std::memcpy(a.codes, codes, std::min(A, kKernargCodes));
     a.codes_dev = nullptr;
-    return A > kWsweepMaxAttrs ? device_codes(codes, A, &a.codes_dev) : HDX_OK;
+    return A > kWsweepMaxAttrs || hash_variant() == 301 ? device_codes(codes, A, &a.codes_dev) : HDX_OK;
 }
 
 // ---- device binding -------------------------------------------------------
@@ -746,7 +747,9 @@ HDX_EXPORT uint64_t hdxdbg_region_chunk_objects(uint64_t n, uint32_t attrs_sz) {
 
 HDX_EXPORT int hdxdbg_kernel_for(const uint32_t* types, uint32_t attrs_sz, uint64_t n, const char** name) {
     BatchArgs a{};
-    if (check_schema(types, attrs_sz, a.codes) != HDX_OK) return -2;
+    std::vector<uint8_t> codes(attrs_sz ? attrs_sz : 1);
+    if (check_schema(types, attrs_sz, codes.data()) != HDX_OK) return -2;
+    std::memcpy(a.codes, codes.data(), std::min(attrs_sz, kKernargCodes));
     a.A = attrs_sz;
     a.n = n;
     finalize_args(a);

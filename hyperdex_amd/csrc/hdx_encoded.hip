@@ -367,9 +367,9 @@ static hipError_t launch_encoded(const EncodedArgs& a_in, hipStream_t stream) {
 hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
     if (a_in.n == 0) return hipSuccess;
     EncodedArgs a = a_in;
-    if (a.A > kWsweepMaxAttrs) {
+    if (a.A > kWsweepMaxAttrs || hash_variant() == 301) {
         // wide schemas (hdx_wide.hip): the wide sweep, then one lookup launch
-        // per table
+        // per table (debug variant 301: at any A)
         const RegionHashFn hash = [&](uint64_t first, uint64_t count, uint64_t* c) {
             EncodedArgs b = a;
             b.key_off += first;
@@ -468,6 +468,11 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
         // branchy class, 246 without TNUM
         case 230: case 231: case 232: case 236: case 237: case 238: case 239: case 242: case 243: case 244: case 245: case 246: {
             const hipError_t e = launch_hash_wsweep(a, stream, hash_variant() - 230);
+            if (e != hipErrorInvalidValue) return e;
+            break;
+        }
+        case 256: case 257: {  // the product sweep with one / two waves per workgroup
+            const hipError_t e = launch_hash_wsweep(a, stream, hash_variant() - 256 + 23);
             if (e != hipErrorInvalidValue) return e;
             break;
         }

@@ -36,7 +36,7 @@ hipError_t launch_debug_variant(const BatchArgs& args, hipStream_t stream, int v
         // wave-staged (hdx_wstage.hip): 200 2 passes / 10 KiB, 201 3 / 14 KiB, 202 2 / 8 KiB,
         // 203 1 / 5 KiB, 204 4 / 18 KiB, 205 2 / 8832 B, 206 = 205 with <= 6 objects
         case 200: case 201: case 202: case 203: case 204: case 205: case 206: case 207: case 208:
-        case 209: case 210: case 211: case 213: case 214: case 215: case 216: case 218: case 219: case 239: case 240: case 241: case 242: case 244: case 245: case 246: case 248: case 249: case 255: {
+        case 209: case 210: case 211: case 213: case 214: case 215: case 216: case 218: case 219: case 239: case 240: case 241: case 242: case 244: case 245: case 246: case 248: case 249: case 255: case 256: case 257: {
             const hipError_t e = launch_hash_wstage(args, stream, variant - 200);
             return e == hipErrorInvalidValue ? launch_hash_batch_variant(args, stream, 44) : e;
         }
@@ -75,6 +75,7 @@ static bool known_variant(int v) {
         case -1: case 12: case 18: case 19: case 20: case 21: case 25: case 26: case 30: case 31: case 35: case 37:
         case 38: case 39: case 44: case 45: case 46:
         case 300:  // the wide kernel (hdx_wide.hip), at any A
+        case 301:  // the wide sweep (hdx_wide.hip), at any A
         case 100: case 101: case 102: case 103: case 104: case 105: case 106: case 107: case 108: case 109:
         case 110: case 111:  // fused hash + lookup_region forms (launch_fused_debug)
         case 170: case 171: case 172: case 173: case 174:  // the sweep's numeric walk (hdx_encoded.hip)
@@ -105,6 +106,7 @@ static bool known_variant(int v) {
         case 252:  // debug shape of 250: no copy, no walk, the hash on made-up descriptors (WRONG coordinates)
         case 253: case 254:  // the product sweep's non-record / record forms with round 3's per-KiB span copy
         case 255:  // 212 with round 3's per-KiB span copy; the sweep with round 3's walk reads
+        case 256: case 257:  // 212 / the product sweep with one / two waves per workgroup
         case 210: case 211:  // wave-staged, sorted over the workgroup
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 49: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)

@@ -47,11 +47,11 @@ namespace {
 
 typedef __attribute__((address_space(3))) void* lds_void_t;
 
-template <int NCH>
+template <int NCH, int WPB = 4>
 struct WStageMeta {
-    uint64_t desc[4][NCH * 64];  // {offset u32, length u32}; then the slot's parked coordinate
-    uint16_t perm[4][NCH * 64];  // slot | code << 8, in class order
-    uint32_t cnt[4][kClasses];
+    uint64_t desc[WPB][NCH * 64];  // {offset u32, length u32}; then the slot's parked coordinate
+    uint16_t perm[WPB][NCH * 64];  // slot | code << 8, in class order
+    uint32_t cnt[WPB][kClasses];
 };
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
@@ -204,16 +204,17 @@ __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, 
 // (lookup_tables_wave), coordinates stored only when args.coords is set.
 // GAP: the class straddling the pass boundary moves whole into the second
 // pass when pads allow (class_sort, hdx_regroup.h).  DL (debug): round 3's
-// span copy, addresses and predicate per KiB (dma_units16_loop).
+// span copy, addresses and predicate per KiB (dma_units16_loop).  WPB: waves
+// (each with its own window) per workgroup.
 template <int NCH, uint32_t WB, int SHAPE = 0, int HT = 0, int ORDER = 1, int W128 = 0, bool REGIONS = false,
-          bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false>
-__global__ void __launch_bounds__(256)
+          bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false, int WPB = 4>
+__global__ void __launch_bounds__(64 * WPB)
 hash_wstage_kernel(const BatchArgs args) {
     static_assert(NCH >= 1 && NCH <= 4 && WB % 16 == 0, "slot indices are 8 bits; windows whole DMA units");
     constexpr uint32_t FRONT = HT ? kFrontHT : 0;
     // +64: dword over-reads past the span; HT: 32 bytes before it (short strings' tail reads)
-    __shared__ __attribute__((aligned(16))) uint8_t win_all[4][FRONT + WB + 64];
-    __shared__ WStageMeta<NCH> meta;
+    __shared__ __attribute__((aligned(16))) uint8_t win_all[WPB][FRONT + WB + 64];
+    __shared__ WStageMeta<NCH, WPB> meta;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     uint8_t* win = win_all[w] + FRONT;
@@ -222,7 +223,7 @@ hash_wstage_kernel(const BatchArgs args) {
     uint32_t* cnt = meta.cnt[w];
     const ldsw_t lw = as_ldsw(win_all[w]);
 
-    const uint64_t o0 = ((uint64_t)blockIdx.x * 4 + w) * args.K;
+    const uint64_t o0 = ((uint64_t)blockIdx.x * WPB + w) * args.K;
     if (o0 >= args.n) return;  // no barrier anywhere: waves are independent
     const Group<NCH> g = describe_group<NCH, WB, SHAPE, ORDER, ADMA, DL>(args, o0, win, 0, desc);
 
@@ -258,16 +259,17 @@ hash_wstage_kernel(const BatchArgs args) {
 // Launch: K = floor(64 * NCH / A) whole objects per wave (at most 63), four
 // independent waves per 256-thread workgroup, no workgroup barrier.
 template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, int HT = 0, int ORDER = 1, int W128 = 0,
-          bool REGIONS = false, bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false>
+          bool REGIONS = false, bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false, int WPB = 4>
 static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     // lane o holds object o's base and lane K the next group's first: K <= 63
     args.K = std::min<uint32_t>(std::min<uint32_t>((uint32_t)(64 * NCH) / args.A, KCAP), 63u);
     if (args.K == 0) return hipErrorInvalidValue;
     const uint64_t waves = (args.n + args.K - 1) / args.K;
-    const uint64_t blocks = (waves + 3) / 4;
+    const uint64_t blocks = (waves + WPB - 1) / WPB;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA, PU, DL>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA, PU, DL, WPB>),
+                       dim3((uint32_t)blocks), dim3(64 * WPB), 0, stream, args);
     return hipGetLastError();
 }
 

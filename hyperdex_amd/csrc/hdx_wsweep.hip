@@ -152,15 +152,16 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
 // coordinate is its descriptor), 2 = no hash and no walk.  SHAPE 4 (debug
 // form 22, correct coordinates): the walk's reads as round 3's dword pairs.
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
-          bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true, bool DL = false>
-__global__ void __launch_bounds__(256)
+          bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true, bool DL = false,
+          int WPB = 4>
+__global__ void __launch_bounds__(64 * WPB)
 hash_sweep_wstage_kernel(const EncodedArgs a) {
     constexpr uint32_t SL = NCH * 64;
-    __shared__ __attribute__((aligned(16))) uint8_t win_all[4][kFrontS + WB + kBackS];
-    __shared__ uint64_t desc_all[4][SL];   // {offset, length | kGlobal}; then the parked coordinate
-    __shared__ uint16_t perm_all[4][SL];   // slot | code << 8, in class order
-    __shared__ uint32_t cnt_all[4][kClasses];
-    __shared__ __attribute__((aligned(4))) uint8_t codes_all[4][SL];
+    __shared__ __attribute__((aligned(16))) uint8_t win_all[WPB][kFrontS + WB + kBackS];
+    __shared__ uint64_t desc_all[WPB][SL];   // {offset, length | kGlobal}; then the parked coordinate
+    __shared__ uint16_t perm_all[WPB][SL];   // slot | code << 8, in class order
+    __shared__ uint32_t cnt_all[WPB][kClasses];
+    __shared__ __attribute__((aligned(4))) uint8_t codes_all[WPB][SL];
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     uint8_t* win = win_all[w];
@@ -171,7 +172,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
     uint8_t* codes = codes_all[w];
     const uint32_t A = a.A;
     const uint32_t K = std::min<uint32_t>(SL / A, KCAP);
-    const uint64_t o0 = ((uint64_t)blockIdx.x * 4 + w) * K;
+    const uint64_t o0 = ((uint64_t)blockIdx.x * WPB + w) * K;
     if (o0 >= a.n) return;
     const uint32_t nobj = (uint32_t)std::min<uint64_t>(K, a.n - o0);
     const uint32_t ns = nobj * A;
@@ -420,14 +421,16 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
 }
 
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
-          bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true, bool DL = false>
+          bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true, bool DL = false,
+          int WPB = 4>
 static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
     const uint32_t K = std::min<uint32_t>(64 * NCH / a.A, KCAP);
     if (K == 0) return hipErrorInvalidValue;
     const uint64_t waves = (a.n + K - 1) / K;
-    const uint64_t blocks = (waves + 3) / 4;
+    const uint64_t blocks = (waves + WPB - 1) / WPB;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU, BF, RECS, KUNITS, DL>), dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU, BF, RECS, KUNITS, DL, WPB>),
+                       dim3((uint32_t)blocks), dim3(64 * WPB), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -479,6 +482,12 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 20: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, true, true>(a, stream);  // round 3's span copy (per KiB)
         case 21: return launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, true, true, true>(a, stream);  // the record form, round 3's span copy
         case 22: return launch_wsweep_t<2, 8704, 6, false, true, 4, 13, false, true, true, false>(a, stream);  // the walk's reads as dword pairs + v_alignbyte (round 3)
+        case 23: return a.keys == a.vals  // the product, one wave per workgroup
+                        ? launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, true, true, false, 1>(a, stream)
+                        : launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, true, false, 1>(a, stream);
+        case 24: return a.keys == a.vals  // the product, two waves per workgroup
+                        ? launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, true, true, false, 2>(a, stream)
+                        : launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, true, false, 2>(a, stream);
         default: return hipErrorInvalidValue;
     }
 }

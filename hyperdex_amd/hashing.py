@@ -8,6 +8,11 @@ plus the batched GPU path over the packed layout of include/hdxhash.h:
 
     hash_batch(types, blob, obj_base, attr_len)       device-resident (torch HIP tensors)
     hash_batch_host(types, blob, obj_base, attr_len)  host-resident (numpy), pipelined H2D/D2H
+    hash_batch_regions_host(...)                      host-resident, region ids out
+    hash_encoded_host(...) / hash_encoded_regions_host(...)
+                                                      the reindex sweep from host memory
+    hash_batch_device_multi / hash_batch_regions_device_multi
+                                                      one shard per device of the set, RCCL gather
 
 All of them run the gfx950 kernels in libhdxhash.so.  Where the reference
 asserts (unknown type, mis-sized numeric value) these raise HdxError.
@@ -141,6 +146,84 @@ def hash_batch_host(types, blob, obj_base, attr_len, out: Optional[np.ndarray] =
                                     blob.size, obj_base.ctypes.data, attr_len.ctypes.data, n,
                                     out.ctypes.data))
     return out
+
+
+def _handles(tables):
+    return (ctypes.c_void_p * max(len(tables), 1))(*[tb.handle.value for tb in tables])
+
+
+def hash_batch_regions_host(types, blob, obj_base, attr_len, tables, coords: bool = False):
+    """hdx_hash_batch_regions_host: host-resident batch -> region ids (T, n)
+    uint64 in the RegionTables `tables` (1..4); with coords=True also the
+    (n, A) coordinates.  Split over the device set like hash_batch_host."""
+    t = _u32_array(types)
+    A = len(t)
+    blob = np.ascontiguousarray(blob, dtype=np.uint8)
+    obj_base = np.ascontiguousarray(obj_base, dtype=np.uint64)
+    attr_len = np.ascontiguousarray(attr_len, dtype=np.uint32)
+    n = len(obj_base)
+    assert attr_len.size == n * A
+    ids = np.empty((len(tables), n), dtype=np.uint64)
+    out = np.empty((n, A), dtype=np.uint64) if coords else None
+    check(lib().hdx_hash_batch_regions_host(t.ctypes.data, A, blob.ctypes.data if blob.size else None, blob.size,
+                                            obj_base.ctypes.data, attr_len.ctypes.data, n, _handles(tables),
+                                            len(tables), ids.ctypes.data, out.ctypes.data if coords else None))
+    return (ids, out) if coords else ids
+
+
+def _stored_host(keys, key_off, key_len, vals, val_off, val_len):
+    records = vals is keys  # one store of [key][value] records: keep it one buffer
+    keys = np.ascontiguousarray(keys, dtype=np.uint8)
+    vals = keys if records else np.ascontiguousarray(vals, dtype=np.uint8)
+    key_off = np.ascontiguousarray(key_off, dtype=np.uint64)
+    key_len = np.ascontiguousarray(key_len, dtype=np.uint32)
+    val_off = np.ascontiguousarray(val_off, dtype=np.uint64)
+    val_len = np.ascontiguousarray(val_len, dtype=np.uint32)
+    n = len(val_off)
+    assert len(key_off) == n and len(key_len) == n and len(val_len) == n
+    return keys, key_off, key_len, vals, val_off, val_len, n
+
+
+def hash_encoded_host(types, keys, key_off, key_len, vals, val_off, val_len, versions: bool = False):
+    """hdx_hash_encoded_host: the reindex sweep over stored objects in host
+    memory (numpy; pass the same array as keys and vals for records
+    [key][value] in one store).  Returns coords (n, A) uint64 (and versions (n,)
+    with versions=True); raises HdxError (HDX_E_BADENC / HDX_E_BADSIZE) after
+    the whole call ran when a value does not decode or a numeric is
+    mis-sized — use hash_encoded_host_status to keep the outputs then."""
+    coords, vers, st, msg = hash_encoded_host_status(types, keys, key_off, key_len, vals, val_off, val_len)
+    if st != _lib.HDX_OK:
+        raise HdxError(st, msg)
+    return (coords, vers) if versions else coords
+
+
+def hash_encoded_host_status(types, keys, key_off, key_len, vals, val_off, val_len, tables=()):
+    """The same, never raising for undecodable values: (coords, versions,
+    status, message), plus region ids (T, n) as a 5th item with `tables`."""
+    t = _u32_array(types)
+    A = len(t)
+    keys, key_off, key_len, vals, val_off, val_len, n = _stored_host(keys, key_off, key_len, vals, val_off, val_len)
+    coords = np.empty((n, A), dtype=np.uint64)
+    vers = np.empty(n, dtype=np.uint64)
+    kp = keys.ctypes.data if keys.size else None
+    vp = kp if vals is keys else (vals.ctypes.data if vals.size else None)
+    if tables:
+        ids = np.empty((len(tables), n), dtype=np.uint64)
+        st = lib().hdx_hash_encoded_regions_host(t.ctypes.data, A, kp, keys.size, key_off.ctypes.data,
+                                                 key_len.ctypes.data, vp, vals.size, val_off.ctypes.data,
+                                                 val_len.ctypes.data, n, _handles(tables), len(tables),
+                                                 ids.ctypes.data, coords.ctypes.data, vers.ctypes.data)
+    else:
+        st = lib().hdx_hash_encoded_host(t.ctypes.data, A, kp, keys.size, key_off.ctypes.data, key_len.ctypes.data,
+                                         vp, vals.size, val_off.ctypes.data, val_len.ctypes.data, n,
+                                         coords.ctypes.data, vers.ctypes.data)
+    msg = ""
+    if st != _lib.HDX_OK:
+        m = lib().hdx_last_error()
+        msg = m.decode() if m else ""
+        if st not in (_lib.HDX_E_BADENC, _lib.HDX_E_BADSIZE):
+            raise HdxError(st, msg)
+    return (coords, vers, st, msg, ids) if tables else (coords, vers, st, msg)
 
 
 def hash_encoded(types, keys, key_off, key_len, vals, val_off, val_len, coords=None,
@@ -307,3 +390,37 @@ def hash_batch_device_multi(types, shards, gather: bool = True, coords=None):
         torch.cuda.current_stream(s[1].device).synchronize()
     check(lib().hdx_hash_batch_device_multi(t.ctypes.data, A, arr, len(shards), 1 if gather else 0))
     return outs
+
+
+def hash_batch_regions_device_multi(types, shards, tables, gather: bool = True, coords: bool = False):
+    """hdx_hash_batch_regions_device_multi: shards[k] = (blob, obj_base,
+    attr_len[, status]) on the k-th device of the set; returns one region-id
+    tensor per device — (T, N) with gather (every device holds every object's
+    ids: only the ids cross the fabric), else (T, n_k) — and, with coords=True,
+    each shard's own (n_k, A) coordinates as a second list."""
+    import torch
+
+    t = _u32_array(types)
+    A = len(t)
+    T = len(tables)
+    counts = [int(s[1].numel()) for s in shards]
+    N = sum(counts)
+    ids_out, coord_out = [], []
+    arr = (_lib.RegionShard * max(len(shards), 1))()
+    for k, s in enumerate(shards):
+        blob, base, lens = s[0], s[1], s[2]
+        status = s[3] if len(s) > 3 else None
+        _check_packed(blob, base, lens, A)
+        _check_status(status, base.device)
+        ids = torch.empty((T, N if gather else counts[k]), dtype=torch.int64, device=base.device)
+        c = torch.empty((counts[k], A), dtype=torch.int64, device=base.device) if coords else None
+        ids_out.append(ids)
+        coord_out.append(c)
+        arr[k] = _lib.RegionShard(blob.data_ptr(), base.data_ptr(), lens.data_ptr(), counts[k], ids.data_ptr(),
+                                  c.data_ptr() if c is not None else None,
+                                  status.data_ptr() if status is not None else None)
+    for s in shards:
+        torch.cuda.current_stream(s[1].device).synchronize()
+    check(lib().hdx_hash_batch_regions_device_multi(t.ctypes.data, A, arr, len(shards), _handles(tables), T,
+                                                    1 if gather else 0))
+    return (ids_out, coord_out) if coords else ids_out

@@ -10,7 +10,6 @@
 #define _GNU_SOURCE
 #include "hdx_oracle.h"
 
-#define HDXO_MAX_ATTRS 256
 
 #include <math.h>
 #include <pthread.h>
@@ -405,6 +404,9 @@ int64_t hdxo_hash_encoded(const uint32_t* types, uint32_t A, const uint8_t* keys
                           const uint64_t* val_off, const uint32_t* val_len, uint64_t n,
                           uint64_t* coords, uint64_t* versions, uint8_t* bad) {
     int64_t nbad = 0;
+    /* any schema width (the reference's attrs_sz is a u16, common/schema.h:49) */
+    const uint8_t** attr_p = (const uint8_t**)malloc(sizeof(*attr_p) * (A ? A : 1));
+    uint32_t* attr_n = (uint32_t*)malloc(sizeof(*attr_n) * (A ? A : 1));
     for (uint64_t i = 0; i < n; ++i) {
         uint64_t* hs = coords + i * A;
         const uint8_t* v = vals + val_off[i];
@@ -417,8 +419,6 @@ int64_t hdxo_hash_encoded(const uint32_t* types, uint32_t A, const uint8_t* keys
         uint32_t count = 0;
         if (ok && ptr + 2 <= end) { count = ((uint32_t)ptr[0] << 8) | ptr[1]; ptr += 2; } else ok = 0;
         if (ok && count != A - 1) ok = 0; /* the schema's value attributes */
-        const uint8_t* attr_p[HDXO_MAX_ATTRS];
-        uint32_t attr_n[HDXO_MAX_ATTRS];
         for (uint32_t k = 0; ok && k < count; ++k) {
             /* :198-213; unlike the reference, the attribute must end inside the value */
             if (ptr + 4 > end) { ok = 0; break; }
@@ -437,12 +437,12 @@ int64_t hdxo_hash_encoded(const uint32_t* types, uint32_t A, const uint8_t* keys
         }
         int e;
         hs[0] = hdxo_hash_value(types[0], keys + key_off[i], key_len[i], &e);
-        if (e) return -1;
-        for (uint32_t k = 0; k + 1 < A; ++k) {
-            hs[k + 1] = hdxo_hash_value(types[k + 1], attr_p[k], attr_n[k], &e);
-            if (e) return -1;
-        }
+        if (e) { nbad = -1; break; }
+        for (uint32_t k = 0; k + 1 < A && !e; ++k) hs[k + 1] = hdxo_hash_value(types[k + 1], attr_p[k], attr_n[k], &e);
+        if (e) { nbad = -1; break; }
     }
+    free(attr_p);
+    free(attr_n);
     return nbad;
 }
 

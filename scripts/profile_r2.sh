@@ -38,7 +38,14 @@ for CFG in cfg3a cfg3b cfg2 cfg1 cfg5 cfg5k cfg5r; do
         -- python3 $ROOT/scripts/run_kernel.py --config $CFG --launches 3 --objects $N \
         > "$OUT/pmc_${CFG}_$C.log" 2>&1 || exit $?
   done
+  # the VALU-issue roofline's counters (4 SQ + 1 GRBM: one pass), with the
+  # kernel trace for the effective clock
+  echo "[$(date +%T)] $CFG VALU"
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE \
+      -d "$OUT/pmc_${CFG}_VALU" -o run --output-format csv \
+      -- python3 $ROOT/scripts/run_kernel.py --config $CFG --launches 3 --objects $N \
+      > "$OUT/pmc_${CFG}_VALU.log" 2>&1 || exit $?
   python3 $ROOT/scripts/traffic_from_pmc.py "$OUT/pmc_${CFG}_FETCH_SIZE" "$OUT/pmc_${CFG}_WRITE_SIZE" $CFG \
-      "$OUT/traffic.json" $N || exit $?
+      "$OUT/traffic.json" $N "$OUT/pmc_${CFG}_VALU" || exit $?
 done
 echo "profile round $TAG done"

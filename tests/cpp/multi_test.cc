@@ -10,10 +10,16 @@
 // 3. the same batch sharded over the set by hdx_shard_ranges, each shard
 //    uploaded to its device, hashed by hdx_hash_batch_device_multi with the
 //    RCCL gather, and every device's full matrix read back;
+// 4. the region-id forms: hdx_hash_batch_regions_host (split over the set)
+//    and hdx_hash_batch_regions_device_multi with the gather of region ids
+//    only (16 bytes per object for two tables instead of 104 of coordinates);
 // all coordinates checked against the product's per-object CPU path
-// (hdx_hash_object, common/hash.cc:56-68's signature).  Prints "multi ok".
+// (hdx_hash_object, common/hash.cc:56-68's signature), region ids against a
+// first-match scan of the boxes (configuration::lookup_region,
+// common/configuration.cc:698-735).  Prints "multi ok".
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -37,6 +43,25 @@
             std::exit(1);                                                             \
         }                                                                             \
     } while (0)
+
+// configuration::lookup_region: the first region whose box holds the
+// subspace's coordinates (inclusive), else 0
+struct Table {
+    std::vector<uint16_t> attrs;
+    std::vector<uint64_t> lower, upper, ids;
+    uint64_t lookup(const uint64_t* hs) const {
+        const size_t D = attrs.size();
+        for (size_t r = 0; r < ids.size(); ++r) {
+            bool in = true;
+            for (size_t d = 0; d < D && in; ++d) {
+                const uint64_t h = hs[attrs[d]];
+                in = lower[r * D + d] <= h && h <= upper[r * D + d];
+            }
+            if (in) return ids[r];
+        }
+        return 0;
+    }
+};
 
 static uint64_t splitmix(uint64_t& s) {
     uint64_t z = (s += 0x9e3779b97f4a7c15ull);
@@ -70,8 +95,8 @@ int main(int argc, char** argv) {
     // the product's per-object CPU path
     std::vector<uint64_t> want(n * A);
     for (uint64_t i = 0; i < n; ++i) {
-        const uint8_t* vals[HDX_MAX_ATTRS];
-        size_t lens[HDX_MAX_ATTRS];
+        const uint8_t* vals[16];
+        size_t lens[16];
         uint64_t off = base[i] + len[i * A];
         for (uint32_t j = 1; j < A; ++j) {
             vals[j - 1] = &blob[off];
@@ -150,6 +175,62 @@ int main(int argc, char** argv) {
             return 1;
         }
     }
+
+    // 4. region ids: a key grid of 64 equal ranges and a 2-attribute table of
+    // random (overlapping) boxes
+    std::vector<Table> tabs(2);
+    tabs[0].attrs = {0};
+    for (uint64_t r = 0; r < 64; ++r) {
+        tabs[0].lower.push_back(r << 58);
+        tabs[0].upper.push_back(r == 63 ? ~0ull : ((r + 1) << 58) - 1);
+        tabs[0].ids.push_back(100 + r);
+    }
+    tabs[1].attrs = {3, 8};
+    for (uint64_t r = 0; r < 40; ++r) {
+        for (int d = 0; d < 2; ++d) {
+            uint64_t a = splitmix(rng), b = splitmix(rng);
+            tabs[1].lower.push_back(std::min(a, b));
+            tabs[1].upper.push_back(std::max(a, b));
+        }
+        tabs[1].ids.push_back(500 + r);
+    }
+    std::vector<hdx_region_table> handles(2);
+    for (int t = 0; t < 2; ++t)
+        CHECK(hdx_region_table_create((uint32_t)tabs[t].attrs.size(), (uint32_t)tabs[t].ids.size(),
+                                      tabs[t].attrs.data(), tabs[t].lower.data(), tabs[t].upper.data(),
+                                      tabs[t].ids.data(), &handles[t]));
+    std::vector<uint64_t> want_ids(2 * n);
+    for (int t = 0; t < 2; ++t)
+        for (uint64_t i = 0; i < n; ++i) want_ids[t * n + i] = tabs[t].lookup(&want[i * A]);
+    std::vector<uint64_t> host_ids(2 * n), host_coords(n * A);
+    CHECK(hdx_hash_batch_regions_host(types.data(), A, blob.data(), total, base.data(), len.data(), n,
+                                      handles.data(), 2, host_ids.data(), host_coords.data()));
+    if (host_ids != want_ids || host_coords != want) {
+        std::printf("FAIL hdx_hash_batch_regions_host\n");
+        return 1;
+    }
+    std::vector<hdx_region_shard> rshards(nd);
+    std::vector<void*> id_allocs(nd);
+    for (int k = 0; k < nd; ++k) {
+        HCHECK(hipSetDevice(devs[k]));
+        HCHECK(hipMalloc(&id_allocs[k], 2 * n * 8));
+        HCHECK(hipMemset(id_allocs[k], 0, 2 * n * 8));
+        rshards[k] = hdx_region_shard{shards[k].blob, shards[k].obj_base, shards[k].attr_len, shards[k].n,
+                                      (uint64_t*)id_allocs[k], nullptr, nullptr};
+    }
+    CHECK(hdx_hash_batch_regions_device_multi(types.data(), A, rshards.data(), (uint32_t)nd, handles.data(), 2, 1));
+    std::vector<uint64_t> ids_back(2 * n);
+    for (int k = 0; k < nd; ++k) {
+        HCHECK(hipSetDevice(devs[k]));
+        HCHECK(hipMemcpy(ids_back.data(), id_allocs[k], 2 * n * 8, hipMemcpyDeviceToHost));
+        if (ids_back != want_ids) {
+            std::printf("FAIL gathered region ids on device %d differ\n", devs[k]);
+            return 1;
+        }
+        HCHECK(hipFree(id_allocs[k]));
+    }
+    for (auto h : handles) CHECK(hdx_region_table_destroy(h));
+
     for (size_t a = 0; a < allocs.size(); ++a) {
         HCHECK(hipSetDevice(devs[a / 4]));
         HCHECK(hipFree(allocs[a]));

@@ -9,7 +9,12 @@
 //     restatement of dist.shard_ranges' rule;
 //   * the region tables' interval index and host lookup (hdx_region_index.h,
 //     the batcher's calling-thread path) against the oracle's lookup_region,
-//     index and scan, with every table array in an exact-size buffer.
+//     index and scan, with every table array in an exact-size buffer;
+//   * the device set's exchange plan (hdx_exchange.h: which collective moves
+//     which rows) applied to per-device matrices holding only their own
+//     rows, for equal, unequal and empty shards at world 1..8, coordinates
+//     and region-id sections: every device must end with the full matrix;
+//   * the cut rule over stored objects (key + value bytes, the host sweep).
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -21,6 +26,7 @@
 #include <vector>
 
 #include "hdx_cuts.h"
+#include "hdx_exchange.h"
 #include "hdx_host_common.h"
 #include "hdx_region_index.h"
 
@@ -212,6 +218,73 @@ int main() {
                   rep, D, R, kind, (unsigned long long)i, (unsigned long long)a, (unsigned long long)b,
                   (unsigned long long)want[i]);
         }
+    }
+    // exchange plans: equal / unequal / empty shards, world 1..8, coordinate
+    // rows (one section of N * A) and region-id sections (T sections of N)
+    for (int rep = 0; rep < 600; ++rep) {
+        const uint32_t world = 1 + (uint32_t)(g() % 8);
+        std::vector<uint64_t> counts(world);
+        const int kind = rep % 4;
+        for (auto& c : counts) c = kind == 0 ? 37 : (uint64_t)(g() % (kind == 3 ? 3 : 200));  // kind 3: many empty
+        if (kind == 1 && world > 1) counts[g() % world] = 0;
+        const bool ids = rep % 2 == 1;
+        const uint32_t A = 1 + (uint32_t)(g() % 20), T = 1 + (uint32_t)(g() % 4);
+        uint64_t N = 0;
+        for (auto c : counts) N += c;
+        const uint64_t row = ids ? 1 : A, sections = ids ? T : 1, stride = ids ? N : N * A;
+        const std::vector<hdx::ExchangeOp> plan = hdx::exchange_plan(counts.data(), world, row, (uint32_t)sections, stride);
+        bool equal = true;
+        for (auto c : counts) equal = equal && c == counts[0];
+        uint64_t nonempty = 0;
+        for (auto c : counts) nonempty += c != 0;
+        const size_t want_ops = N == 0 ? 0 : equal ? sections : sections * nonempty;
+        CHECK(plan.size() == want_ops, "plan rep %d: %zu ops, want %zu", rep, plan.size(), want_ops);
+        // the full matrix, and each device holding only its own rows (others poisoned)
+        std::vector<uint64_t> full(sections * stride);
+        for (auto& x : full) x = g();
+        std::vector<std::vector<uint64_t>> mats(world, std::vector<uint64_t>(full.size(), 0xdeadbeefdeadbeefull));
+        uint64_t first = 0;
+        for (uint32_t k = 0; k < world; ++k) {
+            for (uint64_t s2 = 0; s2 < sections; ++s2)
+                for (uint64_t e = first * row; e < (first + counts[k]) * row; ++e)
+                    mats[k][s2 * stride + e] = full[s2 * stride + e];
+            first += counts[k];
+        }
+        hdx::exchange_apply(plan, mats);
+        for (uint32_t k = 0; k < world; ++k)
+            CHECK(mats[k] == full, "plan rep %d (world %u, %s): device %u's matrix differs", rep, world,
+                  ids ? "ids" : "coords", k);
+        // bytes a device receives: every row but its own, once per section
+        for (uint32_t k = 0; k < world && N; ++k)
+            CHECK(hdx::exchange_bytes_in(plan, world, k) == (N - counts[k]) * row * sections * 8,
+                  "plan rep %d: device %u receives %llu bytes", rep, k,
+                  (unsigned long long)hdx::exchange_bytes_in(plan, world, k));
+    }
+    // cuts over stored objects (key + value bytes) against a direct prefix search
+    for (int rep = 0; rep < 200; ++rep) {
+        const uint64_t n = rep < 5 ? (uint64_t)rep : g() % 200000;
+        const uint32_t world = 1 + (uint32_t)(g() % 8);
+        std::vector<uint32_t> kl(n), vl(n);
+        for (uint64_t i = 0; i < n; ++i) {
+            kl[i] = (uint32_t)(g() % 100);
+            vl[i] = rep % 3 == 0 && i < n / 2 ? 0u : (uint32_t)(g() % 3000);
+        }
+        std::vector<uint64_t> first(world + 1);
+        hdx::shard_cuts_of(hdx::StoredSizes{kl.data(), vl.data()}, n, world, 0.0, first.data());
+        std::vector<uint64_t> pre(n + 1, 0);
+        for (uint64_t i = 0; i < n; ++i) pre[i + 1] = pre[i] + kl[i] + vl[i];
+        std::vector<uint64_t> want(world + 1);
+        want[0] = 0;
+        want[world] = n;
+        for (uint32_t k = 1; k < world; ++k) {
+            const double target = (double)pre[n] * k / world;
+            uint64_t i = 0;
+            while (i <= n && (double)pre[i] < target) ++i;
+            want[k] = std::min(std::max(std::min(i, n), want[k - 1]), n);
+        }
+        for (uint32_t k = 0; k <= world; ++k)
+            CHECK(first[k] == want[k], "stored cuts rep %d k %u: %llu vs %llu", rep, k, (unsigned long long)first[k],
+                  (unsigned long long)want[k]);
     }
     if (failures) {
         fprintf(stderr, "%d failures\n", failures);

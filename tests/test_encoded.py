@@ -167,7 +167,7 @@ def test_oracle_scattered_layout(oracle):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [-1, 43, 47, 49, 170, 171, 173, 230, 232, 236, 239, 242, 243, 244, 245, 246, 250, 251, 253, 254, 255])
+@pytest.mark.parametrize("variant", [-1, 43, 47, 49, 301, 170, 171, 173, 230, 232, 236, 239, 242, 243, 244, 245, 246, 250, 251, 253, 254, 255])
 def test_gpu_encoded_scattered_layout(oracle, variant):
     """Objects whose keys and values lie in shuffled order with gaps hash
     exactly as the packed layout does."""
@@ -189,7 +189,7 @@ def test_gpu_encoded_scattered_layout(oracle, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [-1, 33, 43, 47, 48, 49, 170, 171, 172, 173, 174, 230, 231, 232, 236, 239, 242, 243, 244, 245, 246, 250, 251, 253, 254, 255])
+@pytest.mark.parametrize("variant", [-1, 33, 43, 47, 48, 49, 301, 170, 171, 172, 173, 174, 230, 231, 232, 236, 239, 242, 243, 244, 245, 246, 250, 251, 253, 254, 255])
 def test_gpu_encoded_every_variant(oracle, variant):
     """Every stored-object sweep kernel (hdx_encoded.hip; 33 adds the line
     touch) is bit-exact on every config, on corrupt values, on ragged object
@@ -215,7 +215,7 @@ def test_gpu_encoded_every_variant(oracle, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [-1, 170, 171, 173, 174, 230, 232, 236, 239, 242, 243, 244, 245, 246, 250, 251, 253, 254, 255])
+@pytest.mark.parametrize("variant", [-1, 301, 170, 171, 173, 174, 230, 232, 236, 239, 242, 243, 244, 245, 246, 250, 251, 253, 254, 255])
 def test_gpu_encoded_bad_numeric_size(oracle, variant):
     """A stored int64 / float / timestamp value of neither 0 nor 8 bytes (the
     reference asserts, datatype_int64.cc:233): its coordinate is 0 and status

@@ -298,34 +298,39 @@ def test_gpu_batch_regions_every_fused_form(oracle, form):
 
 
 @pytest.mark.gpu
-def test_gpu_tables_from_another_device_are_rejected(oracle):
-    """A region table records the device it was created on; the fused and
-    plain lookups refuse a table of another device (HDX_E_INVALID) instead of
-    reading that device's memory.  One GPU here, so the table's
-    device field (the first int of hdx_region_table_s, hdx_host.h) is
-    rewritten for the check and restored."""
+def test_gpu_tables_used_on_another_device_get_a_replica(oracle):
+    """A region table records the device it was created on; a call on another
+    device (the device set's entry points run every device of the set) uses a
+    replica of the table's host copy uploaded there on first use, never the
+    creating device's memory.  One GPU here, so the table's device
+    field (the first int of hdx_region_table_s, hdx_host.h) is rewritten to
+    another ordinal: the fused and plain lookups then run on a replica and
+    must give the same ids; the replica is freed with the table."""
     import ctypes
 
     import torch
 
     import hyperdex_amd as hdx
-    from hyperdex_amd import _lib, regions, synth
+    from hyperdex_amd import regions, synth
     dev = torch.device("cuda", 0)
     types, blob, base, lens = synth.make_batch_device("cfg2", 1000, device=dev)
     lo, up = oracle.partition(1, 64)
-    t = regions.RegionTable([0], lo, up, np.arange(1, 65, dtype=np.uint64))
+    ids = np.arange(1, 65, dtype=np.uint64)
+    t = regions.RegionTable([0], lo, up, ids)
     field = ctypes.c_int.from_address(t.handle.value)
     assert field.value == 0
     coords = hdx.hash_batch(types, blob, base, lens)
+    want = oracle.lookup_region([0], lo, up, ids, coords.cpu().numpy().view(np.uint64))
     try:
         field.value = 5
-        for call in (lambda: hdx.hash_batch_regions(types, blob, base, lens, [t]),
-                     lambda: regions.lookup_region(t, coords)):
-            with pytest.raises(hdx.HdxError) as e:
-                call()
-            assert e.value.status == _lib.HDX_E_INVALID
+        got1 = hdx.hash_batch_regions(types, blob, base, lens, [t])[0]
+        got2 = regions.lookup_region(t, coords)
+        torch.cuda.synchronize()
     finally:
         field.value = 0
-    hdx.hash_batch_regions(types, blob, base, lens, [t])
+    assert np.array_equal(got1.cpu().numpy().view(np.uint64), want)
+    assert np.array_equal(got2.cpu().numpy().view(np.uint64), want)
+    got3 = hdx.hash_batch_regions(types, blob, base, lens, [t])[0]
     torch.cuda.synchronize()
+    assert np.array_equal(got3.cpu().numpy().view(np.uint64), want)
     t.close()
