@@ -1,7 +1,9 @@
 // hdx_wstage.hip — the product instantiation of the wave-staged batch hash
-// (hdx_wstage.h): two class-sorted passes per wave, 8832-byte windows (four
-// workgroups of four waves per CU), slots hashed from the window with the
-// head/tail reads of hash_slot_window (hdx_lds_hash.h).  The automatic policy
+// (hdx_wstage.h): two class-sorted passes per wave, 8832-byte windows, one
+// wave per workgroup (16 per CU by LDS; round 5: 2.597 vs 2.658 ms for four
+// waves per workgroup, whose 40 KiB stayed allocated until the slowest of the
+// four finished, profiles/r5/ab_wpb.jsonl), slots hashed from the window with
+// the head/tail reads of hash_slot_window (hdx_lds_hash.h).  The automatic policy
 // runs it for mixed string / int64 / float schemas (config 3b: 2.92 vs 3.32 ms
 // for variant 44, profiles/r3/ab_wstage_ht.jsonl).  The A/B forms are in
 // hdx_wstage_dbg.hip (debug library only).
@@ -11,13 +13,13 @@ namespace hdx {
 
 hipError_t launch_hash_wstage_product(const BatchArgs& args, hipStream_t stream) {
     if (args.n == 0) return hipSuccess;
-    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, false, true, true>(args, stream);
+    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, false, true, true, true, false, 1>(args, stream);
 }
 
 // ... with the fused region lookup (args.T tables; args.coords may be NULL)
 hipError_t launch_hash_wstage_regions(const BatchArgs& args, hipStream_t stream) {
     if (args.n == 0) return hipSuccess;
-    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, true, true, true>(args, stream);
+    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, true, true, true, true, false, 1>(args, stream);
 }
 
 }  // namespace hdx

@@ -440,15 +440,18 @@ static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
 // lookups is faster (hdx_encoded.hip).  A <= kWsweepMaxAttrs.
 // The record span is compiled in only when keys and values are one store (the
 // check costs the other layouts ~1 %: 3.78 vs 3.74 ms per 10 M on a key column).
+// One wave per workgroup (round 5: 3.466 vs 3.626 ms per 10 M on the key
+// column for four, whose 40 KiB stayed allocated until the slowest of the four
+// finished; profiles/r5/ab_wpb.jsonl).
 hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
     const bool recs = a.keys == a.vals;
     if (a.T)
-        return recs ? launch_wsweep_t<2, 8704, 6, true, true, 0, 13, false, true, true, true>(a, stream)
-                    : launch_wsweep_t<2, 8704, 6, true, true, 0, 13, false, true, true, false>(a, stream);
+        return recs ? launch_wsweep_t<2, 8704, 6, true, true, 0, 13, false, true, true, true, true, false, 1>(a, stream)
+                    : launch_wsweep_t<2, 8704, 6, true, true, 0, 13, false, true, true, false, true, false, 1>(a, stream);
     if (!a.coords) return hipErrorInvalidValue;
-    return recs ? launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, true>(a, stream)
-                : launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false>(a, stream);
+    return recs ? launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, true, true, false, 1>(a, stream)
+                : launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, true, false, 1>(a, stream);
 }
 
 #ifndef HDX_DEBUG_BUILD
@@ -488,6 +491,12 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 24: return a.keys == a.vals  // the product, two waves per workgroup
                         ? launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, true, true, false, 2>(a, stream)
                         : launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, true, false, 2>(a, stream);
+        case 25: return a.keys == a.vals  // 7.75 KiB windows, one wave per workgroup: 17 waves per CU
+                        ? launch_wsweep_t<2, 7936, 6, false, true, 0, 13, false, true, true, true, true, false, 1>(a, stream)
+                        : launch_wsweep_t<2, 7936, 6, false, true, 0, 13, false, true, true, false, true, false, 1>(a, stream);
+        case 26: return a.keys == a.vals  // round 4's product: four waves per workgroup
+                        ? launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, true, true, false, 4>(a, stream)
+                        : launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, true, false, 4>(a, stream);
         default: return hipErrorInvalidValue;
     }
 }
