@@ -35,10 +35,12 @@ hipError_t launch_hash_batch_variant(const BatchArgs& args, hipStream_t stream, 
         // the automatic policy's kernels (auto_variant)
         case 12: return launch_chunk<true>(args, stream);
         case 20: return launch_regroup<8, true, false>(args, stream);
-        case 21: return launch_regroup<4, true, false>(args, stream);
+        // 21 and 46: one wave per workgroup (round 5, profiles/r5/ab_wpb.jsonl: config 2 0.331 vs 0.336 ms,
+        // mixed 2.18 vs 2.31; 25 and 12 keep four: 2.246 vs 2.302, 0.146 vs 0.147)
+        case 21: return launch_regroup<4, true, false, true, false, false, false, 0, 1>(args, stream);
         case 25: return launch_regroup<16, true, false, false>(args, stream);
         case 44: return launch_regroup<2, true, true, true, true, false, true, 1>(args, stream);
-        case 46: return launch_regroup<8, true, true, true, false, false, true, 1>(args, stream);
+        case 46: return launch_regroup<8, true, true, true, false, false, true, 1, 1>(args, stream);
         case 212: return launch_hash_wstage_product(args, stream);  // hdx_wstage.hip
         case 300: return launch_hash_wide(args, stream);            // hdx_wide.hip
         default:
@@ -190,19 +192,19 @@ const char* variant_kernel_name(int v) {
         case 12: return "void hdx::hash_chunk_kernel<true, false, 0, false>(hdx::BatchArgs)";
         case 30: return "void hdx::hash_chunk_kernel<true, true, 0, false>(hdx::BatchArgs)";
         case 31: return "void hdx::hash_chunk_kernel<true, false, 0, true>(hdx::BatchArgs)";
-        case 18: return "void hdx::hash_regroup_kernel<4, true, true, true, false, false, false, 0>(hdx::BatchArgs)";
-        case 19: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, false, 0>(hdx::BatchArgs)";
-        case 20: return "void hdx::hash_regroup_kernel<8, true, false, true, false, false, false, 0>(hdx::BatchArgs)";
-        case 21: return "void hdx::hash_regroup_kernel<4, true, false, true, false, false, false, 0>(hdx::BatchArgs)";
-        case 25: return "void hdx::hash_regroup_kernel<16, true, false, false, false, false, false, 0>(hdx::BatchArgs)";
-        case 26: return "void hdx::hash_regroup_kernel<2, true, true, true, false, false, false, 0>(hdx::BatchArgs)";
-        case 35: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, false, 0>(hdx::BatchArgs)";
-        case 37: return "void hdx::hash_regroup_kernel<2, true, true, true, true, true, false, 0>(hdx::BatchArgs)";
-        case 38: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true, 0>(hdx::BatchArgs)";
-        case 39: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, true, 0>(hdx::BatchArgs)";
-        case 44: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true, 1>(hdx::BatchArgs)";
-        case 45: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true, 2>(hdx::BatchArgs)";
-        case 46: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, true, 1>(hdx::BatchArgs)";
+        case 18: return "void hdx::hash_regroup_kernel<4, true, true, true, false, false, false, 0, 4>(hdx::BatchArgs)";
+        case 19: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, false, 0, 4>(hdx::BatchArgs)";
+        case 20: return "void hdx::hash_regroup_kernel<8, true, false, true, false, false, false, 0, 4>(hdx::BatchArgs)";
+        case 21: return "void hdx::hash_regroup_kernel<4, true, false, true, false, false, false, 0, 1>(hdx::BatchArgs)";
+        case 25: return "void hdx::hash_regroup_kernel<16, true, false, false, false, false, false, 0, 4>(hdx::BatchArgs)";
+        case 26: return "void hdx::hash_regroup_kernel<2, true, true, true, false, false, false, 0, 4>(hdx::BatchArgs)";
+        case 35: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, false, 0, 4>(hdx::BatchArgs)";
+        case 37: return "void hdx::hash_regroup_kernel<2, true, true, true, true, true, false, 0, 4>(hdx::BatchArgs)";
+        case 38: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true, 0, 4>(hdx::BatchArgs)";
+        case 39: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, true, 0, 4>(hdx::BatchArgs)";
+        case 44: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true, 1, 4>(hdx::BatchArgs)";
+        case 45: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true, 2, 4>(hdx::BatchArgs)";
+        case 46: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, true, 1, 1>(hdx::BatchArgs)";
         case 300: return "hdx::hash_wide_kernel(hdx::BatchArgs)";
         case 212: return "void hdx::hash_wstage_kernel<2, 8832u, 0, 5, 4, 0, false, true, true, true, false, 1>(hdx::BatchArgs)";
         default: return "";

@@ -207,11 +207,11 @@ __device__ __forceinline__ void class_sort(uint32_t* cnt, uint16_t* perm, const 
 // chunks in slot order, one coalesced 512 B store each.  A wave whose C*64
 // slots all share one class skips the permutation.
 // ===========================================================================
-template <int C>
+template <int C, int WPB = 4>
 struct RegroupLds {
-    SlotDesc desc[4][C * 64];   // reused for the coordinates in phase 2
-    uint16_t perm[4][C * 64];
-    uint32_t cnt[4][kClasses];  // ASORT: per-class counters / cursors
+    SlotDesc desc[WPB][C * 64];   // reused for the coordinates in phase 2
+    uint16_t perm[WPB][C * 64];
+    uint32_t cnt[WPB][kClasses];  // ASORT: per-class counters / cursors
 };
 
 // A4: dword-aligned loads (hdx_loads.h); PIPE: the > 64-byte loop keeps the
@@ -223,8 +223,8 @@ struct RegroupLds {
 // lookup_region, hdx_region_lookup.h; tbl = the workgroup's LDS copies) and
 // stores coordinates only when args.coords is set.
 template <int C, bool NT_STORE, bool SORT, bool DIRECT, bool A4, bool PIPE, bool ASORT, int ORDER, bool REG,
-          bool UNI = false, bool REGD = false, bool QUAD = false, int LATE = 0>
-__device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C>& lds, const uint64_t* tbl,
+          bool UNI = false, bool REGD = false, bool QUAD = false, int LATE = 0, class Lds = RegroupLds<C>>
+__device__ __forceinline__ void regroup_body(const BatchArgs& args, Lds& lds, const uint64_t* tbl,
                                              uint64_t wave = ~0ull) {
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
@@ -232,7 +232,7 @@ __device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C
     uint16_t* perm = lds.perm[w];
     uint64_t* res = reinterpret_cast<uint64_t*>(desc);  // res[2*s] = first 8 bytes of desc[s]
 
-    if (wave == ~0ull) wave = (uint64_t)blockIdx.x * 4 + w;
+    if (wave == ~0ull) wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + w;
     const uint32_t A = args.A;
     uint64_t qw, nslots, o_begin = 0, o_end = 0;  // nslots: end of this wave's slots
     if constexpr (REG) {
@@ -450,11 +450,13 @@ __device__ __forceinline__ void regroup_body(const BatchArgs& args, RegroupLds<C
     if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
+// WPB: waves per workgroup (each with its own LDS; the workgroup keeps it all
+// until its last wave ends).
 template <int C, bool NT_STORE, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false,
-          bool ASORT = false, int ORDER = 0>
-__global__ void __launch_bounds__(256)
+          bool ASORT = false, int ORDER = 0, int WPB = 4>
+__global__ void __launch_bounds__(64 * WPB)
 hash_regroup_kernel(const BatchArgs args) {
-    __shared__ RegroupLds<C> lds;
+    __shared__ RegroupLds<C, WPB> lds;
     regroup_body<C, NT_STORE, SORT, DIRECT, A4, PIPE, ASORT, ORDER, false>(args, lds, nullptr);
 }
 
@@ -479,24 +481,24 @@ hash_regroup_regions_kernel(const BatchArgs args) {
 }
 
 template <int C, bool NT, bool SORT = true, bool DIRECT = true, bool A4 = false, bool PIPE = false,
-          bool ASORT = false, int ORDER = 0>
+          bool ASORT = false, int ORDER = 0, int WPB = 4>
 inline hipError_t launch_regroup(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
-    const uint64_t blocks = (waves + 3) / 4;
+    const uint64_t blocks = (waves + WPB - 1) / WPB;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT, DIRECT, A4, PIPE, ASORT, ORDER>), dim3((uint32_t)blocks), dim3(256), 0,
-                       stream, args);
+    hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT, DIRECT, A4, PIPE, ASORT, ORDER, WPB>), dim3((uint32_t)blocks),
+                       dim3(64 * WPB), 0, stream, args);
     return hipGetLastError();
 }
 
-template <bool NT, bool PIPE = false, int SHAPE = 0, bool A4 = false>
+template <bool NT, bool PIPE = false, int SHAPE = 0, bool A4 = false, int WPB = 4>
 inline hipError_t launch_chunk(const BatchArgs& args, hipStream_t stream) {
     const uint64_t waves = (args.n * args.A + 63) / 64;
-    const uint64_t blocks = (waves + 3) / 4;
+    const uint64_t blocks = (waves + WPB - 1) / WPB;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_chunk_kernel<NT, PIPE, SHAPE, A4>), dim3((uint32_t)blocks), dim3(256), 0, stream, args);
+    hipLaunchKernelGGL((hash_chunk_kernel<NT, PIPE, SHAPE, A4>), dim3((uint32_t)blocks), dim3(64 * WPB), 0, stream, args);
     return hipGetLastError();
 }
 
