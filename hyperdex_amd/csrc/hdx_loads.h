@@ -595,6 +595,17 @@ __device__ __forceinline__ void split_slot(uint64_t q, uint32_t A, double inv_A,
     j0 = (uint32_t)rem;
 }
 
+// XCD-aware block order: the dispatcher deals workgroups round-robin over
+// the 8 XCDs (block b to XCD b % 8), each with its own L2.  Renumbering so
+// that each XCD's blocks take one contiguous run of the logical order keeps
+// neighbouring groups — which share the cache lines at their span edges — on
+// one L2.  A bijection on [0, gridDim.x).
+__device__ __forceinline__ uint32_t xcd_block() {
+    const uint32_t nb = gridDim.x, b = blockIdx.x;
+    const uint32_t per = nb >> 3, rem = nb & 7, x = b & 7, k = b >> 3;
+    return x < rem ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
+}
+
 __device__ __forceinline__ uint32_t wave_sum_dpp(uint32_t v) {
     return __builtin_amdgcn_readlane(wave_scan_dpp(v), 63);
 }

@@ -207,7 +207,7 @@ __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, 
 // span copy, addresses and predicate per KiB (dma_units16_loop).  WPB: waves
 // (each with its own window) per workgroup.
 template <int NCH, uint32_t WB, int SHAPE = 0, int HT = 0, int ORDER = 1, int W128 = 0, bool REGIONS = false,
-          bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false, int WPB = 4>
+          bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false, int WPB = 4, bool XS = false>
 __global__ void __launch_bounds__(64 * WPB)
 hash_wstage_kernel(const BatchArgs args) {
     static_assert(NCH >= 1 && NCH <= 4 && WB % 16 == 0, "slot indices are 8 bits; windows whole DMA units");
@@ -223,7 +223,7 @@ hash_wstage_kernel(const BatchArgs args) {
     uint32_t* cnt = meta.cnt[w];
     const ldsw_t lw = as_ldsw(win_all[w]);
 
-    const uint64_t o0 = ((uint64_t)blockIdx.x * WPB + w) * args.K;
+    const uint64_t o0 = ((uint64_t)(XS ? xcd_block() : blockIdx.x) * WPB + w) * args.K;
     if (o0 >= args.n) return;  // no barrier anywhere: waves are independent
     const Group<NCH> g = describe_group<NCH, WB, SHAPE, ORDER, ADMA, DL>(args, o0, win, 0, desc);
 
@@ -259,7 +259,8 @@ hash_wstage_kernel(const BatchArgs args) {
 // Launch: K = floor(64 * NCH / A) whole objects per wave (at most 63), four
 // independent waves per 256-thread workgroup, no workgroup barrier.
 template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, int HT = 0, int ORDER = 1, int W128 = 0,
-          bool REGIONS = false, bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false, int WPB = 4>
+          bool REGIONS = false, bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false, int WPB = 4,
+          bool XS = false>
 static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     // lane o holds object o's base and lane K the next group's first: K <= 63
     args.K = std::min<uint32_t>(std::min<uint32_t>((uint32_t)(64 * NCH) / args.A, KCAP), 63u);
@@ -268,7 +269,7 @@ static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     const uint64_t blocks = (waves + WPB - 1) / WPB;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA, PU, DL, WPB>),
+    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA, PU, DL, WPB, XS>),
                        dim3((uint32_t)blocks), dim3(64 * WPB), 0, stream, args);
     return hipGetLastError();
 }

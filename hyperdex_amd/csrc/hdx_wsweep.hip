@@ -153,7 +153,7 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
 // form 22, correct coordinates): the walk's reads as round 3's dword pairs.
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
           bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true, bool DL = false,
-          int WPB = 4>
+          int WPB = 4, bool XS = false>
 __global__ void __launch_bounds__(64 * WPB)
 hash_sweep_wstage_kernel(const EncodedArgs a) {
     constexpr uint32_t SL = NCH * 64;
@@ -172,7 +172,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
     uint8_t* codes = codes_all[w];
     const uint32_t A = a.A;
     const uint32_t K = std::min<uint32_t>(SL / A, KCAP);
-    const uint64_t o0 = ((uint64_t)blockIdx.x * WPB + w) * K;
+    const uint64_t o0 = ((uint64_t)(XS ? xcd_block() : blockIdx.x) * WPB + w) * K;
     if (o0 >= a.n) return;
     const uint32_t nobj = (uint32_t)std::min<uint64_t>(K, a.n - o0);
     const uint32_t ns = nobj * A;
@@ -422,14 +422,14 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
 
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
           bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true, bool DL = false,
-          int WPB = 4>
+          int WPB = 4, bool XS = false>
 static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
     const uint32_t K = std::min<uint32_t>(64 * NCH / a.A, KCAP);
     if (K == 0) return hipErrorInvalidValue;
     const uint64_t waves = (a.n + K - 1) / K;
     const uint64_t blocks = (waves + WPB - 1) / WPB;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU, BF, RECS, KUNITS, DL, WPB>),
+    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU, BF, RECS, KUNITS, DL, WPB, XS>),
                        dim3((uint32_t)blocks), dim3(64 * WPB), 0, stream, a);
     return hipGetLastError();
 }
@@ -494,6 +494,9 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 25: return a.keys == a.vals  // 7.75 KiB windows, one wave per workgroup: 17 waves per CU
                         ? launch_wsweep_t<2, 7936, 6, false, true, 0, 13, false, true, true, true, true, false, 1>(a, stream)
                         : launch_wsweep_t<2, 7936, 6, false, true, 0, 13, false, true, true, false, true, false, 1>(a, stream);
+        case 27: return a.keys == a.vals  // the product, XCD-aware block order
+                        ? launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, true, true, false, 1, true>(a, stream)
+                        : launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, true, false, 1, true>(a, stream);
         case 26: return a.keys == a.vals  // round 4's product: four waves per workgroup
                         ? launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, true, true, false, 4>(a, stream)
                         : launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, true, false, 4>(a, stream);
