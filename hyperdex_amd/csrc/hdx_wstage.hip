@@ -13,13 +13,13 @@ namespace hdx {
 
 hipError_t launch_hash_wstage_product(const BatchArgs& args, hipStream_t stream) {
     if (args.n == 0) return hipSuccess;
-    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, false, true, true, true, false, 1>(args, stream);
+    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, false, true, true, true, false, 1, true>(args, stream);
 }
 
 // ... with the fused region lookup (args.T tables; args.coords may be NULL)
 hipError_t launch_hash_wstage_regions(const BatchArgs& args, hipStream_t stream) {
     if (args.n == 0) return hipSuccess;
-    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, true, true, true, true, false, 1>(args, stream);
+    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, true, true, true, true, false, 1, true>(args, stream);
 }
 
 }  // namespace hdx
