@@ -119,6 +119,7 @@ static bool known_variant(int v) {
         case 259:  // 212 / the sweep as in round 4: four waves per workgroup
         case 270:  // 212 / the product sweep with the XCD-aware block order
         case 271:  // the sweep with 7 objects per wave (9.5 KiB windows)
+        case 272:  // the sweep with 7 objects per wave (9 KiB windows)
         case 210: case 211:  // wave-staged, sorted over the workgroup
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 49: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)

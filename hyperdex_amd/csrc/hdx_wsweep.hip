@@ -443,16 +443,19 @@ static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
 // One wave per workgroup (round 5: 3.466 vs 3.626 ms per 10 M on the key
 // column for four, whose 40 KiB stayed allocated until the slowest of the four
 // finished; profiles/r5/ab_wpb.jsonl), in the XCD-aware block order
-// (xcd_block: 3.412 vs 3.447 ms, profiles/r5/ab_xcd.jsonl).
+// (xcd_block: 3.412 vs 3.447 ms, profiles/r5/ab_xcd.jsonl), 7 objects per
+// wave in 9.5 KiB windows (the per-wave skeleton over one more object:
+// 3.301 vs 3.415 ms for 6 in 8.5 KiB; 9 KiB windows 3.343 — a group of 7
+// then overflows the window more often; profiles/r5/ab_sweep_k7.jsonl).
 hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
     const bool recs = a.keys == a.vals;
     if (a.T)
-        return recs ? launch_wsweep_t<2, 8704, 6, true, true, 0, 13, false, true, true, true, true, false, 1, true>(a, stream)
-                    : launch_wsweep_t<2, 8704, 6, true, true, 0, 13, false, true, true, false, true, false, 1, true>(a, stream);
+        return recs ? launch_wsweep_t<2, 9728, 7, true, true, 0, 13, false, true, true, true, true, false, 1, true>(a, stream)
+                    : launch_wsweep_t<2, 9728, 7, true, true, 0, 13, false, true, true, false, true, false, 1, true>(a, stream);
     if (!a.coords) return hipErrorInvalidValue;
-    return recs ? launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, true, true, false, 1, true>(a, stream)
-                : launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, true, false, 1, true>(a, stream);
+    return recs ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true>(a, stream)
+                : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true>(a, stream);
 }
 
 #ifndef HDX_DEBUG_BUILD
@@ -501,6 +504,9 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 28: return a.keys == a.vals  // 7 objects per wave in 9.5 KiB windows (one wave per workgroup, XCD order)
                         ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true>(a, stream)
                         : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true>(a, stream);
+        case 29: return a.keys == a.vals  // 7 objects per wave in 9 KiB windows (one wave per workgroup, XCD order)
+                        ? launch_wsweep_t<2, 9216, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true>(a, stream)
+                        : launch_wsweep_t<2, 9216, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true>(a, stream);
         case 26: return a.keys == a.vals  // round 4's product: four waves per workgroup
                         ? launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, true, true, false, 4>(a, stream)
                         : launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, true, false, 4>(a, stream);

@@ -16,6 +16,7 @@
 #   profile[=MODE]     scripts/profile_r2.sh TAG MODE (round evidence: MODE trace | pmc | all)
 #   py=SCRIPT[,ARGS]   python SCRIPT ARGS (commas for spaces)
 #   sh=SCRIPT[,ARGS]   bash SCRIPT ARGS (commas for spaces)
+#   exe=PROG[,ARGS]    ./PROG ARGS (a built tool; commas for spaces)
 set -o pipefail
 TAG=${1:?tag}; shift
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -62,6 +63,8 @@ for STEP in "$@"; do
       timeout -k 10 900 python -u ${arg//,/ } > "$log" 2> "$log.err" ;;
     sh)
       timeout -k 10 900 bash ${arg//,/ } > "$log" 2> "$log.err" ;;
+    exe)
+      timeout -k 10 300 ${arg//,/ } > "$log" 2> "$log.err" ;;
     *)
       echo "unknown step $STEP"; exit 2 ;;
   esac

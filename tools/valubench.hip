@@ -79,7 +79,10 @@ struct Fma64 {
     }
 };
 
-template <class Op>
+// LANES: how many lanes of each wave run the loop (64 = all; 32 = the
+// lower half only; 8; 1) — does a wave64 instruction cost less on the
+// SIMD-32 when one half of its exec mask is empty?
+template <class Op, int LANES = 64>
 __global__ void __launch_bounds__(256) k_valu(uint32_t* out, uint32_t seed, unsigned long long* clk) {
     uint32_t r[8];
 #pragma unroll
@@ -87,7 +90,8 @@ __global__ void __launch_bounds__(256) k_valu(uint32_t* out, uint32_t seed, unsi
     const uint32_t k = seed | 1u;
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
     const uint64_t w0 = __builtin_amdgcn_s_memrealtime();
-    for (int it = 0; it < kIters; ++it) Op::run(r, k);
+    if (LANES == 64 || (int)(threadIdx.x & 63) < LANES)
+        for (int it = 0; it < kIters; ++it) Op::run(r, k);
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
     const uint64_t w1 = __builtin_amdgcn_s_memrealtime();
     uint32_t x = 0;
@@ -100,17 +104,17 @@ __global__ void __launch_bounds__(256) k_valu(uint32_t* out, uint32_t seed, unsi
     }
 }
 
-template <class Op>
+template <class Op, int LANES = 64>
 static void bench(uint32_t* out, unsigned long long* clk, int cus) {
     const int waves_per_simd = 8;
     const int blocks = cus * waves_per_simd;  // 4 waves per block = one per SIMD
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    hipLaunchKernelGGL(k_valu<Op>, dim3(blocks), dim3(256), 0, 0, out, 7u, clk);
+    hipLaunchKernelGGL((k_valu<Op, LANES>), dim3(blocks), dim3(256), 0, 0, out, 7u, clk);
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0));
-    hipLaunchKernelGGL(k_valu<Op>, dim3(blocks), dim3(256), 0, 0, out, 7u, clk);
+    hipLaunchKernelGGL((k_valu<Op, LANES>), dim3(blocks), dim3(256), 0, 0, out, 7u, clk);
     CK(hipEventRecord(e1));
     CK(hipEventSynchronize(e1));
     float ms = 0;
@@ -122,8 +126,8 @@ static void bench(uint32_t* out, unsigned long long* clk, int cus) {
     const double cycles_per_instr = (ms * 1e-3 * ghz * 1e9) / wave_instr_per_simd;
     // in-kernel: block 0's wave 0 cycles over its own instructions (it shares the SIMD with 7 others)
     const double incl = (double)h[0] / ((double)kIters * 8) / waves_per_simd;
-    printf("{\"op\": \"%s\", \"ms\": %.4f, \"clock_ghz\": %.3f, \"cycles_per_wave_instr\": %.2f, "
-           "\"in_kernel_cycles_per_wave_instr\": %.2f}\n", Op::s, ms, ghz, cycles_per_instr, incl);
+    printf("{\"op\": \"%s\", \"lanes\": %d, \"ms\": %.4f, \"clock_ghz\": %.3f, \"cycles_per_wave_instr\": %.2f, "
+           "\"in_kernel_cycles_per_wave_instr\": %.2f}\n", Op::s, LANES, ms, ghz, cycles_per_instr, incl);
 }
 
 int main() {
@@ -144,5 +148,13 @@ int main() {
     bench<MadU64>(out, clk, cus);
     bench<LshlAdd64>(out, clk, cus);
     bench<Fma64>(out, clk, cus);
+    // half-empty exec masks
+    bench<Add, 32>(out, clk, cus);
+    bench<Add, 8>(out, clk, cus);
+    bench<AlignBit, 32>(out, clk, cus);
+    bench<MulLo, 32>(out, clk, cus);
+    bench<MadU64, 32>(out, clk, cus);
+    bench<MadU64, 8>(out, clk, cus);
+    bench<LshlAdd64, 32>(out, clk, cus);
     return 0;
 }
