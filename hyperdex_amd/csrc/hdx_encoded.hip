@@ -471,10 +471,11 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
             if (e != hipErrorInvalidValue) return e;
             break;
         }
-        case 256: case 257: case 258: case 259: case 270: case 271: case 272: {  // the product sweep with one / two waves per
+        case 256: case 257: case 258: case 259: case 270: case 271: case 272: case 273: {  // the product sweep with one / two waves per
             // workgroup, 7.75 KiB windows, four waves; 270: XCD-aware block order; 271: 7 objects per wave
             const int v = hash_variant();
-            const hipError_t e = launch_hash_wsweep(a, stream, v == 270 ? 27 : v == 271 ? 28 : v == 272 ? 29 : v - 256 + 23);
+            const hipError_t e = launch_hash_wsweep(a, stream, v == 270 ? 27 : v == 271 ? 28 : v == 272 ? 29 : v == 273 ? 30
+                                                                                                     : v - 256 + 23);
             if (e != hipErrorInvalidValue) return e;
             break;
         }

@@ -147,9 +147,11 @@ __device__ __forceinline__ uint32_t work_class1_bf(uint32_t code, uint32_t n, bo
 // skips the class's regime code (config 3b: the <= 16 / 17..32 regime;
 // config 5's sweep: the first > 64-byte loop).  Without GAP (or without pads
 // enough) pads follow the last class.  fence(): the wave's LDS fence.
+// pos_out (may be NULL): each of the lane's NCH slots' position in perm.
 template <int NCH, bool GAP, class Fence>
 __device__ __forceinline__ void class_sort(uint32_t* cnt, uint16_t* perm, const uint32_t (&cls)[NCH],
-                                           const uint32_t (&code)[NCH], uint32_t ns, Fence fence) {
+                                           const uint32_t (&code)[NCH], uint32_t ns, Fence fence,
+                                           uint32_t* pos_out = nullptr) {
     const int lane = threadIdx.x & 63;
     if (lane < kClasses) cnt[lane] = 0;
     fence();
@@ -188,6 +190,7 @@ __device__ __forceinline__ void class_sort(uint32_t* cnt, uint16_t* perm, const 
             pos = p < gap ? gap_at + p : ns + p;
         }
         perm[pos] = (uint16_t)(s | (code[c] << 8));
+        if (pos_out) pos_out[c] = pos;
     }
     fence();
 }

@@ -47,11 +47,18 @@ namespace {
 
 typedef __attribute__((address_space(3))) void* lds_void_t;
 
-template <int NCH, int WPB = 4>
+template <int NCH, int WPB = 4, bool RD = false>
 struct WStageMeta {
     uint64_t desc[WPB][NCH * 64];  // {offset u32, length u32}; then the slot's parked coordinate
     uint16_t perm[WPB][NCH * 64];  // slot | code << 8, in class order
     uint32_t cnt[WPB][kClasses];
+};
+// RD (descriptors in registers): no desc array
+template <int NCH, int WPB>
+struct WStageMeta<NCH, WPB, true> {
+    uint16_t perm[WPB][NCH * 64];
+    uint32_t cnt[WPB][kClasses];
+    uint64_t desc[WPB][1];  // unused
 };
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
@@ -76,6 +83,7 @@ struct Group {
     uint32_t nobj, ns;
     bool staged;
     uint32_t L[NCH], code[NCH], cls[NCH];
+    uint32_t doff[NCH];  // the slot's descriptor offset (desc[s]'s low word)
 };
 
 // Phases 1-3a: bases and lengths, the span's DMA into win (early when the
@@ -167,7 +175,8 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
         const uint32_t o = div_small(s, args.a_magic);
         const uint32_t orel = (uint32_t)__shfl((int)rel, (int)(o & 63), 64);
         const uint32_t doff = g.staged ? orel + off[c] : off[c];
-        desc[s] = (uint64_t)doff | ((uint64_t)g.L[c] << 32);
+        g.doff[c] = doff;
+        if (desc) desc[s] = (uint64_t)doff | ((uint64_t)g.L[c] << 32);
         g.cls[c] = ORDER == 3   ? work_class3(g.code[c], g.L[c], s < g.ns)
                    : ORDER == 4 ? work_class1_bf(g.code[c], g.L[c], s < g.ns)
                                 : work_class<1>(g.code[c], g.L[c], s < g.ns);
@@ -207,18 +216,20 @@ __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, 
 // span copy, addresses and predicate per KiB (dma_units16_loop).  WPB: waves
 // (each with its own window) per workgroup.
 template <int NCH, uint32_t WB, int SHAPE = 0, int HT = 0, int ORDER = 1, int W128 = 0, bool REGIONS = false,
-          bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false, int WPB = 4, bool XS = false>
+          bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false, int WPB = 4, bool XS = false,
+          bool RD = false>
 __global__ void __launch_bounds__(64 * WPB)
 hash_wstage_kernel(const BatchArgs args) {
     static_assert(NCH >= 1 && NCH <= 4 && WB % 16 == 0, "slot indices are 8 bits; windows whole DMA units");
+    static_assert(!(RD && REGIONS), "the fused lookups read the coordinates parked in desc");
     constexpr uint32_t FRONT = HT ? kFrontHT : 0;
     // +64: dword over-reads past the span; HT: 32 bytes before it (short strings' tail reads)
     __shared__ __attribute__((aligned(16))) uint8_t win_all[WPB][FRONT + WB + 64];
-    __shared__ WStageMeta<NCH, WPB> meta;
+    __shared__ WStageMeta<NCH, WPB, RD> meta;
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     uint8_t* win = win_all[w] + FRONT;
-    uint64_t* desc = meta.desc[w];
+    uint64_t* desc = RD ? nullptr : meta.desc[w];
     uint16_t* perm = meta.perm[w];
     uint32_t* cnt = meta.cnt[w];
     const ldsw_t lw = as_ldsw(win_all[w]);
@@ -228,9 +239,51 @@ hash_wstage_kernel(const BatchArgs args) {
     const Group<NCH> g = describe_group<NCH, WB, SHAPE, ORDER, ADMA, DL>(args, o0, win, 0, desc);
 
     // ---- counting sort by work class (wave-local) --------------------------
-    class_sort<NCH, GAP>(cnt, perm, g.cls, g.code, g.ns, wave_lds_fence);
+    uint32_t pos[NCH];
+    class_sort<NCH, GAP>(cnt, perm, g.cls, g.code, g.ns, wave_lds_fence, RD ? pos : nullptr);
     // every LDS-DMA of this wave must have landed before the window is read
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    if constexpr (RD) {
+        // RD: descriptors and coordinates stay in registers.  Pass t's lane
+        // reads its slot s's descriptor from lane s % 64's registers (set
+        // s / 64) by ds_bpermute, and a coordinate goes back to its slot's
+        // lane the same way (from the lane and pass its position in perm
+        // names) — no desc array in LDS: 1 KiB less per wave.
+        bool bad = false;
+        uint64_t res[NCH];
+#pragma unroll(PU ? NCH : 1)
+        for (int t = 0; t < NCH; ++t) {
+            const uint32_t e = perm[t * 64 + lane];
+            const uint32_t s = e & 0xffu, src = s & 63u, set = s >> 6;
+            uint32_t doff = 0, ln = 0;
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) {
+                const uint32_t d = (uint32_t)__shfl((int)g.doff[c], (int)src, 64);
+                const uint32_t l = (uint32_t)__shfl((int)g.L[c], (int)src, 64);
+                if (set == (uint32_t)c) {
+                    doff = d;
+                    ln = l;
+                }
+            }
+            res[t] = hash_slot<SHAPE, HT, W128>(args, lw, g.staged, g.mybase, s, e >> 8,
+                                                (uint64_t)doff | ((uint64_t)ln << 32), bad);
+        }
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) {
+            const uint32_t p = pos[c], src = p & 63u, pass = p >> 6;
+            uint64_t v = 0;
+#pragma unroll
+            for (int t = 0; t < NCH; ++t) {
+                const uint64_t x = shfl64(res[t], (int)src);
+                if (pass == (uint32_t)t) v = x;
+            }
+            const uint32_t s = (uint32_t)(c * 64 + lane);
+            if (s < g.ns) __builtin_nontemporal_store(v, args.coords + g.q0 + s);
+        }
+        if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
+        return;
+    }
 
     // ---- NCH class-sorted passes, coordinates parked over their descriptors ---
     bool bad = false;
@@ -260,7 +313,7 @@ hash_wstage_kernel(const BatchArgs args) {
 // independent waves per 256-thread workgroup, no workgroup barrier.
 template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, int HT = 0, int ORDER = 1, int W128 = 0,
           bool REGIONS = false, bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false, int WPB = 4,
-          bool XS = false>
+          bool XS = false, bool RD = false>
 static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     // lane o holds object o's base and lane K the next group's first: K <= 63
     args.K = std::min<uint32_t>(std::min<uint32_t>((uint32_t)(64 * NCH) / args.A, KCAP), 63u);
@@ -269,7 +322,7 @@ static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     const uint64_t blocks = (waves + WPB - 1) / WPB;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA, PU, DL, WPB, XS>),
+    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA, PU, DL, WPB, XS, RD>),
                        dim3((uint32_t)blocks), dim3(64 * WPB), 0, stream, args);
     return hipGetLastError();
 }

@@ -164,7 +164,11 @@ hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int for
         case 57: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 2>(args, stream);  // the product, two waves per workgroup
         case 58: return launch_wstage_t<2, 7680, 6, 0, 5, 4, 0, false, true, true, true, false, 1>(args, stream);  // <= 6 objects, 7.5 KiB windows: 18 waves per CU
         case 59: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 4>(args, stream);  // round 4's product: four waves per workgroup
-        case 70: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true>(args, stream);  // the product, XCD-aware block order
+        case 70: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true>(args, stream);  // the product (XCD-aware block order)
+        case 73: return launch_wstage_t<3, 14336, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true>(args, stream);  // 3 passes, 11 objects, 14 KiB
+        case 75: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, true>(args, stream);  // descriptors in registers (17 waves per CU)
+        case 76: return launch_wstage_t<2, 8704, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, true>(args, stream);  // ... with 8.5 KiB windows (18 waves per CU)
+        case 74: return launch_wstage_t<3, 13312, 10, 0, 5, 4, 0, false, true, true, true, false, 1, true>(args, stream);  // 3 passes, 10 objects, 13 KiB
         // the slots class-sorted over the workgroup
         case 10: return launch_wgstage_t<2, 8832>(args, stream);
         case 11: return launch_wgstage_t<1, 4352>(args, stream);

@@ -507,6 +507,9 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 29: return a.keys == a.vals  // 7 objects per wave in 9 KiB windows (one wave per workgroup, XCD order)
                         ? launch_wsweep_t<2, 9216, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true>(a, stream)
                         : launch_wsweep_t<2, 9216, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true>(a, stream);
+        case 30: return a.keys == a.vals  // 3 passes, 11 objects per wave in 14 KiB windows
+                        ? launch_wsweep_t<3, 14336, 11, false, true, 0, 13, false, true, true, true, true, false, 1, true>(a, stream)
+                        : launch_wsweep_t<3, 14336, 11, false, true, 0, 13, false, true, true, false, true, false, 1, true>(a, stream);
         case 26: return a.keys == a.vals  // round 4's product: four waves per workgroup
                         ? launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, true, true, false, 4>(a, stream)
                         : launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, true, false, 4>(a, stream);

@@ -304,10 +304,12 @@ def test_full_size_sampled(oracle, torch_dev, cfg):
 
 
 VARIANTS = [12, 18, 19, 20, 21, 25, 26, 30, 31, 35, 37, 38, 39, 44, 45, 46,
-            200, 201, 202, 203, 204, 205, 206, 210, 211, 212, 214, 215, 216, 219, 239, 240, 242, 244, 245, 246, 255, 300]
+            200, 201, 202, 203, 204, 205, 206, 210, 211, 212, 214, 215, 216, 219, 239, 240, 242, 244, 245, 246, 255, 256,
+            257, 258, 259, 270, 273, 274, 275, 276, 300]
 
 
-@pytest.mark.parametrize("variant", [200, 201, 202, 203, 204, 205, 206, 210, 211, 212, 214, 215, 216, 219, 239, 240, 242, 244, 245, 246, 255])
+@pytest.mark.parametrize("variant", [200, 201, 202, 203, 204, 205, 206, 210, 211, 212, 214, 215, 216, 219, 239, 240, 242, 244, 245, 246, 255,
+                                     256, 257, 258, 259, 270, 273, 274, 275, 276])
 def test_wave_staged_layouts(oracle, torch_dev, variant):
     """The wave-staged kernel (hdx_wstage.hip) stages a group's span only when
     its objects are back to back and fit the window: gaps after some objects
@@ -335,7 +337,7 @@ def test_wave_staged_layouts(oracle, torch_dev, variant):
         check_batch(oracle, torch, dev, types, blob, base, lens)
 
 
-@pytest.mark.parametrize("variant", [212, 255])
+@pytest.mark.parametrize("variant", [212, 255, 275, 276])
 def test_wave_staged_long_strings(oracle, torch_dev, variant):
     """Packed one-string objects, mostly of 0..128 bytes with a few of
     193..1000 per wave (0, 1, a few and many strings past two CityHash loop
