@@ -1088,6 +1088,7 @@ def pinned_passes(work, seconds, passes=3):
     import threading
     cpus = sorted(os.sched_getaffinity(0))
     n = len(work)
+    ready = threading.Barrier(n + 1)  # every thread prepared and warm before pass 0's clock starts
     start = threading.Barrier(n + 1)
     done = threading.Barrier(n + 1)
     reps = [[0] * passes for _ in range(n)]
@@ -1103,6 +1104,7 @@ def pinned_passes(work, seconds, passes=3):
             prepare, run, _, _ = work[k]
             state = prepare()
             run(state)  # warm: first-call page faults and allocations stay out of the passes
+            ready.wait()
             for p in range(passes):
                 start.wait()
                 while time.perf_counter() < deadline[0]:
@@ -1113,6 +1115,7 @@ def pinned_passes(work, seconds, passes=3):
             pass
         except Exception as e:  # noqa: BLE001 — re-raised on the main thread
             errors.append(e)
+            ready.abort()
             start.abort()
             done.abort()
     ths = [threading.Thread(target=worker, args=(k,), daemon=True) for k in range(n)]
@@ -1120,6 +1123,7 @@ def pinned_passes(work, seconds, passes=3):
         th.start()
     rates = []
     try:
+        ready.wait()
         for p in range(passes):
             deadline[0] = time.perf_counter() + seconds / passes
             t0 = time.perf_counter()
