@@ -905,10 +905,13 @@ def source_digest():
 
 def measured_valu(path, cfg, n, kernel_ms):
     """The VALU-issue roofline of the launch from the same
-    digest-matched PMC summary as `traffic`: SQ_INSTS_VALU per launch (scaled
-    to n) x 4 cycles (a wave64 vector instruction's issue cost on one SIMD,
-    MI355X_MICROARCH.md constants table) / (1024 SIMDs x the effective clock
-    of the PMC pass x this run's kernel time).  None when the summary has no
+    digest-matched PMC summary as `traffic`.  `valu_frac` is the PMC pass's own
+    ratio: SQ_INSTS_VALU x 4 cycles (a wave64 vector instruction's issue cost
+    on one SIMD, MI355X_MICROARCH.md constants table) / (1024 SIMDs x the
+    pass's busy cycles, GRBM_GUI_ACTIVE / 8 XCDs) -- instructions and cycles
+    from one run.  `valu_frac_at_2p4ghz` divides the same instructions (scaled
+    to n) by this run's kernel time at the 2.4 GHz peak clock: a lower bound,
+    since the clock under this load is lower.  None when the summary has no
     VALU record or measured other sources."""
     try:
         doc = json.load(open(path))
@@ -919,13 +922,13 @@ def measured_valu(path, cfg, n, kernel_ms):
         return None
     scale = n / rec.get("objects", 10_000_000)
     valu = rec["valu_insts"] * scale
-    clock = rec["effective_clock_ghz"] * 1e9
-    cycles = 1024 * clock * kernel_ms / 1e3
-    return {"valu_frac": round(valu * 4 / cycles, 4),
+    pmc_cycles = 1024 * rec["grbm_gui_active"] / 8
+    return {"valu_frac": round(rec["valu_insts"] * 4 / pmc_cycles, 4),
+            "valu_frac_at_2p4ghz": round(valu * 4 / (1024 * 2.4e9 * kernel_ms / 1e3), 4),
             "valu_insts_per_launch": int(valu), "salu_insts_per_launch": int(rec["salu_insts"] * scale),
             "valu_per_wave": round(rec["valu_per_wave"], 1), "salu_per_wave": round(rec["salu_per_wave"], 1),
-            "effective_clock_ghz": round(rec["effective_clock_ghz"], 3),
-            "convention": "SQ_INSTS_VALU x 4 cycles / (256 CUs x 4 SIMDs x effective clock x kernel time)"}
+            "pmc_effective_clock_ghz": round(rec["effective_clock_ghz"], 3),
+            "convention": "SQ_INSTS_VALU x 4 cycles / (256 CUs x 4 SIMDs x GRBM_GUI_ACTIVE/8) of the PMC pass"}
 
 
 def measured_traffic(path, cfg, n):

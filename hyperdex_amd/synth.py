@@ -66,6 +66,14 @@ CONFIGS = {
                + [_n(dt.HYPERDATATYPE_INT64)] * 3 + [_n(dt.HYPERDATATYPE_FLOAT)] * 3),
     "m3b128": ([_s(64)] + [Rule(dt.HYPERDATATYPE_STRING, UNIFORM, 0, 128)] * 10
                + [_n(dt.HYPERDATATYPE_INT64)] * 3 + [_n(dt.HYPERDATATYPE_FLOAT)] * 3),
+    # measurement-only: config 3b's attribute mix repeated to 200 / 1000 attributes
+    # (the A > 128 gather kernel 44 and the A > 256 wide kernel)
+    "w200": [_s(64)] + ([Rule(dt.HYPERDATATYPE_STRING, UNIFORM, 0, 195)] * 10
+                        + [_n(dt.HYPERDATATYPE_INT64)] * 3 + [_n(dt.HYPERDATATYPE_FLOAT)] * 3) * 12
+                      + [_s(64)] * 7,
+    "w1000": [_s(64)] + ([Rule(dt.HYPERDATATYPE_STRING, UNIFORM, 0, 195)] * 10
+                         + [_n(dt.HYPERDATATYPE_INT64)] * 3 + [_n(dt.HYPERDATATYPE_FLOAT)] * 3) * 62
+                       + [_s(64)] * 7,
 }
 
 

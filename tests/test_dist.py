@@ -144,6 +144,53 @@ def test_allgather_matches_single_process(world):
     assert all(ret[r] for r in range(world))
 
 
+_EXCHANGE_CASES = ([6, 6, 6], [5, 0, 7], [0, 0, 9], [1, 2, 3], [0, 0, 0])
+
+
+def _exchange_worker(rank, world, port, want, ret):
+    """allgather_coords on rank `rank`'s rows of the mix64 pattern, for each
+    case of _EXCHANGE_CASES; the result must equal every device matrix of the
+    C++ exchange plan (want[case] = world x N x ROW)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ok = True
+    for counts, plan_mats in zip(_EXCHANGE_CASES, want):
+        N = sum(counts)
+        first = sum(counts[:rank])
+        e = np.arange(first * 3, (first + counts[rank]) * 3, dtype=np.uint64) + np.uint64(1)
+        local = torch.from_numpy(synth.mix64(e).view(np.int64).reshape(counts[rank], 3))
+        got = hdist.allgather_coords(local, counts).numpy().view(np.uint64)  # padded form when unequal
+        ok &= got.shape == (N, 3)
+        for k in range(world):
+            ok &= bool(np.array_equal(got.reshape(-1), plan_mats[k]))
+    ret[rank] = ok
+    dist.destroy_process_group()
+
+
+def test_exchange_plan_matches_python_gather(tmp_path):
+    """The C-ABI device set's exchange plan (hdx_exchange.h, equal / unequal /
+    empty shards) leaves every device with the matrix dist.allgather_coords
+    gathers on the same shards (world 3, gloo)."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "exchange_dump")
+    subprocess.run(["g++", "-std=c++17", "-O1", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-I", os.path.join(root, "hyperdex_amd", "csrc"),
+                    os.path.join(root, "tests", "cpp", "exchange_dump.cc"), "-o", exe], check=True)
+    world = 3
+    want = []
+    for i, counts in enumerate(_EXCHANGE_CASES):
+        out = str(tmp_path / ("plan%d.bin" % i))
+        subprocess.run([exe, out, "3"] + [str(c) for c in counts], check=True)
+        mats = np.fromfile(out, dtype=np.uint64).reshape(world, -1) if sum(counts) else np.zeros((world, 0), np.uint64)
+        want.append(mats)
+    ctx = mp.get_context("spawn")
+    ret = ctx.Manager().dict()
+    mp.start_processes(_exchange_worker, args=(world, _free_port(), want, ret), nprocs=world, start_method="spawn")
+    assert all(ret[r] for r in range(world))
+
+
 @pytest.mark.gpu
 def test_hash_sharded_rccl_world1():
     """The RCCL branch of allgather_coords / hash_sharded in one process."""
