@@ -40,6 +40,16 @@ hipError_t launch_debug_variant(const BatchArgs& args, hipStream_t stream, int v
         case 263: return launch_regroup<8, true, false, true, false, false, false, 0, 1>(args, stream);
         case 264: return launch_regroup<8, true, true, true, false, false, true, 1, 1>(args, stream);
         case 265: return launch_regroup<2, true, true, true, true, false, true, 1, 1>(args, stream);
+        // deferred strings (round 5, hash_regroup_defer_kernel): 280 = 21 with the strings
+        // first, 281 = ... with cached stores, 282 = strings last, 283 = 8 chunks, 284 = A4 loads,
+        // 285 = strings last with cached stores, 286 = 8 chunks with cached stores
+        case 280: return launch_regroup_defer<4, true, false, 1>(args, stream);
+        case 281: return launch_regroup_defer<4, false, false, 1>(args, stream);
+        case 282: return launch_regroup_defer<4, true, false, 2>(args, stream);
+        case 283: return launch_regroup_defer<8, true, false, 1>(args, stream);
+        case 284: return launch_regroup_defer<4, true, true, 1>(args, stream);
+        case 285: return launch_regroup_defer<4, false, false, 2>(args, stream);
+        case 286: return launch_regroup_defer<8, false, false, 1>(args, stream);
         // wave-staged (hdx_wstage.hip): 200 2 passes / 10 KiB, 201 3 / 14 KiB, 202 2 / 8 KiB,
         // 203 1 / 5 KiB, 204 4 / 18 KiB, 205 2 / 8832 B, 206 = 205 with <= 6 objects
         case 200: case 201: case 202: case 203: case 204: case 205: case 206: case 207: case 208:
@@ -82,6 +92,7 @@ static bool known_variant(int v) {
         case -1: case 12: case 18: case 19: case 20: case 21: case 25: case 26: case 30: case 31: case 35: case 37:
         case 38: case 39: case 44: case 45: case 46:
         case 260: case 261: case 262: case 263: case 264: case 265:  // 21 / 25 / 12 / 20 / 46 / 44, one wave per workgroup
+        case 280: case 281: case 282: case 283: case 284: case 285: case 286:  // 21 with the string slots deferred to passes of their own
         case 300:  // the wide kernel (hdx_wide.hip), at any A
         case 301:  // the wide sweep (hdx_wide.hip), at any A
         case 100: case 101: case 102: case 103: case 104: case 105: case 106: case 107: case 108: case 109:

@@ -498,6 +498,22 @@ __device__ __forceinline__ uint64_t hash_blk(uint32_t code, const uint8_t* p, ui
     return hash_numeric(code, bits);
 }
 
+// hash_blk for a slot that is not a string (numerics, timestamps, non-hashable).
+template <bool A4 = false>
+__device__ __forceinline__ uint64_t hash_blk_nonstring(uint32_t code, const uint8_t* p, uint32_t n, const Blk& b,
+                                                       bool& bad) {
+    if (code == CODE_ZERO) return 0;
+    const uint32_t sh = (uint32_t)(uintptr_t)p & 15;
+    uint64_t bits = 0;
+    if (n == 8) {
+        bits = window8(A4 ? b.v1 : b.v0, A4 ? b.v3 : b.v1, sh);
+    } else if (n != 0) {
+        bad = true;
+        return 0;
+    }
+    return hash_numeric(code, bits);
+}
+
 // hash_blk (A4) with the > 64-byte loop quad-cooperative: called by the whole
 // wave; the loop runs, wave-uniformly, while any lane has a block left.
 __device__ __forceinline__ uint64_t hash_blk_quad(uint32_t code, const uint8_t* p, uint32_t n, const Blk& b,

@@ -226,7 +226,8 @@ struct RegroupLds {
 // lookup_region, hdx_region_lookup.h; tbl = the workgroup's LDS copies) and
 // stores coordinates only when args.coords is set.
 template <int C, bool NT_STORE, bool SORT, bool DIRECT, bool A4, bool PIPE, bool ASORT, int ORDER, bool REG,
-          bool UNI = false, bool REGD = false, bool QUAD = false, int LATE = 0, class Lds = RegroupLds<C>>
+          bool UNI = false, bool REGD = false, bool QUAD = false, int LATE = 0, int DEFER = 0,
+          class Lds = RegroupLds<C>>
 __device__ __forceinline__ void regroup_body(const BatchArgs& args, Lds& lds, const uint64_t* tbl,
                                              uint64_t wave = ~0ull) {
     const int lane = threadIdx.x & 63;
@@ -270,6 +271,14 @@ __device__ __forceinline__ void regroup_body(const BatchArgs& args, Lds& lds, co
     // REGD (unsorted waves only): each lane keeps its C descriptors in
     // registers — pass t's slot t * 64 + lane is the lane's own chunk-t slot
     static_assert(!REGD || (!SORT && !REG), "register descriptors need slot-order passes");
+    // DEFER (slot-order passes with direct stores only): the string slots are
+    // queued (perm) in phase 1 and hashed together in their own passes — 1
+    // string before the numeric passes, the first numeric pass's loads in
+    // flight; 2 after them — so a numeric pass no longer runs a string regime
+    // for the few key lanes among its numerics (config 2: 13 of 64).
+    static_assert(DEFER == 0 || (!SORT && DIRECT && !REG && !REGD && !QUAD && LATE == 0),
+                  "deferred strings need slot-order passes with direct stores");
+    uint32_t nq = 0;  // wave-uniform: queued string slots
     SlotDesc dreg[REGD ? C : 1];
     uint32_t cls[C];
 #pragma unroll
@@ -297,6 +306,14 @@ __device__ __forceinline__ void regroup_body(const BatchArgs& args, Lds& lds, co
         if constexpr (REGD) dreg[c] = d;
         else desc[c * 64 + lane] = d;
         cls[c] = work_class<ORDER>(code, L, valid);
+        if constexpr (DEFER != 0) {
+            const bool def = code == CODE_STRING;  // slots past the end are CODE_ZERO
+            const uint64_t m = __ballot(def);
+            if (def)
+                perm[nq + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
+                    (uint16_t)(c * 64 + lane);
+            nq += (uint32_t)__popcll(m);
+        }
     }
 
     // ---- counting sort by class (wave-local) ---------------------------------
@@ -359,13 +376,33 @@ __device__ __forceinline__ void regroup_body(const BatchArgs& args, Lds& lds, co
             // block; LATE 2: only the one-block strings (65..128 bytes)
             const bool g64 = (P.d.code_slot & 0xffu) == CODE_STRING && P.d.n > 64 && (LATE == 1 || P.d.n <= 128);
             P.blk = issue_any<A4>(g64 ? (uint32_t)CODE_ZERO : P.d.code_slot & 0xffu, P.d.p, g64 ? 0u : P.d.n);
+        } else if constexpr (DEFER != 0) {  // a queued string loads nothing here
+            const bool def = (P.d.code_slot & 0xffu) == CODE_STRING;
+            P.blk = issue_any<A4>(def ? (uint32_t)CODE_ZERO : P.d.code_slot & 0xffu, P.d.p, def ? 0u : P.d.n);
         } else {
             P.blk = issue_any<A4>(P.d.code_slot & 0xffu, P.d.p, P.d.n);
         }
     };
     bool bad = false;
+    // the queued strings: one lane per string, every lane in the same regimes
+    auto string_passes = [&]() {
+        for (uint32_t b0 = 0; b0 < nq; b0 += 64) {
+            const bool act = b0 + (uint32_t)lane < nq;
+            const uint32_t s = act ? perm[b0 + lane] : 0u;
+            const SlotDesc d = desc[s];
+            const uint32_t code = act ? (uint32_t)CODE_STRING : (uint32_t)CODE_ZERO;
+            const uint32_t n = act ? d.n : 0u;
+            const Raw r = issue_any<A4>(code, d.p, n);
+            const uint64_t h = hash_blk<PIPE, false, A4>(code, d.p, n, consume_any<A4>(r), bad);
+            if (act) {
+                if (NT_STORE) __builtin_nontemporal_store(h, args.coords + qw + s);
+                else args.coords[qw + s] = h;
+            }
+        }
+    };
     Pass P0, P1;
     load_pass(0, P0);
+    if constexpr (DEFER == 1) string_passes();  // pass 0's numerics in flight meanwhile
 #pragma unroll
     for (int t = 0; t < C; ++t) {
         Pass& cur = (t & 1) ? P1 : P0;
@@ -381,12 +418,15 @@ __device__ __forceinline__ void regroup_body(const BatchArgs& args, Lds& lds, co
         } else if constexpr (QUAD) {
             static_assert(A4, "the quad-cooperative loop follows the A4 piece layout");
             h = hash_blk_quad(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n, consume_any<A4>(cur.blk), bad);
+        } else if constexpr (DEFER != 0) {  // a queued string is hashed in its own pass
+            const uint32_t cd = cur.d.code_slot & 0xffu;
+            h = cd == CODE_STRING ? 0ull : hash_blk_nonstring<A4>(cd, cur.d.p, cur.d.n, consume_any<A4>(cur.blk), bad);
         } else {
             h = hash_blk<PIPE, false, A4>(cur.d.code_slot & 0xffu, cur.d.p, cur.d.n, consume_any<A4>(cur.blk), bad);
         }
         if (DIRECT && uniform && !REG) {  // pass t is chunk t in slot order: store straight to HBM
             const uint64_t q = qw + t * 64 + lane;
-            if (q < nslots) {
+            if (q < nslots && !(DEFER != 0 && (cur.d.code_slot & 0xffu) == CODE_STRING)) {
                 if (NT_STORE) __builtin_nontemporal_store(h, args.coords + q);
                 else args.coords[q] = h;
             }
@@ -394,6 +434,7 @@ __device__ __forceinline__ void regroup_body(const BatchArgs& args, Lds& lds, co
             res[2 * (cur.d.code_slot >> 8)] = h;
         }
     }
+    if constexpr (DEFER == 2) string_passes();
     if (DIRECT && uniform && !REG) {
         if (bad && args.status) atomicOr(args.status, 1u << 2 /* HDX_E_BADSIZE */);
         return;
@@ -463,6 +504,16 @@ hash_regroup_kernel(const BatchArgs args) {
     regroup_body<C, NT_STORE, SORT, DIRECT, A4, PIPE, ASORT, ORDER, false>(args, lds, nullptr);
 }
 
+// The regroup kernel with the string slots deferred to passes of their own
+// (DEFER 1: first, 2: last; slot-order passes, direct stores).
+template <int C, bool NT_STORE, bool A4, int DEFER, int WPB = 1>
+__global__ void __launch_bounds__(64 * WPB)
+hash_regroup_defer_kernel(const BatchArgs args) {
+    __shared__ RegroupLds<C, WPB> lds;
+    regroup_body<C, NT_STORE, false, true, A4, false, false, 0, false, false, false, false, 0, DEFER>(args, lds,
+                                                                                                   nullptr);
+}
+
 // hash + lookup_region in one launch (hdx_hash_batch_regions_device).  The
 // workgroup first copies the indexed tables that fit into LDS (its only
 // barrier, before any wave may leave).
@@ -492,6 +543,17 @@ inline hipError_t launch_regroup(const BatchArgs& args, hipStream_t stream) {
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
     hipLaunchKernelGGL((hash_regroup_kernel<C, NT, SORT, DIRECT, A4, PIPE, ASORT, ORDER, WPB>), dim3((uint32_t)blocks),
                        dim3(64 * WPB), 0, stream, args);
+    return hipGetLastError();
+}
+
+template <int C, bool NT, bool A4, int DEFER, int WPB = 1>
+inline hipError_t launch_regroup_defer(const BatchArgs& args, hipStream_t stream) {
+    const uint64_t waves = (args.n * args.A + C * 64 - 1) / (C * 64);
+    const uint64_t blocks = (waves + WPB - 1) / WPB;
+    if (blocks == 0) return hipSuccess;
+    if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((hash_regroup_defer_kernel<C, NT, A4, DEFER, WPB>), dim3((uint32_t)blocks), dim3(64 * WPB), 0,
+                       stream, args);
     return hipGetLastError();
 }
 

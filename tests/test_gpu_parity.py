@@ -212,6 +212,34 @@ def test_bad_size_sets_status(torch_dev):
     assert e.value.status == _lib.HDX_E_BADSIZE
 
 
+@pytest.mark.parametrize("variant", [12, 21, 25, 44, 46, 212, 280, 281, 282, 285, 286])
+def test_bad_size_every_variant(oracle, torch_dev, variant):
+    """A config-2 batch (key + 4 int64) with one 5-byte int64 in a late
+    object: HDX_E_BADSIZE, that coordinate 0, every other coordinate the
+    oracle's (the deferred-string forms hash the key in its own pass)."""
+    torch, dev = torch_dev
+    types, blob, base, lens = synth.make_batch_host("cfg2", 3001, seed=8)
+    A = len(types)
+    want, _ = oracle.hash_batch(types, blob, base, lens)
+    lens = lens.copy()
+    victim = 2900 * A + 3
+    assert lens[victim] == 8
+    lens[victim] = 5
+    with _lib.debug_library(variant):
+        status = torch.zeros(1, dtype=torch.int32, device=dev)
+        got = gpu_hash(torch, dev, types, blob, base, lens, status=status)
+    assert int(status.item()) == 1 << _lib.HDX_E_BADSIZE
+    got = np.asarray(got).reshape(-1)
+    assert got[victim] == 0
+    ok = np.ones(len(got), bool)
+    ok[victim] = False
+    # the shortened value moves the victim object's last attribute (bases are
+    # explicit, so no other object moves): compare every other object
+    o = victim // A
+    ok[o * A:(o + 1) * A] = False
+    assert np.array_equal(got[ok], want.reshape(-1)[ok])
+
+
 def test_bad_type_rejected_before_launch(torch_dev):
     torch, dev = torch_dev
     b, o, L = to_dev(torch, dev, np.zeros(8, np.uint8), np.zeros(1, np.uint64),
@@ -305,7 +333,7 @@ def test_full_size_sampled(oracle, torch_dev, cfg):
 
 VARIANTS = [12, 18, 19, 20, 21, 25, 26, 30, 31, 35, 37, 38, 39, 44, 45, 46,
             200, 201, 202, 203, 204, 205, 206, 210, 211, 212, 214, 215, 216, 219, 239, 240, 242, 244, 245, 246, 255, 256,
-            257, 258, 259, 270, 273, 274, 275, 276, 300]
+            257, 258, 259, 270, 273, 274, 275, 276, 280, 281, 282, 283, 284, 285, 286, 300]
 
 
 @pytest.mark.parametrize("variant", [200, 201, 202, 203, 204, 205, 206, 210, 211, 212, 214, 215, 216, 219, 239, 240, 242, 244, 245, 246, 255,
