@@ -70,9 +70,21 @@ __device__ __forceinline__ void dma_units16_loop(const uint8_t* src, void* dst, 
 // is predicated (round 3's loop recomputed both addresses and the predicate
 // for every KiB: ~6 VALU + ~8 SALU each).  ASM: inline asm (not seen by the
 // compiler's waits), else the builtin.
-template <bool ASM>
+// NT: the loads non-temporal (the `nt` policy bit: the span is read once).
+#define HDX_DMA_ASM(NTS, OFFS) "s_mov_b32 m0, %1\n\ts_nop 0\n\t" OFFS(NTS)
+#define HDX_DMA1(NTS) "global_load_lds_dwordx4 %0, off" NTS
+#define HDX_DMA2(NTS) HDX_DMA1(NTS) "\n\tglobal_load_lds_dwordx4 %0, off offset:1024" NTS
+#define HDX_DMA3(NTS) HDX_DMA2(NTS) "\n\tglobal_load_lds_dwordx4 %0, off offset:2048" NTS
+#define HDX_DMA4(NTS) HDX_DMA3(NTS) "\n\tglobal_load_lds_dwordx4 %0, off offset:3072" NTS
+#define HDX_DMA_EMIT(N)                                                                                      \
+    do {                                                                                                     \
+        if constexpr (NT) asm volatile(HDX_DMA_ASM(" nt", HDX_DMA##N)::"v"(p), "s"(m0) : "memory", "m0"); \
+        else asm volatile(HDX_DMA_ASM("", HDX_DMA##N)::"v"(p), "s"(m0) : "memory", "m0");                  \
+    } while (0)
+template <bool ASM, bool NT = false>
 __device__ __forceinline__ void dma_units16(const uint8_t* src, void* dst, uint32_t units) {
 #if defined(__HIP_DEVICE_COMPILE__)  // the host pass cannot instantiate the VGPR / SGPR constraints
+    constexpr int POL = NT ? 2 : 0;  // the builtin's cache-policy operand: nt
     const uint32_t lane = threadIdx.x & 63;
     const uint8_t* p = src + 16 * lane;
     uint32_t m0 = lds_addr_s(dst);
@@ -80,56 +92,38 @@ __device__ __forceinline__ void dma_units16(const uint8_t* src, void* dst, uint3
     uint32_t full = __builtin_amdgcn_readfirstlane(units >> 6);
     for (; full >= 4; full -= 4) {
         if constexpr (ASM)
-            asm volatile(
-                "s_mov_b32 m0, %1\n\ts_nop 0\n\t"
-                "global_load_lds_dwordx4 %0, off\n\tglobal_load_lds_dwordx4 %0, off offset:1024\n\t"
-                "global_load_lds_dwordx4 %0, off offset:2048\n\tglobal_load_lds_dwordx4 %0, off offset:3072" ::"v"(p),
-                "s"(m0)
-                : "memory", "m0");
+            HDX_DMA_EMIT(4);
         else {
-            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 1024, 0);
-            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 2048, 0);
-            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 3072, 0);
+            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 0, POL);
+            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 1024, POL);
+            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 2048, POL);
+            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 3072, POL);
         }
         p += 4096;
         m0 += 4096;
     }
     if (full) {
         if constexpr (ASM) {
-            if (full == 1)
-                asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(m0)
-                             : "memory", "m0");
-            else if (full == 2)
-                asm volatile(
-                    "s_mov_b32 m0, %1\n\ts_nop 0\n\t"
-                    "global_load_lds_dwordx4 %0, off\n\tglobal_load_lds_dwordx4 %0, off offset:1024" ::"v"(p),
-                    "s"(m0)
-                    : "memory", "m0");
-            else
-                asm volatile(
-                    "s_mov_b32 m0, %1\n\ts_nop 0\n\t"
-                    "global_load_lds_dwordx4 %0, off\n\tglobal_load_lds_dwordx4 %0, off offset:1024\n\t"
-                    "global_load_lds_dwordx4 %0, off offset:2048" ::"v"(p),
-                    "s"(m0)
-                    : "memory", "m0");
+            if (full == 1) HDX_DMA_EMIT(1);
+            else if (full == 2) HDX_DMA_EMIT(2);
+            else HDX_DMA_EMIT(3);
         } else {
-            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 0, 0);
-            if (full >= 2) __builtin_amdgcn_global_load_lds(p, at(m0), 16, 1024, 0);
-            if (full >= 3) __builtin_amdgcn_global_load_lds(p, at(m0), 16, 2048, 0);
+            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 0, POL);
+            if (full >= 2) __builtin_amdgcn_global_load_lds(p, at(m0), 16, 1024, POL);
+            if (full >= 3) __builtin_amdgcn_global_load_lds(p, at(m0), 16, 2048, POL);
         }
         p += 1024 * full;
         m0 += 1024 * full;
     }
     if (lane < (units & 63)) {
         if constexpr (ASM)
-            asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(p), "s"(m0)
-                         : "memory", "m0");
+            HDX_DMA_EMIT(1);
         else
-            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(p, at(m0), 16, 0, POL);
     }
 #endif
 }
+#undef HDX_DMA_EMIT
 
 // 16 bytes at a dword-aligned LDS address as one ds_read_b128 (gfx950 serves
 // dword-aligned b128 reads; the compiler emits them for 4-byte-aligned

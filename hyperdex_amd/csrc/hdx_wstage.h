@@ -94,7 +94,8 @@ struct Group {
 // ADMA: the DMA as inline asm (dma_x4_asm), the code table loaded with the
 // bases and lengths and waited for before the DMA goes out — nothing in
 // phases 2-3 then waits for the DMA.
-template <int NCH, uint32_t WB, int SHAPE, int ORDER = 1, bool ADMA = false, bool DL = false>
+// NT: the bases, lengths and span loaded non-temporal (read once).
+template <int NCH, uint32_t WB, int SHAPE, int ORDER = 1, bool ADMA = false, bool DL = false, bool NT = false>
 __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint64_t o0, uint8_t* win, uint32_t win_off,
                                                      uint64_t* desc) {
     const int lane = threadIdx.x & 63;
@@ -107,12 +108,13 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
     // ---- bases (lane nobj: the next group's first object) and lengths ------
     const bool has_next = o0 + K < args.n;
     const uint32_t nbase = g.nobj + (has_next ? 1u : 0u);
-    const uint64_t mybase = (uint32_t)lane < nbase ? args.obj_base[o0 + lane] : 0;
+    const uint64_t mybase =
+        (uint32_t)lane < nbase ? (NT ? __builtin_nontemporal_load(args.obj_base + o0 + lane) : args.obj_base[o0 + lane]) : 0;
     g.mybase = mybase;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
         const uint32_t s = (uint32_t)(c * 64 + lane);
-        g.L[c] = s < g.ns ? args.attr_len[g.q0 + s] : 0u;
+        g.L[c] = s < g.ns ? (NT ? __builtin_nontemporal_load(args.attr_len + g.q0 + s) : args.attr_len[g.q0 + s]) : 0u;
     }
     uint32_t packed_codes = 0;
     if constexpr (ADMA) {
@@ -127,7 +129,7 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
     // span write nothing: the window need not be whole KiB
     auto dma = [&](uint32_t units) {
         if constexpr (DL) dma_units16_loop<ADMA>(s16, win, units);
-        else dma_units16<ADMA>(s16, win, units);
+        else dma_units16<ADMA, NT>(s16, win, units);
     };
     // the span up to the next group's first object, before the lengths are back
     const bool early = has_next && bnext > b0 && lead + (bnext - b0) <= WB;
@@ -214,10 +216,11 @@ __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, 
 // GAP: the class straddling the pass boundary moves whole into the second
 // pass when pads allow (class_sort, hdx_regroup.h).  DL (debug): round 3's
 // span copy, addresses and predicate per KiB (dma_units16_loop).  WPB: waves
-// (each with its own window) per workgroup.
+// (each with its own window) per workgroup.  NT: the lengths, bases and span
+// loaded non-temporal (read once).
 template <int NCH, uint32_t WB, int SHAPE = 0, int HT = 0, int ORDER = 1, int W128 = 0, bool REGIONS = false,
           bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false, int WPB = 4, bool XS = false,
-          bool RD = false>
+          bool RD = false, bool NT = false>
 __global__ void __launch_bounds__(64 * WPB)
 hash_wstage_kernel(const BatchArgs args) {
     static_assert(NCH >= 1 && NCH <= 4 && WB % 16 == 0, "slot indices are 8 bits; windows whole DMA units");
@@ -236,7 +239,7 @@ hash_wstage_kernel(const BatchArgs args) {
 
     const uint64_t o0 = ((uint64_t)(XS ? xcd_block() : blockIdx.x) * WPB + w) * args.K;
     if (o0 >= args.n) return;  // no barrier anywhere: waves are independent
-    const Group<NCH> g = describe_group<NCH, WB, SHAPE, ORDER, ADMA, DL>(args, o0, win, 0, desc);
+    const Group<NCH> g = describe_group<NCH, WB, SHAPE, ORDER, ADMA, DL, NT>(args, o0, win, 0, desc);
 
     // ---- counting sort by work class (wave-local) --------------------------
     uint32_t pos[NCH];
@@ -313,7 +316,7 @@ hash_wstage_kernel(const BatchArgs args) {
 // independent waves per 256-thread workgroup, no workgroup barrier.
 template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, int HT = 0, int ORDER = 1, int W128 = 0,
           bool REGIONS = false, bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false, int WPB = 4,
-          bool XS = false, bool RD = false>
+          bool XS = false, bool RD = false, bool NT = false>
 static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     // lane o holds object o's base and lane K the next group's first: K <= 63
     args.K = std::min<uint32_t>(std::min<uint32_t>((uint32_t)(64 * NCH) / args.A, KCAP), 63u);
@@ -322,7 +325,7 @@ static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     const uint64_t blocks = (waves + WPB - 1) / WPB;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA, PU, DL, WPB, XS, RD>),
+    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA, PU, DL, WPB, XS, RD, NT>),
                        dim3((uint32_t)blocks), dim3(64 * WPB), 0, stream, args);
     return hipGetLastError();
 }

@@ -7,19 +7,23 @@
 // runs it for mixed string / int64 / float schemas (config 3b: 2.92 vs 3.32 ms
 // for variant 44, profiles/r3/ab_wstage_ht.jsonl).  The A/B forms are in
 // hdx_wstage_dbg.hip (debug library only).
+// Round 5: the bases, lengths and span loaded non-temporal (each byte is read
+// once): 2.556 / 2.561 / 2.554 vs 2.573 / 2.628 / 2.602 ms on three boxes
+// (variant 279 vs 270/212, profiles/r5/ab_nt_misaligned.jsonl,
+// ab_persistent_prefetch.jsonl).
 #include "hdx_wstage.h"
 
 namespace hdx {
 
 hipError_t launch_hash_wstage_product(const BatchArgs& args, hipStream_t stream) {
     if (args.n == 0) return hipSuccess;
-    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, false, true, true, true, false, 1, true>(args, stream);
+    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, false, true, true, true, false, 1, true, false, true>(args, stream);
 }
 
 // ... with the fused region lookup (args.T tables; args.coords may be NULL)
 hipError_t launch_hash_wstage_regions(const BatchArgs& args, hipStream_t stream) {
     if (args.n == 0) return hipSuccess;
-    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, true, true, true, true, false, 1, true>(args, stream);
+    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, true, true, true, true, false, 1, true, false, true>(args, stream);
 }
 
 }  // namespace hdx
