@@ -326,6 +326,7 @@ HDX_EXPORT hdx_status hdx_shutdown(void) {
         std::lock_guard<std::mutex> lk(g_scratch_mu);
         for (Scratch* s : g_scratch) s->release();
     }
+    trim_region_pools();
     if (had && dev >= 0) (void)hipSetDevice(dev);
     (void)hipGetLastError();
     return HDX_OK;

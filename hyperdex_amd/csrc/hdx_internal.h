@@ -122,8 +122,9 @@ hipError_t launch_lookup_region(const RegionArgs& a, hipStream_t stream);
 // Debug variant 235: by lookup at any n, 64 MiB chunks (tests); 247: the
 // same with the scratch allocation failing (the fallback).
 using RegionHashFn = std::function<hipError_t(uint64_t first, uint64_t count, uint64_t* coords)>;
-constexpr uint64_t kRegionChunkBytes = 1ull << 30;
+constexpr uint64_t kRegionChunkBytes = 2ull << 30;
 constexpr uint64_t kRegionLookupMinObjects = 1ull << 20;
+void trim_region_pools();  // hdx_regions.hip: release the regions scratch pools' cached memory
 bool regions_by_lookup_pays(uint64_t n);
 uint64_t regions_chunk_objects(uint64_t n, uint32_t A);
 hipError_t regions_by_lookup(uint64_t n, uint32_t A, const SweepTable* t, uint32_t T, uint64_t* coords,

@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 
 #include "hdx_internal.h"
 #include "hdx_region_lookup.h"
@@ -121,6 +122,42 @@ uint64_t regions_chunk_objects(uint64_t n, uint32_t A) {
     return std::min<uint64_t>(n, std::max<uint64_t>(1, bytes / (8ull * A)));
 }
 
+// The regions scratch comes from a memory pool of the library's own per
+// device that keeps up to one chunk cached between calls (the device's default
+// pool returns freed memory at every synchronisation, so each call would map
+// its chunk afresh); the pool is trimmed at hdx_shutdown.
+static std::mutex g_pool_mu;
+static hipMemPool_t g_pool[64];
+
+static hipError_t region_pool(hipStream_t stream, hipMemPool_t* out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (!g_pool[dev]) {
+        hipMemPoolProps props{};
+        props.allocType = hipMemAllocationTypePinned;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = dev;
+        if ((e = hipMemPoolCreate(&g_pool[dev], &props)) != hipSuccess) {
+            g_pool[dev] = nullptr;
+            return e;
+        }
+        uint64_t keep = kRegionChunkBytes;
+        (void)hipMemPoolSetAttribute(g_pool[dev], hipMemPoolAttrReleaseThreshold, &keep);
+    }
+    (void)stream;
+    *out = g_pool[dev];
+    return hipSuccess;
+}
+
+void trim_region_pools() {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (hipMemPool_t p : g_pool)
+        if (p) (void)hipMemPoolTrimTo(p, 0);
+}
+
 hipError_t regions_by_lookup(uint64_t n, uint32_t A, const SweepTable* t, uint32_t T, uint64_t* coords,
                              const RegionHashFn& hash, hipStream_t stream, bool* no_scratch) {
     *no_scratch = false;
@@ -129,7 +166,9 @@ hipError_t regions_by_lookup(uint64_t n, uint32_t A, const SweepTable* t, uint32
     uint64_t* scratch = nullptr;
     hipError_t e = hipSuccess;
     if (!coords) {
-        e = hipMallocAsync((void**)&scratch, chunk * A * 8, stream);
+        hipMemPool_t pool = nullptr;
+        e = region_pool(stream, &pool);
+        if (e == hipSuccess) e = hipMallocFromPoolAsync((void**)&scratch, chunk * A * 8, pool, stream);
 #if HDX_DEBUG_BUILD
         if (e == hipSuccess && hash_variant() == 247) {  // tests: the allocation "fails"
             (void)hipFreeAsync(scratch, stream);
