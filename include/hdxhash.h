@@ -321,8 +321,9 @@ hdx_status hdx_lookup_region_device(hdx_region_table table, const uint64_t* coor
  * Implementation note: below 2^20 objects this is one fused launch; from
  * 2^20 on, the hash and one lookup launch per table (faster there: the hash
  * kernels are VALU-bound), and with coords NULL the coordinates then pass
- * through device scratch of at most 4 GiB per call, allocated and freed
- * stream-ordered on `stream` (hipMallocAsync / hipFreeAsync). */
+ * through device scratch of at most 2 GiB per chunk, allocated and freed
+ * stream-ordered on `stream` from a memory pool the library keeps per device
+ * (one chunk cached between calls; hdx_shutdown trims it). */
 hdx_status hdx_hash_encoded_regions_device(const uint32_t* types, uint32_t attrs_sz,
                                            const uint8_t* keys, const uint64_t* key_off,
                                            const uint32_t* key_len, const uint8_t* vals,
