@@ -312,17 +312,22 @@ def run_rank(args):
                 types, (keys, key_off, key_len, vals, val_off, val_len), n, A, dev, stream, max_over_ranks,
                 result["roofline"]["kernel_ms"], result["regions"]["lookup_ms"])
 
+    # One-process extras (world 1): a failure is reported in the line, not fatal
+    # to it; the device-set runs (every visible device from one process) also
+    # under a watchdog that prints the line measured so far.
     if not args.no_host_path and rank == 0 and world == 1:
         if cfg == "cfg5":
-            result["host_path"] = time_host_sweep(types, (keys, key_off, key_len, vals, val_off, val_len), A,
-                                                  args.store_layout, coords)
+            guarded(result, "host_path", lambda: time_host_sweep(
+                types, (keys, key_off, key_len, vals, val_off, val_len), A, args.store_layout, coords),
+                watchdog_s=DEVICE_SET_WATCHDOG_S)
         else:
-            result["host_path"] = time_host_path(types, blob, base, lens, A)
+            guarded(result, "host_path", lambda: time_host_path(types, blob, base, lens, A),
+                    watchdog_s=DEVICE_SET_WATCHDOG_S)
 
     if rank == 0 and world == 1 and cfg == "cfg3a" and not args.no_secondary:
         # BASELINE's third config with its mixed attribute types, measured the
         # same way in the same run (the headline line stays config 3a's)
-        result["secondary"] = {"cfg3b": time_config("cfg3b", n, dev, stream)}
+        guarded(result, "secondary", lambda: {"cfg3b": time_config("cfg3b", n, dev, stream)})
 
     if args.config4_objects and cfg != "cfg5":
         result["config4"] = time_config4(args.config4_objects, world, rank, dev, stream, max_over_ranks,
@@ -331,21 +336,53 @@ def run_rank(args):
             # the same batch through the C-ABI device set: one process drives
             # every visible device (what a C++ daemon links), RCCL gather in-process
             torch.cuda.empty_cache()
-            result["config4_device_set"] = time_config4_device_set(args.config4_objects, dev, stream)
+            guarded(result, "config4_device_set",
+                    lambda: time_config4_device_set(args.config4_objects, dev, stream),
+                    watchdog_s=DEVICE_SET_WATCHDOG_S)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if cfg == "cfg5":
-            result["cpu_baseline"] = cpu_baseline_encoded(
-                types, (keys, key_off, key_len, vals, val_off, val_len), A, args.cpu_seconds, coords)
+            guarded(result, "cpu_baseline", lambda: cpu_baseline_encoded(
+                types, (keys, key_off, key_len, vals, val_off, val_len), A, args.cpu_seconds, coords))
         else:
-            result["cpu_baseline"] = cpu_baseline(types, blob, base, lens, A, args.cpu_seconds,
-                                                  coords)
-            result["cpu_per_object"] = cpu_per_object_suite(dev, stream, max(1.5, args.cpu_seconds / 3))
+            guarded(result, "cpu_baseline", lambda: cpu_baseline(types, blob, base, lens, A, args.cpu_seconds,
+                                                                 coords))
+            guarded(result, "cpu_per_object",
+                    lambda: cpu_per_object_suite(dev, stream, max(1.5, args.cpu_seconds / 3)))
 
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+# the device-set extras' watchdog: their first run on a node of distinct
+# devices must not cost the line (a hang prints what was measured, then exits)
+DEVICE_SET_WATCHDOG_S = 300
+
+
+def guarded(result, key, fn, watchdog_s=None):
+    """result[key] = fn(), or {"error": ...} when fn raises; with watchdog_s,
+    a fn still running after that many seconds has result printed as the
+    bench line (result[key] an error) and the process ended (world 1 only)."""
+    timer = None
+    if watchdog_s:
+        import threading
+
+        def fire():
+            result[key] = {"error": "no result after %d s (watchdog); the line ends here" % watchdog_s}
+            print(json.dumps(result), flush=True)
+            os._exit(0)
+        timer = threading.Timer(watchdog_s, fire)
+        timer.daemon = True
+        timer.start()
+    try:
+        result[key] = fn()
+    except Exception as e:  # an extra's failure is reported in the line
+        result[key] = {"error": "%s: %s" % (type(e).__name__, str(e)[:400])}
+    finally:
+        if timer is not None:
+            timer.cancel()
 
 
 def time_allgather(coords, world, dev, backend, max_over_ranks, reps=3):
@@ -426,7 +463,15 @@ def time_config4_device_set(n_total, dev0, stream, steps=3):
                 hdx.hash_batch_device_multi(types, shards, gather=gather, coords=outs)
             return (time.perf_counter() - t0) / steps * 1e3
         hash_ms = timed(False, own)
+        # the exchange's check: sampled rows of every shard as its own device
+        # hashed them, then found at the shard's place in every device's matrix
+        samples = []
+        for k, (f, c) in enumerate(ranges):
+            idx = torch.arange(0, c, max(1, c // 4099), device=own[k].device)
+            samples.append((f, idx.to(dev0), own[k][idx].to(dev0)))
         both_ms = timed(True, full)
+        exchange_ok = all(torch.equal(full[k][f + idx.to(full[k].device)].to(dev0), rows)
+                          for k in range(ndev) for f, idx, rows in samples)
     finally:
         hdx.shutdown()
     counts = [c for _, c in ranges]
@@ -438,6 +483,9 @@ def time_config4_device_set(n_total, dev0, stream, steps=3):
                                           (hash_ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
            "hash_and_gather_ms": round(both_ms, 3),
            "gather": "in-place ncclAllGather" if len(set(counts)) == 1 else "grouped in-place ncclBroadcast",
+           "exchange_verified": exchange_ok,
+           "exchange_check": "every shard's rows (about 4 k sampled per shard, as its own device hashed them) "
+                             "at the shard's place in every device's matrix after the exchange",
            "timing": "host clock around synchronous hdx_hash_batch_device_multi calls"}
     del shards, full, own
     torch.cuda.empty_cache()
