@@ -267,6 +267,39 @@ def test_gpu_batch_regions_by_lookup(oracle, case, with_coords):
 
 
 @pytest.mark.gpu
+def test_gpu_regions_scratch_pool_across_calls_and_shutdown(oracle):
+    """The regions scratch comes from the library's per-device memory pool
+    (hdx_regions.hip region_pool): chunks reused call after call from the
+    pool's cache, the cache trimmed by hdx_shutdown, and the next call after it
+    allocating afresh — the same region ids every time (debug variant 235:
+    three 64 MiB chunks per call)."""
+    import torch
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import RegionTable, _lib
+    dev = torch.device("cuda", 0)
+    n = 200_003
+    types, blob, base, lens = synth.make_batch_host(WIDE_MIXED, n, seed=78)
+    want_coords, _ = oracle.hash_batch(types, blob, base, lens)
+    specs = [([0],) + tuple(oracle.partition(1, 64)), ([1, 2, 99],) + tuple(oracle.partition(3, 64))]
+    ids_of = [np.arange(1, len(lo) + 1, dtype=np.uint64) * 3 for _, lo, _ in specs]
+    want = [oracle.lookup_region(at, lo, up, ids_of[k], want_coords) for k, (at, lo, up) in enumerate(specs)]
+    d = (torch.from_numpy(blob).to(dev), torch.from_numpy(base.view(np.int64)).to(dev),
+         torch.from_numpy(lens.view(np.int32)).to(dev))
+    with _lib.debug_library(235):
+        for step in range(4):
+            if step == 2:
+                hdx.shutdown()  # trims the pool; the next call allocates again
+            tables = [RegionTable(at, lo, up, ids_of[k]) for k, (at, lo, up) in enumerate(specs)]
+            ids = hdx.hash_batch_regions(types, *d, tables)
+            torch.cuda.synchronize()
+            for k in range(len(specs)):
+                assert np.array_equal(ids[k].cpu().numpy().view(np.uint64), want[k]), (step, k)
+            for t in tables:
+                t.close()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("form", list(range(100, 112)) + [217])
 def test_gpu_batch_regions_every_fused_form(oracle, form):
     """The debug library's fused forms (hdx_kernels_dbg.hip launch_fused_debug:
