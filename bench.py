@@ -365,24 +365,26 @@ def guarded(result, key, fn, watchdog_s=None):
     """result[key] = fn(), or {"error": ...} when fn raises; with watchdog_s,
     a fn still running after that many seconds has result printed as the
     bench line (result[key] an error) and the process ended (world 1 only)."""
+    import threading
+    lock = threading.Lock()  # the line is written by one thread: the watchdog's, or this one
     timer = None
     if watchdog_s:
-        import threading
-
         def fire():
-            result[key] = {"error": "no result after %d s (watchdog); the line ends here" % watchdog_s}
-            print(json.dumps(result), flush=True)
-            os._exit(0)
+            with lock:
+                result[key] = {"error": "no result after %d s (watchdog); the line ends here" % watchdog_s}
+                print(json.dumps(result), flush=True)
+                os._exit(0)
         timer = threading.Timer(watchdog_s, fire)
         timer.daemon = True
         timer.start()
     try:
-        result[key] = fn()
+        value = fn()
     except Exception as e:  # an extra's failure is reported in the line
-        result[key] = {"error": "%s: %s" % (type(e).__name__, str(e)[:400])}
-    finally:
-        if timer is not None:
-            timer.cancel()
+        value = {"error": "%s: %s" % (type(e).__name__, str(e)[:400])}
+    if timer is not None:
+        timer.cancel()
+    with lock:
+        result[key] = value
 
 
 def time_allgather(coords, world, dev, backend, max_over_ranks, reps=3):
