@@ -129,7 +129,7 @@ uint64_t regions_chunk_objects(uint64_t n, uint32_t A) {
 static std::mutex g_pool_mu;
 static hipMemPool_t g_pool[64];
 
-static hipError_t region_pool(hipMemPool_t* out) {
+static hipError_t region_pool(hipStream_t stream, hipMemPool_t* out) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
@@ -147,6 +147,7 @@ static hipError_t region_pool(hipMemPool_t* out) {
         uint64_t keep = kRegionChunkBytes;
         (void)hipMemPoolSetAttribute(g_pool[dev], hipMemPoolAttrReleaseThreshold, &keep);
     }
+    (void)stream;
     *out = g_pool[dev];
     return hipSuccess;
 }
@@ -166,7 +167,7 @@ hipError_t regions_by_lookup(uint64_t n, uint32_t A, const SweepTable* t, uint32
     hipError_t e = hipSuccess;
     if (!coords) {
         hipMemPool_t pool = nullptr;
-        e = region_pool(&pool);
+        e = region_pool(stream, &pool);
         if (e == hipSuccess) e = hipMallocFromPoolAsync((void**)&scratch, chunk * A * 8, pool, stream);
 #if HDX_DEBUG_BUILD
         if (e == hipSuccess && hash_variant() == 247) {  // tests: the allocation "fails"
