@@ -3,7 +3,7 @@
 # non-temporal bit, alternated twice on one box (run under gpurun); the lines
 # land in gpurun_out/s2v/.
 cd ${GRAFT_REPO_ROOT:-.}
-O=gpurun_out/s2v
+O=gpurun_out/${AB_TAG:-s2v}
 mkdir -p $O
 for r in 1 2; do
   timeout -k 10 300 python -u bench.py --cpu-seconds 2 > $O/nt_$r.log 2> $O/nt_$r.err || exit $?
