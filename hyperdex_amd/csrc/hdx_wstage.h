@@ -220,9 +220,12 @@ __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, 
 // loaded non-temporal (read once).
 template <int NCH, uint32_t WB, int SHAPE = 0, int HT = 0, int ORDER = 1, int W128 = 0, bool REGIONS = false,
           bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false, int WPB = 4, bool XS = false,
-          bool RD = false, bool NT = false>
+          bool RD = false, bool NT = false, int PRIO = 0>
 __global__ void __launch_bounds__(64 * WPB)
 hash_wstage_kernel(const BatchArgs args) {
+    // PRIO (A/B): 1 = the load phase at high wave priority, the passes at low;
+    // 2 = the reverse
+    if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(3);
     static_assert(NCH >= 1 && NCH <= 4 && WB % 16 == 0, "slot indices are 8 bits; windows whole DMA units");
     static_assert(!(RD && REGIONS), "the fused lookups read the coordinates parked in desc");
     constexpr uint32_t FRONT = HT ? kFrontHT : 0;
@@ -246,6 +249,8 @@ hash_wstage_kernel(const BatchArgs args) {
     class_sort<NCH, GAP>(cnt, perm, g.cls, g.code, g.ns, wave_lds_fence, RD ? pos : nullptr);
     // every LDS-DMA of this wave must have landed before the window is read
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(3);
 
     if constexpr (RD) {
         // RD: descriptors and coordinates stay in registers.  Pass t's lane
@@ -316,7 +321,7 @@ hash_wstage_kernel(const BatchArgs args) {
 // independent waves per 256-thread workgroup, no workgroup barrier.
 template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, int HT = 0, int ORDER = 1, int W128 = 0,
           bool REGIONS = false, bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false, int WPB = 4,
-          bool XS = false, bool RD = false, bool NT = false>
+          bool XS = false, bool RD = false, bool NT = false, int PRIO = 0>
 static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     // lane o holds object o's base and lane K the next group's first: K <= 63
     args.K = std::min<uint32_t>(std::min<uint32_t>((uint32_t)(64 * NCH) / args.A, KCAP), 63u);
@@ -325,7 +330,7 @@ static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     const uint64_t blocks = (waves + WPB - 1) / WPB;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA, PU, DL, WPB, XS, RD, NT>),
+    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA, PU, DL, WPB, XS, RD, NT, PRIO>),
                        dim3((uint32_t)blocks), dim3(64 * WPB), 0, stream, args);
     return hipGetLastError();
 }

@@ -171,6 +171,8 @@ hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int for
         case 74: return launch_wstage_t<3, 13312, 10, 0, 5, 4, 0, false, true, true, true, false, 1, true>(args, stream);  // 3 passes, 10 objects, 13 KiB
         case 79: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true>(args, stream);  // the product (round 5: 70 with non-temporal loads)
         case 78: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 1, false, true, true, true, false, 1, true, false, true>(args, stream);  // the product with dword-aligned ds_read_b128 window reads
+        case 87: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 1>(args, stream);  // the product, loads at high wave priority
+        case 88: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 2>(args, stream);  // the product, passes at high wave priority
         // the slots class-sorted over the workgroup
         case 10: return launch_wgstage_t<2, 8832>(args, stream);
         case 11: return launch_wgstage_t<1, 4352>(args, stream);

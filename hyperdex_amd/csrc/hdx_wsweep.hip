@@ -153,9 +153,10 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
 // form 22, correct coordinates): the walk's reads as round 3's dword pairs.
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
           bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true, bool DL = false,
-          int WPB = 4, bool XS = false>
+          int WPB = 4, bool XS = false, int PRIO = 0>
 __global__ void __launch_bounds__(64 * WPB)
 hash_sweep_wstage_kernel(const EncodedArgs a) {
+    if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(3);
     constexpr uint32_t SL = NCH * 64;
     __shared__ __attribute__((aligned(16))) uint8_t win_all[WPB][kFrontS + WB + kBackS];
     __shared__ uint64_t desc_all[WPB][SL];   // {offset, length | kGlobal}; then the parked coordinate
@@ -281,6 +282,8 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         if (vheld && SHAPE != 3) copy_span<ASM, DL>(a.vals + v0 - vlead, win + kFrontS + kreg, vheld, lane);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the compiler does not order ds_read after LDS DMA
+    if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(3);
     wave_fence();
 
     // ---- decode_value (datalayer_encodings.cc:168-217), lane = object --------
@@ -422,14 +425,14 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
 
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
           bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true, bool DL = false,
-          int WPB = 4, bool XS = false>
+          int WPB = 4, bool XS = false, int PRIO = 0>
 static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
     const uint32_t K = std::min<uint32_t>(64 * NCH / a.A, KCAP);
     if (K == 0) return hipErrorInvalidValue;
     const uint64_t waves = (a.n + K - 1) / K;
     const uint64_t blocks = (waves + WPB - 1) / WPB;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU, BF, RECS, KUNITS, DL, WPB, XS>),
+    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU, BF, RECS, KUNITS, DL, WPB, XS, PRIO>),
                        dim3((uint32_t)blocks), dim3(64 * WPB), 0, stream, a);
     return hipGetLastError();
 }
@@ -447,15 +450,20 @@ static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
 // wave in 9.5 KiB windows (the per-wave skeleton over one more object:
 // 3.301 vs 3.415 ms for 6 in 8.5 KiB; 9 KiB windows 3.343 — a group of 7
 // then overflows the window more often; profiles/r5/ab_sweep_k7.jsonl).
+// Round 5: the load phase (offsets, lengths, the span DMA) at high wave
+// priority, the walk and the passes at low (s_setprio): a wave that has just
+// started gets its loads out ahead of the waves that are hashing — 3.345 vs
+// 3.369 ms per 10 M on the key column, 3.578 vs 3.619 keys in place, 3.296 vs
+// 3.338 records (profiles/r5/ab_priority.jsonl).
 hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
     const bool recs = a.keys == a.vals;
     if (a.T)
-        return recs ? launch_wsweep_t<2, 9728, 7, true, true, 0, 13, false, true, true, true, true, false, 1, true>(a, stream)
-                    : launch_wsweep_t<2, 9728, 7, true, true, 0, 13, false, true, true, false, true, false, 1, true>(a, stream);
+        return recs ? launch_wsweep_t<2, 9728, 7, true, true, 0, 13, false, true, true, true, true, false, 1, true, 1>(a, stream)
+                    : launch_wsweep_t<2, 9728, 7, true, true, 0, 13, false, true, true, false, true, false, 1, true, 1>(a, stream);
     if (!a.coords) return hipErrorInvalidValue;
-    return recs ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true>(a, stream)
-                : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true>(a, stream);
+    return recs ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 1>(a, stream)
+                : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 1>(a, stream);
 }
 
 #ifndef HDX_DEBUG_BUILD
@@ -510,6 +518,15 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 30: return a.keys == a.vals  // 3 passes, 11 objects per wave in 14 KiB windows
                         ? launch_wsweep_t<3, 14336, 11, false, true, 0, 13, false, true, true, true, true, false, 1, true>(a, stream)
                         : launch_wsweep_t<3, 14336, 11, false, true, 0, 13, false, true, true, false, true, false, 1, true>(a, stream);
+        case 31: case 32: {  // 31: the product without wave priorities (round 5 before), 32: passes high, loads low
+            if (form == 31)
+                return a.keys == a.vals
+                           ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 0>(a, stream)
+                           : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 0>(a, stream);
+            return a.keys == a.vals
+                       ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 2>(a, stream)
+                       : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 2>(a, stream);
+        }
         case 26: return a.keys == a.vals  // round 4's product: four waves per workgroup
                         ? launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, true, true, false, 4>(a, stream)
                         : launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, true, false, 4>(a, stream);
