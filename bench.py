@@ -1130,7 +1130,10 @@ def host_info(threads, quota):
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
-def pinned_passes(work, seconds, passes=3):
+CPU_PASSES = 5  # the baseline's passes: a pass disturbed by the box's other tenants stays out of the median
+
+
+def pinned_passes(work, seconds, passes=CPU_PASSES):
     """Times `work` (one (prepare, run, nbytes, nobj) per thread) on threads
     pinned one per CPU of this process's affinity set.  Each thread first
     touches its own copy of its chunk (prepare(), on that thread: its pages
@@ -1200,7 +1203,7 @@ def cpu_baseline(types, blob, base, lens, A, seconds, coords):
     """The oracle (C restatement of common/hash.cc, -O2) on this host's cores,
     on a bounded sample of the same batch: one pinned thread per core, each
     over its own first-touched copy of a contiguous chunk (pinned_passes),
-    median of 3 passes.  Also verifies the sample's GPU coordinates against
+    median of 5 passes.  Also verifies the sample's GPU coordinates against
     it (a failed check aborts the bench)."""
     from oracle import oracle
     threads, quota = cpu_threads()
@@ -1233,7 +1236,7 @@ def cpu_baseline(types, blob, base, lens, A, seconds, coords):
             "passes_GiB_s": [round(r[0] / 2**30, 3) for r in rates],
             "single_thread_GiB_s": round(ob / 2**30, 3),
             "sample": "%d objects (%.0f MB) of the same batch, oracle/hdx_oracle.c -O2, one pinned thread per core "
-                      "over its own first-touched copy of a contiguous chunk, median of 3 passes (%d chunk passes); "
+                      "over its own first-touched copy of a contiguous chunk, median of 5 passes (%d chunk passes); "
                       "verified equal to the GPU coords" % (ns, nb / 1e6, reps),
             **host_info(len(work), quota)}
 
@@ -1356,7 +1359,7 @@ def cpu_baseline_encoded(types, enc, A, seconds, coords):
     """Config 5 CPU baseline: the oracle's decode_value + hash, one pinned
     thread per core as cpu_baseline, each over its own first-touched compact
     copy (keys back to back, values back to back) of a 20 k-object chunk, so
-    every store layout times the same work; median of 3 passes.  The
+    every store layout times the same work; median of 5 passes.  The
     sample's GPU coordinates, and those of objects spread over the whole
     store, are checked against the oracle first."""
     from oracle import oracle
@@ -1402,7 +1405,7 @@ def cpu_baseline_encoded(types, enc, A, seconds, coords):
             "passes_GiB_s": [round(r[0] / 2**30, 3) for r in rates],
             "sample": "%d stored objects (%.0f MB), oracle hdxo_hash_encoded -O2, one pinned thread per core over its "
                       "own first-touched compact copy (keys and values back to back, whatever the store's layout) "
-                      "of a contiguous chunk, median of 3 passes (%d chunk passes); verified equal to the GPU coords, "
+                      "of a contiguous chunk, median of 5 passes (%d chunk passes); verified equal to the GPU coords, "
                       "and %d objects spread over the whole store (the last 64 and random ones)"
                       % (ns, nbytes / 1e6, reps, spread),
             **host_info(len(work), quota)}
