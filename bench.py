@@ -321,7 +321,7 @@ def run_rank(args):
                 types, (keys, key_off, key_len, vals, val_off, val_len), A, args.store_layout, coords),
                 watchdog_s=DEVICE_SET_WATCHDOG_S)
         else:
-            guarded(result, "host_path", lambda: time_host_path(types, blob, base, lens, A),
+            guarded(result, "host_path", lambda: time_host_path(types, blob, base, lens, A, coords),
                     watchdog_s=DEVICE_SET_WATCHDOG_S)
 
     if rank == 0 and world == 1 and cfg == "cfg3a" and not args.no_secondary:
@@ -997,11 +997,12 @@ def measured_traffic(path, cfg, n):
     return int(per_obj * n), "%s (rocprofv3 PMC, digest %s)" % (os.path.relpath(path, ROOT), source_digest())
 
 
-def time_host_path(types, blob, base, lens, A, n_host=2_000_000):
+def time_host_path(types, blob, base, lens, A, coords=None, n_host=2_000_000):
     """PCIe-inclusive rate: pinned host batch -> hdx_hash_batch_host -> pinned coords,
     over the device set of every visible device (hdx_init_mask: the library
     splits the batch byte-balanced over the devices, one worker pipeline each;
-    n_host objects per device, at most the resident batch)."""
+    n_host objects per device, at most the resident batch).  With `coords`
+    (the device-resident run's), the host path's rows are checked equal."""
     import ctypes
 
     import hyperdex_amd as hdx
@@ -1029,13 +1030,21 @@ def time_host_path(types, blob, base, lens, A, n_host=2_000_000):
         hdx._lib.check(lib.hdx_hash_batch_host(t.ctypes.data, A, ptrs["blob"], nb, ptrs["base"],
                                                ptrs["lens"], n, ptrs["out"]))
     dt = (time.perf_counter() - t0) / reps
+    verified = None
+    if coords is not None and n:
+        got = np.ctypeslib.as_array((ctypes.c_uint64 * (n * A)).from_address(ptrs["out"]))
+        verified = bool(np.array_equal(got, coords[:n].reshape(-1).cpu().numpy().view(np.uint64)))
+        del got
     for p in ptrs.values():
         lib.hdx_free_pinned(p)
     hdx.shutdown()  # the set's workers and staging; later phases run on the caller's device
-    return {"objects": n, "devices": len(devices), "ms": round(dt * 1e3, 3),
-            "GiB_s": round(nb / dt / 2**30, 3), "GiB_s_per_device": round(nb / dt / 2**30 / len(devices), 3),
-            "mobjects_per_s": round(n / dt / 1e6, 2),
-            "path": "hdx_init_mask(all visible devices) + hdx_hash_batch_host: pinned H2D, kernel, D2H"}
+    res = {"objects": n, "devices": len(devices), "ms": round(dt * 1e3, 3),
+           "GiB_s": round(nb / dt / 2**30, 3), "GiB_s_per_device": round(nb / dt / 2**30 / len(devices), 3),
+           "mobjects_per_s": round(n / dt / 1e6, 2),
+           "path": "hdx_init_mask(all visible devices) + hdx_hash_batch_host: pinned H2D, kernel, D2H"}
+    if verified is not None:
+        res["verified_vs_device_coords"] = verified
+    return res
 
 
 def time_host_sweep(types, enc, A, layout, coords, n_host=1_000_000):
