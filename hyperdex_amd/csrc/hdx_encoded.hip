@@ -479,6 +479,11 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
             if (e != hipErrorInvalidValue) return e;
             break;
         }
+        case 289: {  // the product sweep with its stores at high priority too
+            const hipError_t e = launch_hash_wsweep(a, stream, 33);
+            if (e != hipErrorInvalidValue) return e;
+            break;
+        }
         case 277: case 278: {  // the product sweep without wave priorities (277), with the passes high (278)
             const hipError_t e = launch_hash_wsweep(a, stream, hash_variant() == 277 ? 31 : 32);
             if (e != hipErrorInvalidValue) return e;

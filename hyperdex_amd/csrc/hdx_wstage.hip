@@ -10,20 +10,24 @@
 // Round 5: the bases, lengths and span loaded non-temporal (each byte is read
 // once): 2.556 / 2.561 / 2.554 vs 2.573 / 2.628 / 2.602 ms on three boxes
 // (variant 279 vs 270/212, profiles/r5/ab_nt_misaligned.jsonl,
-// ab_persistent_prefetch.jsonl).
+// ab_persistent_prefetch.jsonl); and the load phase at high wave priority, the
+// passes at low (s_setprio, PRIO 1): a wave that has just started gets its
+// loads and span DMA out ahead of the waves that are hashing — 2.500 vs 2.555
+// ms on a fast box, 2.711–2.729 vs 2.716–2.746 on a slow one (variant 287 vs
+// 279, profiles/r5/ab_priority.jsonl).
 #include "hdx_wstage.h"
 
 namespace hdx {
 
 hipError_t launch_hash_wstage_product(const BatchArgs& args, hipStream_t stream) {
     if (args.n == 0) return hipSuccess;
-    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, false, true, true, true, false, 1, true, false, true>(args, stream);
+    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, false, true, true, true, false, 1, true, false, true, 1>(args, stream);
 }
 
 // ... with the fused region lookup (args.T tables; args.coords may be NULL)
 hipError_t launch_hash_wstage_regions(const BatchArgs& args, hipStream_t stream) {
     if (args.n == 0) return hipSuccess;
-    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, true, true, true, true, false, 1, true, false, true>(args, stream);
+    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, true, true, true, true, false, 1, true, false, true, 1>(args, stream);
 }
 
 }  // namespace hdx

@@ -169,10 +169,13 @@ hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int for
         case 75: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, true>(args, stream);  // descriptors in registers (17 waves per CU)
         case 76: return launch_wstage_t<2, 8704, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, true>(args, stream);  // ... with 8.5 KiB windows (18 waves per CU)
         case 74: return launch_wstage_t<3, 13312, 10, 0, 5, 4, 0, false, true, true, true, false, 1, true>(args, stream);  // 3 passes, 10 objects, 13 KiB
-        case 79: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true>(args, stream);  // the product (round 5: 70 with non-temporal loads)
+        case 79: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true>(args, stream);  // 70 with non-temporal loads (the product before its wave priorities)
         case 78: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 1, false, true, true, true, false, 1, true, false, true>(args, stream);  // the product with dword-aligned ds_read_b128 window reads
-        case 87: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 1>(args, stream);  // the product, loads at high wave priority
+        case 87: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 1>(args, stream);  // the product: 79 with the loads at high wave priority
         case 88: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 2>(args, stream);  // the product, passes at high wave priority
+        case 89: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 3>(args, stream);  // the product, loads and stores at high wave priority
+        case 90: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 4>(args, stream);  // the product, stores alone at high wave priority
+        case 91: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 5>(args, stream);  // loads and stores at the top priority
         // the slots class-sorted over the workgroup
         case 10: return launch_wgstage_t<2, 8832>(args, stream);
         case 11: return launch_wgstage_t<1, 4352>(args, stream);

@@ -156,7 +156,7 @@ template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = 
           int WPB = 4, bool XS = false, int PRIO = 0>
 __global__ void __launch_bounds__(64 * WPB)
 hash_sweep_wstage_kernel(const EncodedArgs a) {
-    if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(3);
+    if constexpr (PRIO == 1 || PRIO == 3) __builtin_amdgcn_s_setprio(3);
     constexpr uint32_t SL = NCH * 64;
     __shared__ __attribute__((aligned(16))) uint8_t win_all[WPB][kFrontS + WB + kBackS];
     __shared__ uint64_t desc_all[WPB][SL];   // {offset, length | kGlobal}; then the parked coordinate
@@ -282,7 +282,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         if (vheld && SHAPE != 3) copy_span<ASM, DL>(a.vals + v0 - vlead, win + kFrontS + kreg, vheld, lane);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the compiler does not order ds_read after LDS DMA
-    if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO == 1 || PRIO == 3) __builtin_amdgcn_s_setprio(0);
     if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(3);
     wave_fence();
 
@@ -409,6 +409,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         desc[s] = h;
     }
     wave_fence();
+    if constexpr (PRIO == 3) __builtin_amdgcn_s_setprio(2);  // the stores (and the wave's end) ahead of the hashing waves
     if (!REGIONS || a.coords) {
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
@@ -518,6 +519,9 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 30: return a.keys == a.vals  // 3 passes, 11 objects per wave in 14 KiB windows
                         ? launch_wsweep_t<3, 14336, 11, false, true, 0, 13, false, true, true, true, true, false, 1, true>(a, stream)
                         : launch_wsweep_t<3, 14336, 11, false, true, 0, 13, false, true, true, false, true, false, 1, true>(a, stream);
+        case 33: return a.keys == a.vals  // the product with its stores at high priority too (PRIO 3)
+                        ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 3>(a, stream)
+                        : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 3>(a, stream);
         case 31: case 32: {  // 31: the product without wave priorities (round 5 before), 32: passes high, loads low
             if (form == 31)
                 return a.keys == a.vals
