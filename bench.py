@@ -43,7 +43,7 @@ def sweep_kernel_name(layout):
     rocprofv3 names it: the record instantiation when keys and values are one
     store (layout "records"), else the other one."""
     return ("void hdx::hash_sweep_wstage_kernel<2, 9728u, 7u, false, true, 0, 13, false, true, true, %s, true, "
-            "false, 1, true, 1>(hdx::EncodedArgs)" % ("true" if layout == "records" else "false"))
+            "false, 1, true, 4>(hdx::EncodedArgs)" % ("true" if layout == "records" else "false"))
 
 
 def log(*a):

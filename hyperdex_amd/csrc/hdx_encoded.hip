@@ -479,8 +479,10 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
             if (e != hipErrorInvalidValue) return e;
             break;
         }
-        case 289: {  // the product sweep with its stores at high priority too
-            const hipError_t e = launch_hash_wsweep(a, stream, 33);
+        case 289: case 290: case 291: {  // the product sweep's priority forms: loads and stores high (289), loads
+            // high alone (290, the product before the walk's medium priority), the walk high (291)
+            const int v = hash_variant();
+            const hipError_t e = launch_hash_wsweep(a, stream, v == 289 ? 33 : v == 290 ? 34 : 35);
             if (e != hipErrorInvalidValue) return e;
             break;
         }

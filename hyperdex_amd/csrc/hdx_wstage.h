@@ -226,7 +226,7 @@ hash_wstage_kernel(const BatchArgs args) {
     // PRIO (A/B): 1 = the load phase at high wave priority, the passes at low;
     // 2 = the reverse
     // 3 = 1 with the stores at high priority again; 4 = the stores alone high; 5 = 3 at the top level
-    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 5) __builtin_amdgcn_s_setprio(3);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 5 || PRIO == 6) __builtin_amdgcn_s_setprio(3);
     static_assert(NCH >= 1 && NCH <= 4 && WB % 16 == 0, "slot indices are 8 bits; windows whole DMA units");
     static_assert(!(RD && REGIONS), "the fused lookups read the coordinates parked in desc");
     constexpr uint32_t FRONT = HT ? kFrontHT : 0;
@@ -247,10 +247,11 @@ hash_wstage_kernel(const BatchArgs args) {
 
     // ---- counting sort by work class (wave-local) --------------------------
     uint32_t pos[NCH];
+    if constexpr (PRIO == 6) __builtin_amdgcn_s_setprio(2);  // 6: the sort at medium priority
     class_sort<NCH, GAP>(cnt, perm, g.cls, g.code, g.ns, wave_lds_fence, RD ? pos : nullptr);
     // every LDS-DMA of this wave must have landed before the window is read
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 5) __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 5 || PRIO == 6) __builtin_amdgcn_s_setprio(0);
     if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(3);
 
     if constexpr (RD) {

@@ -176,6 +176,7 @@ hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int for
         case 89: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 3>(args, stream);  // the product, loads and stores at high wave priority
         case 90: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 4>(args, stream);  // the product, stores alone at high wave priority
         case 91: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 5>(args, stream);  // loads and stores at the top priority
+        case 92: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 6>(args, stream);  // loads high, the sort medium, the passes low
         // the slots class-sorted over the workgroup
         case 10: return launch_wgstage_t<2, 8832>(args, stream);
         case 11: return launch_wgstage_t<1, 4352>(args, stream);

@@ -156,7 +156,7 @@ template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = 
           int WPB = 4, bool XS = false, int PRIO = 0>
 __global__ void __launch_bounds__(64 * WPB)
 hash_sweep_wstage_kernel(const EncodedArgs a) {
-    if constexpr (PRIO == 1 || PRIO == 3) __builtin_amdgcn_s_setprio(3);
+    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4 || PRIO == 5) __builtin_amdgcn_s_setprio(3);
     constexpr uint32_t SL = NCH * 64;
     __shared__ __attribute__((aligned(16))) uint8_t win_all[WPB][kFrontS + WB + kBackS];
     __shared__ uint64_t desc_all[WPB][SL];   // {offset, length | kGlobal}; then the parked coordinate
@@ -284,6 +284,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the compiler does not order ds_read after LDS DMA
     if constexpr (PRIO == 1 || PRIO == 3) __builtin_amdgcn_s_setprio(0);
     if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(3);
+    if constexpr (PRIO == 4) __builtin_amdgcn_s_setprio(2);  // 4: the walk and sort at medium priority, the passes low
     wave_fence();
 
     // ---- decode_value (datalayer_encodings.cc:168-217), lane = object --------
@@ -380,6 +381,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         }
     }
     class_sort<NCH, GAP>(cnt, perm, cls, cd, ns, wave_fence);
+    if constexpr (PRIO == 4 || PRIO == 5) __builtin_amdgcn_s_setprio(0);  // 5: the walk and sort stay high
 
     // ---- NCH class-sorted passes, coordinates parked over their descriptors ---
     // (PU 0: the loop not unrolled, one copy of the hash code instead of NCH)
@@ -451,20 +453,23 @@ static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
 // wave in 9.5 KiB windows (the per-wave skeleton over one more object:
 // 3.301 vs 3.415 ms for 6 in 8.5 KiB; 9 KiB windows 3.343 — a group of 7
 // then overflows the window more often; profiles/r5/ab_sweep_k7.jsonl).
-// Round 5: the load phase (offsets, lengths, the span DMA) at high wave
-// priority, the walk and the passes at low (s_setprio): a wave that has just
-// started gets its loads out ahead of the waves that are hashing — 3.345 vs
-// 3.369 ms per 10 M on the key column, 3.578 vs 3.619 keys in place, 3.296 vs
-// 3.338 records (profiles/r5/ab_priority.jsonl).
+// Round 5: wave priorities (s_setprio, PRIO 4): the load phase (offsets,
+// lengths, the span DMA) high, the walk and the class sort — chains of
+// dependent LDS reads and atomics — medium, the passes low: a wave that has
+// just started gets its loads out, and a walking wave its next read, ahead of
+// the waves that are hashing.  3.198 vs 3.274 ms per 10 M on the key column,
+// 3.357 vs 3.424 keys in place, 3.146 vs 3.213 records; the walk at high
+// priority 3.211 / 3.369 / 3.155; loads high alone −0.3 to −1.2 %
+// (profiles/r5/ab_priority.jsonl).
 hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
     const bool recs = a.keys == a.vals;
     if (a.T)
-        return recs ? launch_wsweep_t<2, 9728, 7, true, true, 0, 13, false, true, true, true, true, false, 1, true, 1>(a, stream)
-                    : launch_wsweep_t<2, 9728, 7, true, true, 0, 13, false, true, true, false, true, false, 1, true, 1>(a, stream);
+        return recs ? launch_wsweep_t<2, 9728, 7, true, true, 0, 13, false, true, true, true, true, false, 1, true, 4>(a, stream)
+                    : launch_wsweep_t<2, 9728, 7, true, true, 0, 13, false, true, true, false, true, false, 1, true, 4>(a, stream);
     if (!a.coords) return hipErrorInvalidValue;
-    return recs ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 1>(a, stream)
-                : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 1>(a, stream);
+    return recs ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 4>(a, stream)
+                : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 4>(a, stream);
 }
 
 #ifndef HDX_DEBUG_BUILD
@@ -519,6 +524,12 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 30: return a.keys == a.vals  // 3 passes, 11 objects per wave in 14 KiB windows
                         ? launch_wsweep_t<3, 14336, 11, false, true, 0, 13, false, true, true, true, true, false, 1, true>(a, stream)
                         : launch_wsweep_t<3, 14336, 11, false, true, 0, 13, false, true, true, false, true, false, 1, true>(a, stream);
+        case 34: return a.keys == a.vals  // loads high, the walk and passes low (PRIO 1, the product before PRIO 4)
+                        ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 1>(a, stream)
+                        : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 1>(a, stream);
+        case 35: return a.keys == a.vals  // loads, the walk and sort high, the passes low (PRIO 5)
+                        ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 5>(a, stream)
+                        : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 5>(a, stream);
         case 33: return a.keys == a.vals  // the product with its stores at high priority too (PRIO 3)
                         ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 3>(a, stream)
                         : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 3>(a, stream);
