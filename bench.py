@@ -319,10 +319,10 @@ def run_rank(args):
         if cfg == "cfg5":
             guarded(result, "host_path", lambda: time_host_sweep(
                 types, (keys, key_off, key_len, vals, val_off, val_len), A, args.store_layout, coords),
-                watchdog_s=DEVICE_SET_WATCHDOG_S)
+                watchdog_s=DEVICE_SET_WATCHDOG_S, fatal=True)
         else:
             guarded(result, "host_path", lambda: time_host_path(types, blob, base, lens, A, coords),
-                    watchdog_s=DEVICE_SET_WATCHDOG_S)
+                    watchdog_s=DEVICE_SET_WATCHDOG_S, fatal=True)
 
     if rank == 0 and world == 1 and cfg == "cfg3a" and not args.no_secondary:
         # BASELINE's third config with its mixed attribute types, measured the
@@ -338,7 +338,7 @@ def run_rank(args):
             torch.cuda.empty_cache()
             guarded(result, "config4_device_set",
                     lambda: time_config4_device_set(args.config4_objects, dev, stream),
-                    watchdog_s=DEVICE_SET_WATCHDOG_S)
+                    watchdog_s=DEVICE_SET_WATCHDOG_S, fatal=True)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if cfg == "cfg5":
@@ -354,6 +354,10 @@ def run_rank(args):
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if FAILED_EXTRAS:
+        log("bench.py: device-set extras failed: %s (reported in the line)" % FAILED_EXTRAS)
+        return 1
+    return 0
 
 
 # the device-set extras' watchdog: their first run on a node of distinct
@@ -361,19 +365,31 @@ def run_rank(args):
 DEVICE_SET_WATCHDOG_S = 300
 
 
-def guarded(result, key, fn, watchdog_s=None):
-    """result[key] = fn(), or {"error": ...} when fn raises; with watchdog_s,
+WATCHDOG_EXIT = 3     # the process exit status after the watchdog printed the line
+FAILED_EXTRAS = []    # keys of fatal extras that failed: main() exits non-zero after the line
+
+
+def guarded(result, key, fn, watchdog_s=None, fatal=False):
+    """result[key] = fn(), or {"error": ...} when fn raises.  With watchdog_s,
     a fn still running after that many seconds has result printed as the
-    bench line (result[key] an error) and the process ended (world 1 only)."""
+    bench line (result[key] an error) and the process ended with status
+    WATCHDOG_EXIT (world 1 only): a process that has touched the GPU and
+    hung must not look like a success.  With fatal, a failure is still
+    reported in the line, and the process exits non-zero after printing it
+    (main() reads FAILED_EXTRAS)."""
     import threading
     lock = threading.Lock()  # the line is written by one thread: the watchdog's, or this one
+    state = {"done": False}
     timer = None
     if watchdog_s:
         def fire():
             with lock:
+                if state["done"]:  # fn returned as the timer fired: its result stands
+                    return
                 result[key] = {"error": "no result after %d s (watchdog); the line ends here" % watchdog_s}
                 print(json.dumps(result), flush=True)
-                os._exit(0)
+                sys.stderr.flush()
+                os._exit(WATCHDOG_EXIT)
         timer = threading.Timer(watchdog_s, fire)
         timer.daemon = True
         timer.start()
@@ -381,10 +397,13 @@ def guarded(result, key, fn, watchdog_s=None):
         value = fn()
     except Exception as e:  # an extra's failure is reported in the line
         value = {"error": "%s: %s" % (type(e).__name__, str(e)[:400])}
+    with lock:
+        state["done"] = True
+        result[key] = value
     if timer is not None:
         timer.cancel()
-    with lock:
-        result[key] = value
+    if fatal and isinstance(value, dict) and "error" in value:
+        FAILED_EXTRAS.append(key)
 
 
 def time_allgather(coords, world, dev, backend, max_over_ranks, reps=3):
@@ -693,6 +712,7 @@ def rehearse_cpu(args):
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 def key_subspace_tables(A):
@@ -1421,4 +1441,4 @@ def cpu_baseline_encoded(types, enc, A, seconds, coords):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

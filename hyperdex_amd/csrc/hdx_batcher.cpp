@@ -99,11 +99,18 @@ struct Slot {
 }  // namespace
 
 struct hdx_batcher_s {
+    ~hdx_batcher_s() {
+        if (codes_dev) {  // after hdx_batcher_destroy's slot frees, or a failed create
+            (void)hipSetDevice(device);
+            (void)hipFree((void*)codes_dev);
+            (void)hipGetLastError();
+        }
+    }
     int device = -1;
     uint32_t A = 0;
     std::vector<uint8_t> codes;
     std::vector<uint32_t> types;
-    const uint8_t* codes_dev = nullptr;  // A > 128: the wide kernels' device copy (set_codes)
+    const uint8_t* codes_dev = nullptr;  // A > 256: the wide kernel's classes, owned (freed with the batcher)
     uint64_t host_max_bytes = 0;  // 0 with HDX_BATCHER_DEVICE_ONLY
     uint32_t max_obj = 0;
     uint64_t max_bytes = 0;
@@ -430,7 +437,19 @@ HDX_EXPORT hdx_status hdx_batcher_create(const uint32_t* types, uint32_t attrs_s
             delete b;
             return st;
         }
-        b->codes_dev = tmp.codes_dev;
+        if (tmp.codes_dev) {
+            // its own copy: the library's cache is freed at hdx_shutdown, a
+            // batcher may outlive that
+            uint8_t* own = nullptr;
+            if (hipMalloc((void**)&own, attrs_sz) != hipSuccess ||
+                hipMemcpy(own, codes.data(), attrs_sz, hipMemcpyHostToDevice) != hipSuccess) {
+                (void)hipGetLastError();
+                (void)hipFree(own);
+                delete b;
+                return fail(HDX_E_NOMEM, "batcher: device copy of %u attribute classes", attrs_sz);
+            }
+            b->codes_dev = own;
+        }
     }
     b->max_obj = c.max_objects ? c.max_objects : 4096;
     b->max_bytes = c.max_bytes ? c.max_bytes : (8ull << 20);

@@ -60,17 +60,19 @@ hdx_status check_schema(const uint32_t* types, uint32_t A, uint8_t* codes_out) {
     return HDX_OK;
 }
 
-// Attribute classes in device memory for the wide kernels (A > 128,
-// hdx_wide.hip): one copy per (device, schema), kept for the process's life
-// (a few bytes per attribute; an asynchronous launch may still read it when
-// hdx_shutdown runs).  On the calling thread's current device.
+// Attribute classes in device memory for the wide kernels (packed A > 256,
+// stored A > 128, hdx_wide.hip): one copy per (device, schema), cached until
+// hdx_shutdown (free_device_codes, after a device synchronisation, so no
+// launch still reads one).  On the calling thread's current device.
+static std::mutex g_codes_mu;
+static std::map<std::pair<int, std::string>, uint8_t*>* g_codes = new std::map<std::pair<int, std::string>, uint8_t*>();
+
 static hdx_status device_codes(const uint8_t* codes, uint32_t A, const uint8_t** out) {
-    static std::mutex mu;
-    static std::map<std::pair<int, std::string>, uint8_t*>* cache = new std::map<std::pair<int, std::string>, uint8_t*>();
+    std::map<std::pair<int, std::string>, uint8_t*>* cache = g_codes;
     int dev = -1;
     HIP_TRY(hipGetDevice(&dev));
     std::pair<int, std::string> key(dev, std::string((const char*)codes, A));
-    std::lock_guard<std::mutex> lk(mu);
+    std::lock_guard<std::mutex> lk(g_codes_mu);
     auto it = cache->find(key);
     if (it != cache->end()) {
         *out = it->second;
@@ -87,11 +89,21 @@ static hdx_status device_codes(const uint8_t* codes, uint32_t A, const uint8_t**
     return HDX_OK;
 }
 
+static void free_device_codes() {
+    std::lock_guard<std::mutex> lk(g_codes_mu);
+    for (auto& kv : *g_codes) {
+        if (hipSetDevice(kv.first.first) == hipSuccess && hipDeviceSynchronize() == hipSuccess) (void)hipFree(kv.second);
+        (void)hipGetLastError();
+    }
+    g_codes->clear();
+}
+
 // (debug library: variants 300 / 301 force the wide kernels at any A)
 hdx_status set_codes(BatchArgs& args, const uint8_t* codes, uint32_t A) {
     std::memcpy(args.codes, codes, std::min(A, kKernargCodes));
     args.codes_dev = nullptr;
-    return A > 128 || hash_variant() == 300 ? device_codes(codes, A, &args.codes_dev) : HDX_OK;
+    // only hash_wide_kernel (A > kKernargCodes) reads the device copy
+    return A > kKernargCodes || hash_variant() == 300 ? device_codes(codes, A, &args.codes_dev) : HDX_OK;
 }
 
 hdx_status set_codes(EncodedArgs& a, const uint8_t* codes, uint32_t A) {
@@ -327,6 +339,7 @@ HDX_EXPORT hdx_status hdx_shutdown(void) {
         for (Scratch* s : g_scratch) s->release();
     }
     trim_region_pools();
+    free_device_codes();
     if (had && dev >= 0) (void)hipSetDevice(dev);
     (void)hipGetLastError();
     return HDX_OK;
@@ -475,10 +488,10 @@ HDX_EXPORT hdx_status hdx_hash_encoded_regions_device(const uint32_t* types, uin
 }
 
 namespace hdx {
-hdx_status check_tables(const hdx_region_table* tables, uint32_t ntables, uint32_t A, const uint64_t* region_ids) {
+hdx_status check_table_list(const hdx_region_table* tables, uint32_t ntables, uint32_t A) {
     if (ntables > kMaxSweepTables)
         return fail(HDX_E_INVALID, "%u region tables (at most %u)", ntables, kMaxSweepTables);
-    if (ntables && (!tables || !region_ids)) return fail(HDX_E_INVALID, "NULL tables / region_ids");
+    if (ntables && !tables) return fail(HDX_E_INVALID, "NULL tables / region_ids");
     for (uint32_t t = 0; t < ntables; ++t) {
         if (!tables[t]) return fail(HDX_E_INVALID, "NULL table %u", t);
         for (uint32_t d = 0; d < tables[t]->D; ++d)
@@ -486,6 +499,11 @@ hdx_status check_tables(const hdx_region_table* tables, uint32_t ntables, uint32
                 return fail(HDX_E_INVALID, "table %u: subspace attribute %u >= attrs_sz %u", t, tables[t]->attrs[d], A);
     }
     return HDX_OK;
+}
+
+hdx_status check_tables(const hdx_region_table* tables, uint32_t ntables, uint32_t A, const uint64_t* region_ids) {
+    if (ntables && !region_ids) return fail(HDX_E_INVALID, "NULL tables / region_ids");
+    return check_table_list(tables, ntables, A);
 }
 
 hdx_status batch_args(BatchArgs& args, const uint8_t* codes, uint32_t A, const uint8_t* blob,

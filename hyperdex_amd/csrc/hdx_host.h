@@ -62,6 +62,8 @@ hdx_status set_codes(EncodedArgs& a, const uint8_t* codes, uint32_t A);
 // Region tables of a call: at most kMaxSweepTables, none NULL, every
 // subspace attribute < A; region_ids non-NULL when there are tables.
 hdx_status check_tables(const hdx_region_table* tables, uint32_t ntables, uint32_t A, const uint64_t* region_ids);
+// the table list alone (count, NULLs, subspace attributes < A): no output pointer
+hdx_status check_table_list(const hdx_region_table* tables, uint32_t ntables, uint32_t A);
 // A packed batch's kernel arguments on device `dev` (the calling thread's
 // current device): codes, arrays, and T tables whose ids go to ids + t *
 // ids_stride.

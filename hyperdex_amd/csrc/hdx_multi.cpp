@@ -59,8 +59,11 @@ public:
             stop_ = true;
         }
         cv_.notify_one();
-        th_.join();
+        if (th_.joinable()) th_.join();
     }
+    // a set dropped without destroy_set (a failed create) still ends its
+    // thread: a joinable std::thread's destructor would std::terminate
+    ~Worker() { join(); }
 
 private:
     void run() {
@@ -120,6 +123,11 @@ struct DeviceSet {
 
 static std::mutex g_set_mu;
 static std::shared_ptr<DeviceSet> g_set;
+// Serialises hdx_init_mask / hdx_shutdown (create and teardown) as whole
+// operations: two creates cannot both build a set, and one
+// cannot tear down the set another is installing.  Never taken by a call
+// that uses the set.
+static std::mutex g_lifecycle_mu;
 
 // A call's hold on the set (empty without one).
 class SetRef {
@@ -175,7 +183,7 @@ static void destroy_set(DeviceSet* ds) {
     ds->streams.clear();
 }
 
-void device_set_teardown() {
+static void teardown_locked() {
     std::shared_ptr<DeviceSet> ds;
     {
         std::lock_guard<std::mutex> lk(g_set_mu);
@@ -189,12 +197,18 @@ void device_set_teardown() {
     destroy_set(ds.get());
 }
 
+void device_set_teardown() {
+    std::lock_guard<std::mutex> life(g_lifecycle_mu);
+    teardown_locked();
+}
+
 hdx_status device_set_create(uint64_t mask, const std::vector<int>& devs) {
+    std::lock_guard<std::mutex> life(g_lifecycle_mu);
     {
         std::lock_guard<std::mutex> lk(g_set_mu);
         if (g_set && g_set->mask == mask && g_set->devs == devs) return HDX_OK;
     }
-    device_set_teardown();  // a different mask replaces the set (after the calls in progress)
+    teardown_locked();  // a different mask replaces the set (after the calls in progress)
     int cur = -1;
     const bool had = hipGetDevice(&cur) == hipSuccess;
     auto ds = std::make_shared<DeviceSet>();
@@ -433,7 +447,7 @@ static hdx_status device_multi(const uint32_t* types, uint32_t A, const std::vec
     hdx_status st = check_schema(types, A, codes.data());
     if (st != HDX_OK) return st;
     // the tables (each shard's region_ids pointer is checked with the shard)
-    if ((st = check_tables(tables, T, A, T ? (const uint64_t*)&T : nullptr)) != HDX_OK) return st;
+    if ((st = check_table_list(tables, T, A)) != HDX_OK) return st;
     std::unique_ptr<SetRef> ref = acquire_set();
     DeviceSet* ds = ref->get();
     if (!ds) return fail(HDX_E_INVALID, "no device set: call hdx_init_mask first");

@@ -22,7 +22,9 @@ def _bench(*argv, env_extra=None, timeout=240):
     return p
 
 
-@pytest.mark.parametrize("world,objects,form", [(2, 200_000, "in_place"), (3, 1001, "padded")])
+@pytest.mark.parametrize("world,objects,form", [(2, 200_000, "in_place"), (3, 1001, "padded"),
+                                                # the driver's SCALE command at N = 8
+                                                (8, 1_600_000, "in_place"), (8, 1001, "padded")])
 def test_bare_bench_spawns_ranks(world, objects, form):
     p = _bench("--gpus", str(world), "--config4-objects", str(objects))
     assert p.returncode == 0, p.stderr[-2000:]
