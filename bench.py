@@ -38,12 +38,16 @@ import time
 import numpy as np
 
 
+SWEEP_NUM2 = True  # the product sweep's NUM2 form (config 3b's schema) (hdx_wsweep.hip launch_hash_wsweep_product)
+
+
 def sweep_kernel_name(layout):
     """The product sweep's kernel (hdx_wsweep.hip launch_hash_wsweep_product) as
     rocprofv3 names it: the record instantiation when keys and values are one
     store (layout "records"), else the other one."""
     return ("void hdx::hash_sweep_wstage_kernel<2, 9728u, 7u, false, true, 0, 13, false, true, true, %s, true, "
-            "false, 1, true, 4>(hdx::EncodedArgs)" % ("true" if layout == "records" else "false"))
+            "false, 1, true, 4, %s>(hdx::EncodedArgs)" % ("true" if layout == "records" else "false",
+                                                          "true" if SWEEP_NUM2 else "false"))
 
 
 def log(*a):
@@ -77,6 +81,9 @@ def parse_args(argv=None):
                          "SURVEY §8d) or 'records' ([key][value] back to back, a LevelDB block's adjacency)")
     ap.add_argument("--config4-objects", type=int, default=100_000_000,
                     help="config 4: objects of the whole sharded batch (0 = skip)")
+    ap.add_argument("--cfg5-objects", type=int, default=50_000_000,
+                    help="config 5 (reindex sweep, key column) in the config-3a line's `secondary` "
+                         "(0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-allgather", action="store_true")
@@ -324,10 +331,12 @@ def run_rank(args):
             guarded(result, "host_path", lambda: time_host_path(types, blob, base, lens, A, coords),
                     watchdog_s=DEVICE_SET_WATCHDOG_S, fatal=True)
 
+    secondary = {}
     if rank == 0 and world == 1 and cfg == "cfg3a" and not args.no_secondary:
         # BASELINE's third config with its mixed attribute types, measured the
         # same way in the same run (the headline line stays config 3a's)
-        guarded(result, "secondary", lambda: {"cfg3b": time_config("cfg3b", n, dev, stream)})
+        guarded(secondary, "cfg3b", lambda: time_config("cfg3b", n, dev, stream))
+        result["secondary"] = secondary
 
     if args.config4_objects and cfg != "cfg5":
         result["config4"] = time_config4(args.config4_objects, world, rank, dev, stream, max_over_ranks,
@@ -339,6 +348,13 @@ def run_rank(args):
             guarded(result, "config4_device_set",
                     lambda: time_config4_device_set(args.config4_objects, dev, stream),
                     watchdog_s=DEVICE_SET_WATCHDOG_S, fatal=True)
+
+    if rank == 0 and world == 1 and cfg == "cfg3a" and not args.no_secondary and args.cfg5_objects:
+        # BASELINE config 5 (the reindex sweep at its 50 M objects), after
+        # config 4's buffers are gone: 66 GB beside the headline batch
+        torch.cuda.empty_cache()
+        guarded(secondary, "cfg5", lambda: time_config5(args.cfg5_objects, dev, stream))
+        result["secondary"] = secondary
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         if cfg == "cfg5":
@@ -884,6 +900,54 @@ def time_config(cfg, n, dev, stream, steps=10, warmup=2, warmup_ms=150.0):
     if valu is not None:
         res["valu"] = valu
     del blob, base, lens, coords
+    torch.cuda.empty_cache()
+    return res
+
+
+def time_config5(n, dev, stream, layout="keycol", steps=10, warmup=2, warmup_ms=150.0):
+    """BASELINE config 5 beside the headline line: the reindex
+    sweep over n stored config-3b objects (the daemon's value encoding, keys in
+    a key column: SURVEY §8d's layout), decoded + hashed in HBM by the product
+    sweep (hdx_hash_encoded_device), HIP events around each launch.
+    Algorithmic bytes per object: key + value bytes, two u64
+    offsets + two u32 lengths, 8 B per coordinate."""
+    import torch
+
+    import hyperdex_amd as hdx
+    from hyperdex_amd import synth
+    types, *enc = synth.make_encoded_device("cfg3b", n, device=dev, layout=layout)
+    A = len(types)
+    key_len, val_len = enc[2], enc[5]
+    payload = int(key_len.to(torch.int64).sum().item()) + int(val_len.to(torch.int64).sum().item())
+    coords = torch.empty((n, A), dtype=torch.int64, device=dev)
+
+    def run():
+        hdx.hash_encoded(types, *enc, coords=coords, stream=stream)
+    for _ in range(warmup):
+        run()
+    sustain(run, stream, warmup_ms)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    torch.cuda.synchronize()
+    for s, e in ev:
+        s.record(stream)
+        run()
+        e.record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.mean([s.elapsed_time(e) for s, e in ev]))
+    algo = payload + n * 24 + n * A * 8
+    key = "cfg5" + {"keycol": "k", "records": "r"}.get(layout, "")
+    traffic, traffic_src = measured_traffic(latest_traffic_file(), key, n)
+    res = {"workload": "config 5 (reindex sweep): %dM stored config-3b objects, %s layout" % (n // 1_000_000, layout),
+           "objects": n, "store_layout": layout, "payload_bytes": payload,
+           "GiB_s": round(payload / (ms / 1e3) / 2**30, 3), "mobjects_per_s": round(n / (ms / 1e3) / 1e6, 2),
+           "kernel_ms": round(ms, 4), "algorithmic_bytes_per_launch": algo,
+           "roofline_frac": round(algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
+           "traffic": traffic, "traffic_source": traffic_src,
+           "kernel": sweep_kernel_name(layout)}
+    valu = measured_valu(latest_traffic_file(), key, n, ms)
+    if valu is not None:
+        res["valu"] = valu
+    del enc, coords
     torch.cuda.empty_cache()
     return res
 

@@ -13,7 +13,7 @@ from .hashing import (hash, hash_batch, hash_batch_host, hash_encoded, hash_enco
                       hash_key, hash_object, hashable, schema_check, init_mask, device_set, shutdown,
                       hash_batch_device_multi, hash_batch_regions_host, hash_encoded_host,
                       hash_encoded_host_status, hash_batch_regions_device_multi)
-from .regions import RegionTable, lookup_region  # noqa: F401
+from .regions import PointLeaderAbort, PointLeaders, RegionTable, lookup_region  # noqa: F401
 from .index import index_encode, index_key_size, search_regions, search_space  # noqa: F401
 from .batcher import Batcher  # noqa: F401
 
@@ -21,4 +21,4 @@ __all__ = ["HdxError", "Attribute", "Schema", "hash", "hash_key", "hash_object",
            "hash_batch_host", "hash_encoded", "hash_encoded_regions", "hash_batch_regions", "hash_batch_regions_host",
            "hash_encoded_host", "hash_encoded_host_status", "hash_batch_device_multi", "hash_batch_regions_device_multi",
            "init_mask", "device_set", "shutdown", "hashable", "schema_check", "RegionTable",
-           "lookup_region", "index_encode", "index_key_size", "search_regions", "search_space", "Batcher", "lib"]
+           "lookup_region", "PointLeaders", "PointLeaderAbort", "index_encode", "index_key_size", "search_regions", "search_space", "Batcher", "lib"]

@@ -123,6 +123,19 @@ __device__ __forceinline__ uint64_t encode_double(uint64_t bits) {
     return (bits | 0x8000000000000000ULL) + 2;                     // sign'=1, +2
 }
 
+// encode_double without branches (the same cases, as selects): -bits for a
+// negative finite x (~bits & 0x7fff... + 1), bits + 2^63 + 2 for a positive
+// one, then ±0, ±inf and NaN override in the reference's precedence.
+__device__ __forceinline__ uint64_t encode_double_sel(uint64_t bits) {
+    const uint64_t EXP = 0x7ff0000000000000ULL;
+    const uint64_t mag = bits & 0x7fffffffffffffffULL;
+    const bool neg = (int64_t)bits < 0;
+    uint64_t r = neg ? 0 - bits : bits + 0x8000000000000002ULL;
+    r = mag == 0 ? 0x8000000000000001ULL : r;
+    const uint64_t special = mag == EXP ? (neg ? 0ULL : 0xfff0000000000002ULL) : 0xfff0000000000003ULL;
+    return mag >= EXP ? special : r;
+}
+
 // datatype_timestamp.cc:117-219 for granularity G (0..5 = second..month).
 // TABLE_* (:131-136) visits digit G, G-1, .., 0, then G+1 .. 6; the running
 // divisor y_i = floor(y_{i-1} / I[T[i]]) from y = UINT64_MAX depends only on G,

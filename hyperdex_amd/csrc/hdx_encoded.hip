@@ -486,6 +486,11 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
             if (e != hipErrorInvalidValue) return e;
             break;
         }
+        case 293: {  // round 6: the product sweep with NUM2 (numerics by selects, the class table)
+            const hipError_t e = launch_hash_wsweep(a, stream, 36);
+            if (e != hipErrorInvalidValue) return e;
+            break;
+        }
         case 277: case 278: {  // the product sweep without wave priorities (277), with the passes high (278)
             const hipError_t e = launch_hash_wsweep(a, stream, hash_variant() == 277 ? 31 : 32);
             if (e != hipErrorInvalidValue) return e;

@@ -21,6 +21,7 @@ namespace hdx {
 // the classes from codes_dev, a device copy (device_codes, hdx_capi.cpp).
 constexpr uint32_t kKernargCodes = 256;
 constexpr uint32_t kMaxSweepTables = 4;
+constexpr uint32_t kWavePlanSlots = 128;  // BatchArgs::plan: two 64-slot passes
 struct SweepTable {
     const uint64_t* index;  // interval index (NULL: scan lower/upper)
     const uint64_t* lower;
@@ -50,6 +51,12 @@ struct BatchArgs {
     // objects per wave, lds_tables u64 words of LDS table copies per workgroup
     uint32_t T, K, lds_tables, win_bytes;  // win_bytes: the staged kernels' LDS window (hdx_staged.hip)
     SweepTable t[kMaxSweepTables];
+    // The wave-staged kernel's slot plan (hdx_wstage.h, PLAN; filled by its
+    // launcher): every wave holds K objects of the same schema, so slot s of
+    // any wave is attribute s % A of object s / A — j | o << 8 | code << 16,
+    // code CODE_ZERO past the K objects.  Replaces per-slot division and the
+    // code-table shuffle on the device.
+    uint32_t plan[kWavePlanSlots];
 };
 
 hipError_t launch_hash_batch(const BatchArgs& args, hipStream_t stream);

@@ -417,8 +417,20 @@ __device__ __forceinline__ uint64_t hash_string_window(ldsw_t w, uint32_t off, u
 // TNUM: every slot reads its last 32 bytes before the type dispatch, and an
 // 8-byte numeric takes its value from them (q3) — one read for the numeric
 // and string lanes of a pass instead of two.
-template <int W128 = 0, int LOOP = 1, bool TNUM = false>
+// NUM2: the schema's codes are STRING / INT64 / FLOAT only (pads CODE_ZERO):
+// numerics by selects (encode_int64 / encode_double_sel), no timestamp code.
+template <int W128 = 0, int LOOP = 1, bool TNUM = false, bool NUM2 = false>
 __device__ __forceinline__ uint64_t hash_slot_window(ldsw_t w, uint32_t code, uint32_t off, uint32_t n, bool& bad) {
+    if constexpr (NUM2) {
+        static_assert(TNUM, "NUM2 takes the numeric from the tail read");
+        const Q32 t = lds_read32<W128>(w, off + n - 32);  // the front pad covers n < 32
+        if (code == CODE_STRING) return hash_string_window<W128, LOOP>(w, off, n, t);
+        const bool num = code != CODE_ZERO;
+        bad |= num && n != 8 && n != 0;
+        const uint64_t bits = n == 8 ? t.q3 : 0;
+        const uint64_t h = code == CODE_FLOAT ? encode_double_sel(bits) : encode_int64(bits);
+        return num && (n == 8 || n == 0) ? h : 0;
+    }
     if constexpr (TNUM) {
         if (code == CODE_ZERO) return 0;
         const Q32 t = lds_read32<W128>(w, off + n - 32);  // the front pad covers n < 32

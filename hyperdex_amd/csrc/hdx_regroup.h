@@ -138,6 +138,23 @@ __device__ __forceinline__ uint32_t work_class1_bf(uint32_t code, uint32_t n, bo
     return valid && code == CODE_STRING ? c : 0u;
 }
 
+// work_class<1> from a table: 3-bit classes indexed by ceil(min(n, 272) / 16)
+// (0..17), one 64-bit shift instead of the comparison chain (ORDER 5 of the
+// wave-staged kernel, with the slot plan).
+constexpr uint64_t class1_table() {
+    // idx: 0-1 <= 16 B (2), 2 17..32 (3), 3-4 33..64 (1), 5-8 one block (4),
+    // 9-12 two (5), 13-16 three (6), 17 four or more (7)
+    constexpr uint8_t c[18] = {2, 2, 3, 1, 1, 4, 4, 4, 4, 5, 5, 5, 5, 6, 6, 6, 6, 7};
+    uint64_t t = 0;
+    for (int i = 0; i < 18; ++i) t |= (uint64_t)c[i] << (3 * i);
+    return t;
+}
+__device__ __forceinline__ uint32_t work_class1_tab(uint32_t code, uint32_t n, bool valid) {
+    const uint32_t idx = (min(n, 272u) + 15u) >> 4;
+    const uint32_t c = (uint32_t)(class1_table() >> (3 * idx)) & 7u;
+    return valid && code == CODE_STRING ? c : 0u;
+}
+
 // Wave-local counting sort of a wave's NCH * 64 slots by work class into
 // perm[] (slot | code << 8, pass t = perm[64 t .. 64 t + 63]); slots s >= ns
 // are pads (hashed as CODE_ZERO, results unused).  A pass pays for the union

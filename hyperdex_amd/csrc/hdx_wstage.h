@@ -95,7 +95,10 @@ struct Group {
 // bases and lengths and waited for before the DMA goes out — nothing in
 // phases 2-3 then waits for the DMA.
 // NT: the bases, lengths and span loaded non-temporal (read once).
-template <int NCH, uint32_t WB, int SHAPE, int ORDER = 1, bool ADMA = false, bool DL = false, bool NT = false>
+// PLAN: slot s's object, attribute and code from args.plan (the launcher's
+// per-schema table) instead of a division and a code-table shuffle.
+template <int NCH, uint32_t WB, int SHAPE, int ORDER = 1, bool ADMA = false, bool DL = false, bool NT = false,
+          bool PLAN = false>
 __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint64_t o0, uint8_t* win, uint32_t win_off,
                                                      uint64_t* desc) {
     const int lane = threadIdx.x & 63;
@@ -117,7 +120,15 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
         g.L[c] = s < g.ns ? (NT ? __builtin_nontemporal_load(args.attr_len + g.q0 + s) : args.attr_len[g.q0 + s]) : 0u;
     }
     uint32_t packed_codes = 0;
-    if constexpr (ADMA) {
+    uint32_t pw[NCH];
+    if constexpr (PLAN) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c) pw[c] = args.plan[c * 64 + lane];
+        if constexpr (ADMA) {
+#pragma unroll
+            for (int c = 0; c < NCH; ++c) asm volatile("" ::"v"(pw[c]));  // loaded before the DMA is issued
+        }
+    } else if constexpr (ADMA) {
         packed_codes = reinterpret_cast<const uint32_t*>(args.codes)[lane];
         asm volatile("" ::"v"(packed_codes));  // its load completes before the DMA is issued
     }
@@ -136,22 +147,23 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
     if (early && SHAPE != 2) dma((lead + (uint32_t)(bnext - b0) + 15) >> 4);
 
     // ---- in-object offsets, codes, object sizes ----------------------------
-    if constexpr (!ADMA) packed_codes = reinterpret_cast<const uint32_t*>(args.codes)[lane];
-    uint32_t off[NCH], endv[NCH];
+    if constexpr (!ADMA && !PLAN) packed_codes = reinterpret_cast<const uint32_t*>(args.codes)[lane];
+    uint32_t off[NCH], endv[NCH], obj[NCH];
     uint32_t carry = 0;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
         const uint32_t s = (uint32_t)(c * 64 + lane);
-        const uint32_t o = div_small(s, args.a_magic);
-        const uint32_t j = s - o * A;
+        const uint32_t o = PLAN ? (pw[c] >> 8) & 0xffu : div_small(s, args.a_magic);
+        const uint32_t j = PLAN ? pw[c] & 0xffu : s - o * A;
+        obj[c] = o;
         const uint32_t Sx = wave_scan_dpp(g.L[c]) - g.L[c];
         const int head = lane - (int)j;
         const uint32_t head_sx = __shfl(Sx, head < 0 ? 0 : head, 64);
         off[c] = head >= 0 ? Sx - head_sx : carry + Sx;
         carry = __builtin_amdgcn_readlane(off[c] + g.L[c], 63);
-        const uint32_t cd = args.uniform_code != 0xffu
-                                ? args.uniform_code
-                                : (__shfl(packed_codes, (int)(j >> 2), 64) >> (8 * (j & 3))) & 0xffu;
+        const uint32_t cd = PLAN                          ? pw[c] >> 16
+                            : args.uniform_code != 0xffu ? args.uniform_code
+                                                         : (__shfl(packed_codes, (int)(j >> 2), 64) >> (8 * (j & 3))) & 0xffu;
         g.code[c] = s < g.ns ? cd : (uint32_t)CODE_ZERO;
         endv[c] = off[c] + g.L[c];
     }
@@ -174,13 +186,14 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
         const uint32_t s = (uint32_t)(c * 64 + lane);
-        const uint32_t o = div_small(s, args.a_magic);
+        const uint32_t o = obj[c];
         const uint32_t orel = (uint32_t)__shfl((int)rel, (int)(o & 63), 64);
         const uint32_t doff = g.staged ? orel + off[c] : off[c];
         g.doff[c] = doff;
         if (desc) desc[s] = (uint64_t)doff | ((uint64_t)g.L[c] << 32);
         g.cls[c] = ORDER == 3   ? work_class3(g.code[c], g.L[c], s < g.ns)
                    : ORDER == 4 ? work_class1_bf(g.code[c], g.L[c], s < g.ns)
+                   : ORDER == 5 ? work_class1_tab(g.code[c], g.L[c], s < g.ns)
                                 : work_class<1>(g.code[c], g.L[c], s < g.ns);
     }
     return g;
@@ -193,12 +206,14 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
 // regime from the same two reads; lw then points kFrontHT bytes before the
 // window); HT 2 / 3: hash_slot_window's LOOP 2 / 3; HT 5: LOOP 2 with TNUM.
 constexpr uint32_t kFrontHT = 32;
-template <int SHAPE, int HT = 0, int W128 = 0>
+template <int SHAPE, int HT = 0, int W128 = 0, bool NUM2 = false>
 __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, bool staged, uint64_t mybase,
                                               uint32_t s, uint32_t cd, uint64_t d, bool& bad) {
     const uint32_t doff = (uint32_t)d, dn = (uint32_t)(d >> 32);
     if (SHAPE == 1) return lw[doff >> 2] ^ dn;
-    if (staged && HT) return hash_slot_window<W128, (HT >= 5 ? 2 : HT > 1 ? HT : 1), (HT >= 5)>(lw, cd, doff + kFrontHT, dn, bad);
+    if (staged && HT)
+        return hash_slot_window<W128, (HT >= 5 ? 2 : HT > 1 ? HT : 1), (HT >= 5), NUM2 && HT >= 5>(lw, cd, doff + kFrontHT,
+                                                                                                  dn, bad);
     if (staged) return cd == CODE_STRING ? hash_string_lds(lw, doff, dn) : hash_numeric_lds(lw, cd, doff, dn, bad);
     const uint32_t o = div_small(s, args.a_magic);
     const uint64_t ob = shfl64(mybase, (int)(o & 63));
@@ -218,9 +233,11 @@ __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, 
 // span copy, addresses and predicate per KiB (dma_units16_loop).  WPB: waves
 // (each with its own window) per workgroup.  NT: the lengths, bases and span
 // loaded non-temporal (read once).
+// PLAN: the slot plan (describe_group); NUM2: numerics by selects, the
+// schema holds strings, int64 and floats only (the launcher checks).
 template <int NCH, uint32_t WB, int SHAPE = 0, int HT = 0, int ORDER = 1, int W128 = 0, bool REGIONS = false,
           bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false, int WPB = 4, bool XS = false,
-          bool RD = false, bool NT = false, int PRIO = 0>
+          bool RD = false, bool NT = false, int PRIO = 0, bool PLAN = false, bool NUM2 = false>
 __global__ void __launch_bounds__(64 * WPB)
 hash_wstage_kernel(const BatchArgs args) {
     // PRIO (A/B): 1 = the load phase at high wave priority, the passes at low;
@@ -243,7 +260,7 @@ hash_wstage_kernel(const BatchArgs args) {
 
     const uint64_t o0 = ((uint64_t)(XS ? xcd_block() : blockIdx.x) * WPB + w) * args.K;
     if (o0 >= args.n) return;  // no barrier anywhere: waves are independent
-    const Group<NCH> g = describe_group<NCH, WB, SHAPE, ORDER, ADMA, DL, NT>(args, o0, win, 0, desc);
+    const Group<NCH> g = describe_group<NCH, WB, SHAPE, ORDER, ADMA, DL, NT, PLAN>(args, o0, win, 0, desc);
 
     // ---- counting sort by work class (wave-local) --------------------------
     uint32_t pos[NCH];
@@ -276,7 +293,7 @@ hash_wstage_kernel(const BatchArgs args) {
                     ln = l;
                 }
             }
-            res[t] = hash_slot<SHAPE, HT, W128>(args, lw, g.staged, g.mybase, s, e >> 8,
+            res[t] = hash_slot<SHAPE, HT, W128, NUM2>(args, lw, g.staged, g.mybase, s, e >> 8,
                                                 (uint64_t)doff | ((uint64_t)ln << 32), bad);
         }
 #pragma unroll
@@ -302,7 +319,7 @@ hash_wstage_kernel(const BatchArgs args) {
     for (int t = 0; t < NCH; ++t) {
         const uint32_t e = perm[t * 64 + lane];
         const uint32_t s = e & 0xffu;
-        desc[s] = hash_slot<SHAPE, HT, W128>(args, lw, g.staged, g.mybase, s, e >> 8, desc[s], bad);
+        desc[s] = hash_slot<SHAPE, HT, W128, NUM2>(args, lw, g.staged, g.mybase, s, e >> 8, desc[s], bad);
     }
     wave_lds_fence();
     if constexpr (PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(2);  // the stores (and the wave's end) ahead of the hashing waves
@@ -323,18 +340,37 @@ hash_wstage_kernel(const BatchArgs args) {
 
 // Launch: K = floor(64 * NCH / A) whole objects per wave (at most 63), four
 // independent waves per 256-thread workgroup, no workgroup barrier.
+// The slot plan of BatchArgs::plan for K objects of A attributes.
+inline void fill_wave_plan(BatchArgs& args) {
+    for (uint32_t s = 0; s < kWavePlanSlots; ++s) {
+        const uint32_t o = s / args.A, j = s % args.A;
+        const uint32_t code = o < args.K ? args.codes[j] : (uint32_t)CODE_ZERO;
+        args.plan[s] = (j & 0xffu) | (o & 0xffu) << 8 | code << 16;
+    }
+}
+// Codes the NUM2 kernels handle: strings, int64 and floats.
+inline bool num2_schema(const BatchArgs& args) {
+    for (uint32_t j = 0; j < args.A && j < kKernargCodes; ++j)
+        if (args.codes[j] != CODE_STRING && args.codes[j] != CODE_INT64 && args.codes[j] != CODE_FLOAT) return false;
+    return args.A <= kKernargCodes;
+}
+
 template <int NCH, uint32_t WB, uint32_t KCAP = 63, int SHAPE = 0, int HT = 0, int ORDER = 1, int W128 = 0,
           bool REGIONS = false, bool GAP = false, bool ADMA = false, bool PU = true, bool DL = false, int WPB = 4,
-          bool XS = false, bool RD = false, bool NT = false, int PRIO = 0>
+          bool XS = false, bool RD = false, bool NT = false, int PRIO = 0, bool PLAN = false, bool NUM2 = false>
 static hipError_t launch_wstage_t(BatchArgs args, hipStream_t stream) {
     // lane o holds object o's base and lane K the next group's first: K <= 63
     args.K = std::min<uint32_t>(std::min<uint32_t>((uint32_t)(64 * NCH) / args.A, KCAP), 63u);
     if (args.K == 0) return hipErrorInvalidValue;
+    static_assert(!PLAN || NCH * 64 <= kWavePlanSlots, "the plan covers two passes");
+    if (PLAN) fill_wave_plan(args);
+    if (NUM2 && !num2_schema(args)) return hipErrorInvalidValue;
     const uint64_t waves = (args.n + args.K - 1) / args.K;
     const uint64_t blocks = (waves + WPB - 1) / WPB;
     if (blocks == 0) return hipSuccess;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA, PU, DL, WPB, XS, RD, NT, PRIO>),
+    hipLaunchKernelGGL((hash_wstage_kernel<NCH, WB, SHAPE, HT, ORDER, W128, REGIONS, GAP, ADMA, PU, DL, WPB, XS, RD, NT, PRIO,
+                                           PLAN, NUM2>),
                        dim3((uint32_t)blocks), dim3(64 * WPB), 0, stream, args);
     return hipGetLastError();
 }

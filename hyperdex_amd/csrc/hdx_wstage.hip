@@ -15,19 +15,33 @@
 // loads and span DMA out ahead of the waves that are hashing — 2.500 vs 2.555
 // ms on a fast box, 2.711–2.729 vs 2.716–2.746 on a slow one (variant 287 vs
 // 279, profiles/r5/ab_priority.jsonl).
+// Round 6 (variant 293): the per-schema slot plan (each slot's object,
+// attribute and code from the launcher's table, BatchArgs::plan), numerics by
+// selects for schemas of strings, int64 and floats only (NUM2), and the work
+// class from a table (ORDER 5): 862.6 -> 841.6 VALU and 264.9 -> 238.9 SALU
+// per wave, 2.666 vs 2.709 ms (profiles/r6/ab_plan.jsonl,
+// pmc_lds_cfg3b_plan.txt).  Other schemas (timestamps, non-hashable types:
+// forced debug variants only — the policy gives them the regroup kernel) keep
+// the round-5 instantiation.
 #include "hdx_wstage.h"
 
 namespace hdx {
 
 hipError_t launch_hash_wstage_product(const BatchArgs& args, hipStream_t stream) {
     if (args.n == 0) return hipSuccess;
-    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, false, true, true, true, false, 1, true, false, true, 1>(args, stream);
+    if (num2_schema(args))
+        return launch_wstage_t<2, 8832, 63, 0, 5, 5, 0, false, true, true, true, false, 1, true, false, true, 1, true,
+                               true>(args, stream);
+    return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 1>(args, stream);
 }
 
 // ... with the fused region lookup (args.T tables; args.coords may be NULL)
 hipError_t launch_hash_wstage_regions(const BatchArgs& args, hipStream_t stream) {
     if (args.n == 0) return hipSuccess;
-    return launch_wstage_t<2, 8832, 63, 0, 5, 4, false, true, true, true, true, false, 1, true, false, true, 1>(args, stream);
+    if (num2_schema(args))
+        return launch_wstage_t<2, 8832, 63, 0, 5, 5, 0, true, true, true, true, false, 1, true, false, true, 1, true,
+                               true>(args, stream);
+    return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, true, true, true, true, false, 1, true, false, true, 1>(args, stream);
 }
 
 }  // namespace hdx

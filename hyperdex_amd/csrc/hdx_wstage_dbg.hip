@@ -177,6 +177,12 @@ hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int for
         case 90: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 4>(args, stream);  // the product, stores alone at high wave priority
         case 91: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 5>(args, stream);  // loads and stores at the top priority
         case 92: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 6>(args, stream);  // loads high, the sort medium, the passes low
+        // round 6: the per-schema slot plan (PLAN), numerics by selects (NUM2), the class table (ORDER 5)
+        case 93: return launch_wstage_t<2, 8832, 63, 0, 5, 5, 0, false, true, true, true, false, 1, true, false, true, 1, true, true>(args, stream);  // all three
+        case 94: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 1, true, false>(args, stream);  // the plan alone
+        case 95: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 1, false, true>(args, stream);  // NUM2 alone
+        case 96: return launch_wstage_t<2, 8832, 63, 0, 5, 5, 0, false, true, true, true, false, 1, true, false, true, 1, false, false>(args, stream);  // the class table alone
+        case 97: return launch_wstage_t<2, 8832, 63, 1, 5, 5, 0, false, true, true, true, false, 1, true, false, true, 1, true, true>(args, stream);  // debug shape of 93: no hash (WRONG coordinates)
         // the slots class-sorted over the workgroup
         case 10: return launch_wgstage_t<2, 8832>(args, stream);
         case 11: return launch_wgstage_t<1, 4352>(args, stream);

@@ -105,6 +105,12 @@ __device__ __forceinline__ uint32_t sweep_class_bf(uint32_t code, uint32_t n, bo
     return zero ? 0u : global ? 7u : c;
 }
 
+// ... from the class table (work_class1_tab, NUM2 forms)
+__device__ __forceinline__ uint32_t sweep_class_tab(uint32_t code, uint32_t n, bool zero, bool global) {
+    const uint32_t c = std::min<uint32_t>(work_class1_tab(code, n, true), 6u);
+    return zero ? 0u : global ? 7u : c;
+}
+
 __device__ __forceinline__ uint64_t hash_global(const uint8_t* p, uint32_t code, uint32_t n, bool& bad) {
     return hash_blk<false, false, true>(code, p, n, consume_any<true>(issue_any<true>(code, p, n)), bad);
 }
@@ -151,9 +157,11 @@ __device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint
 // the hash on made-up descriptors (the compute alone); 1 = no hash (a slot's
 // coordinate is its descriptor), 2 = no hash and no walk.  SHAPE 4 (debug
 // form 22, correct coordinates): the walk's reads as round 3's dword pairs.
+// NUM2 (round 6): a schema of strings, int64 and floats only — numerics by
+// selects (hash_slot_window NUM2) and the class from the table.
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
           bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true, bool DL = false,
-          int WPB = 4, bool XS = false, int PRIO = 0>
+          int WPB = 4, bool XS = false, int PRIO = 0, bool NUM2 = false>
 __global__ void __launch_bounds__(64 * WPB)
 hash_sweep_wstage_kernel(const EncodedArgs a) {
     if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4 || PRIO == 5) __builtin_amdgcn_s_setprio(3);
@@ -371,7 +379,8 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
             const bool zero = (uint32_t)d == kZero;
             const uint32_t ln = (uint32_t)(d >> 32);
             cd[c] = valid && !zero ? c0 : (uint32_t)CODE_ZERO;
-            cls[c] = sweep_class_bf(cd[c], ln & ~kGlobal, !valid || zero, (ln & kGlobal) != 0);
+            cls[c] = NUM2 ? sweep_class_tab(cd[c], ln & ~kGlobal, !valid || zero, (ln & kGlobal) != 0)
+                          : sweep_class_bf(cd[c], ln & ~kGlobal, !valid || zero, (ln & kGlobal) != 0);
         } else {
             const uint64_t d = valid ? desc[s] : (uint64_t)kZero;
             const bool zero = (uint32_t)d == kZero;
@@ -406,7 +415,8 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         if (s < ns && off != kZero) {
             if (ln & kGlobal) h = hash_global((j == 0 ? a.keys : a.vals) + ob + off, code, ln & ~kGlobal, bad);
             else if (SHAPE == 1 || SHAPE == 2) h = d ^ lw[off >> 2];
-            else h = hash_slot_window<false, (LOOP >= 10 ? LOOP - 10 : LOOP), (LOOP >= 10)>(lw, code, off, ln, bad);
+            else h = hash_slot_window<false, (LOOP >= 10 ? LOOP - 10 : LOOP), (LOOP >= 10), NUM2 && LOOP >= 10>(
+                lw, code, off, ln, bad);
         }
         desc[s] = h;
     }
@@ -426,16 +436,26 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
+// Codes the NUM2 forms handle: strings, int64 and floats.
+static bool num2_codes(const EncodedArgs& a) {
+    if (a.A > kKernargCodes) return false;
+    for (uint32_t j = 0; j < a.A; ++j)
+        if (a.codes[j] != CODE_STRING && a.codes[j] != CODE_INT64 && a.codes[j] != CODE_FLOAT) return false;
+    return true;
+}
+
 template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = false, int SHAPE = 0, int LOOP = 1,
           bool ASM = false, bool PU = true, bool BF = false, bool RECS = true, bool KUNITS = true, bool DL = false,
-          int WPB = 4, bool XS = false, int PRIO = 0>
+          int WPB = 4, bool XS = false, int PRIO = 0, bool NUM2 = false>
 static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
     const uint32_t K = std::min<uint32_t>(64 * NCH / a.A, KCAP);
     if (K == 0) return hipErrorInvalidValue;
+    if (NUM2 && !num2_codes(a)) return hipErrorInvalidValue;
     const uint64_t waves = (a.n + K - 1) / K;
     const uint64_t blocks = (waves + WPB - 1) / WPB;
     if (blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU, BF, RECS, KUNITS, DL, WPB, XS, PRIO>),
+    hipLaunchKernelGGL((hash_sweep_wstage_kernel<NCH, WB, KCAP, REGIONS, GAP, SHAPE, LOOP, ASM, PU, BF, RECS, KUNITS, DL, WPB, XS, PRIO,
+                                                 NUM2>),
                        dim3((uint32_t)blocks), dim3(64 * WPB), 0, stream, a);
     return hipGetLastError();
 }
@@ -461,15 +481,24 @@ static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
 // 3.357 vs 3.424 keys in place, 3.146 vs 3.213 records; the walk at high
 // priority 3.211 / 3.369 / 3.155; loads high alone −0.3 to −1.2 %
 // (profiles/r5/ab_priority.jsonl).
+// Round 6: NUM2 for schemas of strings, int64 and floats (numerics by
+// selects, the class from the table): 3.258 vs 3.304 ms per 10 M on the key
+// column, VALU 971.8 -> 956.8 and SALU 401.1 -> 370.1 per wave
+// (profiles/r6/ab_sweep_num2.jsonl, pmc_lds_cfg5k_num2.txt); other schemas keep
+// the round-5 form.
+template <bool REG, bool RECS>
+static hipError_t launch_wsweep_product_t(const EncodedArgs& a, hipStream_t stream) {
+    if (num2_codes(a))
+        return launch_wsweep_t<2, 9728, 7, REG, true, 0, 13, false, true, true, RECS, true, false, 1, true, 4, true>(a, stream);
+    return launch_wsweep_t<2, 9728, 7, REG, true, 0, 13, false, true, true, RECS, true, false, 1, true, 4>(a, stream);
+}
+
 hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream) {
     if (a.n == 0) return hipSuccess;
     const bool recs = a.keys == a.vals;
-    if (a.T)
-        return recs ? launch_wsweep_t<2, 9728, 7, true, true, 0, 13, false, true, true, true, true, false, 1, true, 4>(a, stream)
-                    : launch_wsweep_t<2, 9728, 7, true, true, 0, 13, false, true, true, false, true, false, 1, true, 4>(a, stream);
+    if (a.T) return recs ? launch_wsweep_product_t<true, true>(a, stream) : launch_wsweep_product_t<true, false>(a, stream);
     if (!a.coords) return hipErrorInvalidValue;
-    return recs ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 4>(a, stream)
-                : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 4>(a, stream);
+    return recs ? launch_wsweep_product_t<false, true>(a, stream) : launch_wsweep_product_t<false, false>(a, stream);
 }
 
 #ifndef HDX_DEBUG_BUILD
@@ -542,6 +571,9 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
                        ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 2>(a, stream)
                        : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 2>(a, stream);
         }
+        case 36: return a.keys == a.vals  // round 6: the product with NUM2 (numerics by selects, the class table)
+                        ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 4, true>(a, stream)
+                        : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 4, true>(a, stream);
         case 26: return a.keys == a.vals  // round 4's product: four waves per workgroup
                         ? launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, true, true, false, 4>(a, stream)
                         : launch_wsweep_t<2, 8704, 6, false, true, 0, 13, false, true, true, false, true, false, 4>(a, stream);

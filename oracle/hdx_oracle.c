@@ -388,6 +388,26 @@ void hdxo_lookup_region(uint32_t D, uint32_t R, const uint16_t* attrs, const uin
     }
 }
 
+/* ---- point_leader (common/configuration.cc:427-458; :460-497 is the same
+ * scan after finding the region) --------------------------------------------
+ * h = hash(sc, key) (hash.cc:48-54: the key's own type), then the first
+ * subspace-0 region with lower_coord[0] <= h <= upper_coord[0]: its first
+ * replica's virtual server (replicas[0].vsi), or virtual_server_id() == 0 when
+ * the region has no replicas (:446-449).  No region: the reference abort()s
+ * (:453); here *aborted = 1 and the result is 0. */
+uint64_t hdxo_point_leader(uint32_t key_type, const uint8_t* key, size_t len, uint32_t R,
+                           const uint64_t* lower0, const uint64_t* upper0, const uint64_t* leader_vsi,
+                           const uint8_t* has_replicas, int* aborted) {
+    int err = 0;
+    const uint64_t h = hdxo_hash_value(key_type, key, len, &err);
+    *aborted = 0;
+    for (uint32_t pl = 0; pl < R; ++pl) {
+        if (lower0[pl] <= h && h <= upper0[pl]) return has_replicas[pl] ? leader_vsi[pl] : 0;
+    }
+    *aborted = 1;
+    return 0;
+}
+
 /* ---- stored objects (daemon/datalayer_encodings.cc:139-217) ------------ */
 
 static uint64_t be64(const uint8_t* p) {

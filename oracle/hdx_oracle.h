@@ -57,6 +57,9 @@ uint64_t hdxo_partition(uint32_t num_attrs, uint32_t num_servers, uint64_t* lowe
  * table matches object i when lower[r*D+a] <= coords[i*A+attrs[a]] <=
  * upper[r*D+a] for every a < D; the first match's id is written, 0
  * (region_id()) when none matches. */
+uint64_t hdxo_point_leader(uint32_t key_type, const uint8_t* key, size_t len, uint32_t R,
+                           const uint64_t* lower0, const uint64_t* upper0, const uint64_t* leader_vsi,
+                           const uint8_t* has_replicas, int* aborted);
 void hdxo_lookup_region(uint32_t D, uint32_t R, const uint16_t* attrs, const uint64_t* lower,
                         const uint64_t* upper, const uint64_t* ids, const uint64_t* coords,
                         uint32_t A, uint64_t n, uint64_t* out);

@@ -43,6 +43,8 @@ def lib():
         L.hdxo_partition.restype = u64
         L.hdxo_lookup_region.argtypes = [u32, u32, vp, vp, vp, vp, vp, u32, u64, vp]
         L.hdxo_lookup_region.restype = None
+        L.hdxo_point_leader.argtypes = [u32, vp, ctypes.c_size_t, u32, vp, vp, vp, vp, ctypes.POINTER(ctypes.c_int)]
+        L.hdxo_point_leader.restype = u64
         L.hdxo_hash_encoded.argtypes = [vp, u32, vp, vp, vp, vp, vp, vp, u64, vp, vp, vp]
         L.hdxo_index_encode.restype = sz
         L.hdxo_index_encode.argtypes = [u32, vp, sz, vp, ctypes.POINTER(ctypes.c_int)]
@@ -125,6 +127,26 @@ def lookup_region(attrs, lower, upper, ids, coords):
                              upper.ctypes.data, ids.ctypes.data, coords.ctypes.data, A, n,
                              out.ctypes.data)
     return out
+
+
+def point_leader(key_type, keys, lower0, upper0, leader_vsi, has_replicas):
+    """configuration::point_leader (configuration.cc:427-458) for every key of
+    `keys` (a list of bytes): (leaders u64 array, aborted bool array — where
+    the reference abort()s because no subspace-0 region holds the key)."""
+    lower0 = np.ascontiguousarray(lower0, np.uint64).reshape(-1)
+    upper0 = np.ascontiguousarray(upper0, np.uint64).reshape(-1)
+    vsi = np.ascontiguousarray(leader_vsi, np.uint64)
+    rep = np.ascontiguousarray(has_replicas, np.uint8)
+    R = len(vsi)
+    out = np.zeros(len(keys), np.uint64)
+    aborted = np.zeros(len(keys), bool)
+    flag = ctypes.c_int(0)
+    for i, k in enumerate(keys):
+        buf = ctypes.create_string_buffer(bytes(k), max(len(k), 1))
+        out[i] = lib().hdxo_point_leader(key_type, buf, len(k), R, lower0.ctypes.data, upper0.ctypes.data,
+                                         vsi.ctypes.data, rep.ctypes.data, ctypes.byref(flag))
+        aborted[i] = flag.value != 0
+    return out, aborted
 
 
 def hash_encoded(types, keys, key_off, key_len, vals, val_off, val_len):

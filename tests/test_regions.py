@@ -367,3 +367,88 @@ def test_gpu_tables_used_on_another_device_get_a_replica(oracle):
     torch.cuda.synchronize()
     assert np.array_equal(got3.cpu().numpy().view(np.uint64), want)
     t.close()
+
+
+def _pack_keys(keys, dev):
+    import torch
+    lens = np.array([len(k) for k in keys], np.uint32)
+    base = np.zeros(len(keys), np.uint64)
+    base[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    blob = np.frombuffer(b"".join(keys) + b"\0" * 64, np.uint8)
+    return (torch.from_numpy(blob.copy()).to(dev), torch.from_numpy(base.view(np.int64)).to(dev),
+            torch.from_numpy(lens.view(np.int32)).to(dev))
+
+
+def test_point_leader_oracle_semantics(oracle):
+    """configuration.cc:440-454: first subspace-0 region, replicas[0].vsi,
+    0 without replicas, abort without a region (the oracle flags it)."""
+    h = [oracle.cityhash64(k) for k in (b"a", b"b", b"c")]
+    lo = np.array([0, 0], np.uint64)
+    up = np.array([U64MAX, U64MAX], np.uint64)
+    got, ab = oracle.point_leader(9217, [b"a", b"b"], lo, up, [11, 12], [1, 1])
+    assert list(got) == [11, 11] and not ab.any()  # the first region wins
+    got, ab = oracle.point_leader(9217, [b"a"], lo, up, [11, 12], [0, 1])
+    assert list(got) == [0] and not ab.any()  # no replicas: virtual_server_id()
+    lo1 = np.array([h[0]], np.uint64)
+    got, ab = oracle.point_leader(9217, [b"a", b"b", b"c"], lo1, lo1, [5], [1])
+    assert got[0] == 5 and not ab[0] and (ab[1:] == [h[1] != h[0], h[2] != h[0]]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("key_type", [9217, 9218])
+def test_gpu_point_leaders_match_oracle(oracle, key_type):
+    """PointLeaders (one fused launch, two tables) == the oracle's restatement
+    of point_leader for keys hitting every subspace-0 region of a 64-server
+    key subspace, with a tenth of the regions replica-less (VERDICT r5 #6)."""
+    import torch
+
+    from hyperdex_amd import regions
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(key_type)
+    if key_type == 9217:
+        keys = [rng.integers(0, 256, int(rng.integers(0, 100)), dtype=np.uint8).tobytes() for _ in range(20000)]
+    else:  # int64 keys spread over the whole ordered-encoding line
+        keys = [int(x).to_bytes(8, "little", signed=True)
+                for x in rng.integers(-2**63, 2**63 - 1, 20000, dtype=np.int64)]
+    lo, up = oracle.partition(1, 64)
+    vsi = rng.integers(1, 2**63, 64, dtype=np.uint64)
+    has = rng.random(64) > 0.1
+    pl = regions.PointLeaders(lo[:, 0], up[:, 0], vsi, has)
+    try:
+        leader, where = pl.leaders(key_type, *_pack_keys(keys, dev))
+        torch.cuda.synchronize()
+        want, aborted = oracle.point_leader(key_type, keys, lo[:, 0], up[:, 0], vsi, has)
+        assert not aborted.any()
+        assert np.array_equal(leader.cpu().numpy().view(np.uint64), want)
+        assert len(np.unique(where.cpu().numpy())) == 64  # every region is hit
+        assert (want == 0).sum() > 0  # replica-less regions answer virtual_server_id()
+    finally:
+        pl.close()
+
+
+@pytest.mark.gpu
+def test_gpu_point_leader_abort_is_reported(oracle):
+    """A subspace-0 table with a hole: the keys in it are where the reference
+    abort()s; PointLeaders raises, and without the check flags them 0."""
+    import torch
+
+    from hyperdex_amd import regions
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(7)
+    keys = [rng.integers(0, 256, 24, dtype=np.uint8).tobytes() for _ in range(4000)]
+    lo, up = oracle.partition(1, 16)
+    keep = np.arange(16) != 5
+    vsi = np.arange(100, 116, dtype=np.uint64)
+    pl = regions.PointLeaders(lo[keep, 0], up[keep, 0], vsi[keep], np.ones(15, bool))
+    try:
+        packed = _pack_keys(keys, dev)
+        with pytest.raises(regions.PointLeaderAbort):
+            pl.leaders(9217, *packed)
+        leader, where = pl.leaders(9217, *packed, check=False)
+        torch.cuda.synchronize()
+        want, aborted = oracle.point_leader(9217, keys, lo[keep, 0], up[keep, 0], vsi[keep], np.ones(15, bool))
+        assert aborted.any()
+        assert np.array_equal(where.cpu().numpy() == 0, aborted)
+        assert np.array_equal(leader.cpu().numpy().view(np.uint64), want)
+    finally:
+        pl.close()
