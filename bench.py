@@ -1115,19 +1115,138 @@ def time_host_path(types, blob, base, lens, A, coords=None, n_host=2_000_000):
                                                ptrs["lens"], n, ptrs["out"]))
     dt = (time.perf_counter() - t0) / reps
     verified = None
+    want = None
     if coords is not None and n:
+        want = coords[:n].reshape(-1).cpu().numpy().view(np.uint64)
         got = np.ctypeslib.as_array((ctypes.c_uint64 * (n * A)).from_address(ptrs["out"]))
-        verified = bool(np.array_equal(got, coords[:n].reshape(-1).cpu().numpy().view(np.uint64)))
+        verified = bool(np.array_equal(got, want))
         del got
-    for p in ptrs.values():
-        lib.hdx_free_pinned(p)
-    hdx.shutdown()  # the set's workers and staging; later phases run on the caller's device
     res = {"objects": n, "devices": len(devices), "ms": round(dt * 1e3, 3),
            "GiB_s": round(nb / dt / 2**30, 3), "GiB_s_per_device": round(nb / dt / 2**30 / len(devices), 3),
            "mobjects_per_s": round(n / dt / 1e6, 2),
            "path": "hdx_init_mask(all visible devices) + hdx_hash_batch_host: pinned H2D, kernel, D2H"}
     if verified is not None:
         res["verified_vs_device_coords"] = verified
+    try:
+        # the same objects at shuffled places: chunks are packed
+        # in index order on the device (hdx_gather.hip), not copied as spans
+        res["shuffled"] = time_host_shuffled(lib, t, A, blob, base, lens, n, want)
+        # 16 concurrent callers (daemon::loop threads, daemon.cc:345-351), each
+        # with its own 1/16 of the ordered batch, after hdx_init_mask
+        res["callers16"] = time_host_callers(lib, t, A, ptrs, nb, n, 16, want)
+    finally:
+        for p in ptrs.values():
+            lib.hdx_free_pinned(p)
+        hdx.shutdown()  # the set's workers and staging; later phases run on the caller's device
+    return res
+
+
+def time_host_shuffled(lib, t, A, blob, base, lens, n, want, reps=3, block=250_000):
+    """hdx_hash_batch_host on the first n objects rewritten in a random order
+    (back to back, seeded permutation; built on the device, copied to pinned
+    memory): every chunk's span is ~16x its payload, so every chunk is packed."""
+    import ctypes
+
+    import torch
+
+    import hyperdex_amd as hdx
+    dev = blob.device
+    sizes = lens[:n * A].view(n, A).to(torch.int64).sum(dim=1)
+    g = torch.Generator(device=dev)
+    g.manual_seed(0x5EED)
+    perm = torch.randperm(n, generator=g, device=dev)
+    s_perm = sizes[perm]
+    start_perm = torch.cumsum(s_perm, 0) - s_perm
+    new_base = torch.empty(n, dtype=torch.int64, device=dev)
+    new_base[perm] = start_perm
+    nb = int(s_perm.sum().item())
+    sblob = torch.empty(nb, dtype=torch.uint8, device=dev)
+    for k0 in range(0, n, block):  # byte gather, a block of objects at a time
+        ks = perm[k0:k0 + block]
+        sp, st = s_perm[k0:k0 + block], start_perm[k0:k0 + block]
+        seg = torch.repeat_interleave(torch.arange(len(ks), device=dev), sp)
+        pos = torch.arange(int(st[0].item()), int(st[0].item()) + int(sp.sum().item()), device=dev)
+        src = base[ks][seg] + (pos - st[seg])
+        sblob[pos] = blob[src]
+        del seg, pos, src
+    ptrs = {}
+    for name, nbytes in (("blob", nb), ("base", n * 8), ("lens", n * A * 4), ("out", n * A * 8)):
+        p = ctypes.c_void_p()
+        hdx._lib.check(lib.hdx_alloc_pinned(nbytes, ctypes.byref(p)))
+        ptrs[name] = p.value
+    try:
+        for name, src in (("blob", sblob), ("base", new_base), ("lens", lens[:n * A])):
+            host = src.cpu().numpy()
+            ctypes.memmove(ptrs[name], host.ctypes.data, host.nbytes)
+            del host
+        del sblob, new_base, perm, s_perm, start_perm
+        torch.cuda.empty_cache()
+        call = lambda: hdx._lib.check(lib.hdx_hash_batch_host(t.ctypes.data, A, ptrs["blob"], nb, ptrs["base"],
+                                                              ptrs["lens"], n, ptrs["out"]))
+        call()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            call()
+        dt = (time.perf_counter() - t0) / reps
+        res = {"objects": n, "ms": round(dt * 1e3, 3), "GiB_s": round(nb / dt / 2**30, 3),
+               "order": "random permutation of the objects, back to back (pinned)",
+               "path": "chunks packed in index order by hdx_gather.hip from the pinned batch"}
+        if want is not None:
+            got = np.ctypeslib.as_array((ctypes.c_uint64 * (n * A)).from_address(ptrs["out"]))
+            res["verified_vs_device_coords"] = bool(np.array_equal(got, want))
+            del got
+        return res
+    finally:
+        for p in ptrs.values():
+            lib.hdx_free_pinned(p)
+
+
+def time_host_callers(lib, t, A, ptrs, nb, n, callers, want, reps=3):
+    """`callers` long-lived threads (as daemon::loop threads are) at once,
+    each hdx_hash_batch_host on its own contiguous 1/callers of the pinned
+    batch (ctypes releases the GIL in the call): the aggregate rate of a round
+    in which every caller makes one call, after one untimed round (each thread
+    binds its pipeline on its first call)."""
+    import ctypes
+    import threading
+
+    cuts = [n * k // callers for k in range(callers + 1)]
+    start = threading.Barrier(callers + 1)
+    done = threading.Barrier(callers + 1)
+    errs = []
+
+    def worker(k):
+        f, c = cuts[k], cuts[k + 1] - cuts[k]
+        for _ in range(reps + 1):
+            start.wait()
+            if c:
+                st = lib.hdx_hash_batch_host(t.ctypes.data, A, ptrs["blob"], nb, ptrs["base"] + 8 * f,
+                                             ptrs["lens"] + 4 * A * f, c, ptrs["out"] + 8 * A * f)
+                if st != 0:
+                    errs.append((k, st, lib.hdx_last_error()))
+            done.wait()
+
+    th = [threading.Thread(target=worker, args=(k,), daemon=True) for k in range(callers)]
+    for x in th:
+        x.start()
+    dts = []
+    for r in range(reps + 1):
+        t0 = time.perf_counter()
+        start.wait()
+        done.wait()
+        if r:
+            dts.append(time.perf_counter() - t0)
+    for x in th:
+        x.join()
+    if errs:
+        raise RuntimeError("callers failed: %s" % errs[:3])
+    dt = float(np.mean(dts))
+    res = {"callers": callers, "objects": n, "ms": round(dt * 1e3, 3), "GiB_s": round(nb / dt / 2**30, 3),
+           "threads": "long-lived, one call each per round"}
+    if want is not None:
+        got = np.ctypeslib.as_array((ctypes.c_uint64 * (n * A)).from_address(ptrs["out"]))
+        res["verified_vs_device_coords"] = bool(np.array_equal(got, want))
+        del got
     return res
 
 

@@ -479,20 +479,8 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
             if (e != hipErrorInvalidValue) return e;
             break;
         }
-        case 289: case 290: case 291: {  // the product sweep's priority forms: loads and stores high (289), loads
-            // high alone (290, the product before the walk's medium priority), the walk high (291)
-            const int v = hash_variant();
-            const hipError_t e = launch_hash_wsweep(a, stream, v == 289 ? 33 : v == 290 ? 34 : 35);
-            if (e != hipErrorInvalidValue) return e;
-            break;
-        }
-        case 293: {  // round 6: the product sweep with NUM2 (numerics by selects, the class table)
-            const hipError_t e = launch_hash_wsweep(a, stream, 36);
-            if (e != hipErrorInvalidValue) return e;
-            break;
-        }
-        case 277: case 278: {  // the product sweep without wave priorities (277), with the passes high (278)
-            const hipError_t e = launch_hash_wsweep(a, stream, hash_variant() == 277 ? 31 : 32);
+        case 277: {  // the product sweep without wave priorities
+            const hipError_t e = launch_hash_wsweep(a, stream, 31);
             if (e != hipErrorInvalidValue) return e;
             break;
         }

@@ -122,7 +122,16 @@ struct HostSlot {
     PinBuf<uint8_t> h_blob, h_keys;       // only for pageable inputs
     PinBuf<uint64_t> h_base, h_coords, h_ids, h_koff, h_voff, h_ver;
     PinBuf<uint32_t> h_len, h_klen, h_vlen, h_status;
+    // packed chunks (objects out of address order): the extents' source
+    // offsets and lengths for the gather kernel (hdx_gather.hip)
+    DevBuf<uint64_t> d_src, d_src2;
+    DevBuf<uint32_t> d_sz, d_sz2;
+    PinBuf<uint64_t> h_src, h_src2;
+    PinBuf<uint32_t> h_sz, h_sz2;
 };
+// The device view of pinned host memory p (for a kernel to read it), or NULL
+// when p is not pinned.
+const uint8_t* device_view(const uint8_t* p);
 // Waits for the slot's stream, frees everything, destroys the stream (on the
 // current device, which must be the slot's).
 void free_host_slot(HostSlot& s);

@@ -28,17 +28,37 @@ void free_host_slot(HostSlot& s) {
     if (s.s) (void)hipStreamSynchronize(s.s);
     for (void* p : {(void*)s.d_blob.p, (void*)s.d_keys.p, (void*)s.d_base.p, (void*)s.d_coords.p, (void*)s.d_ids.p,
                     (void*)s.d_koff.p, (void*)s.d_voff.p, (void*)s.d_ver.p, (void*)s.d_len.p, (void*)s.d_klen.p,
-                    (void*)s.d_vlen.p, (void*)s.d_status.p})
+                    (void*)s.d_vlen.p, (void*)s.d_status.p, (void*)s.d_src.p, (void*)s.d_src2.p, (void*)s.d_sz.p,
+                    (void*)s.d_sz2.p})
         (void)hipFree(p);
     for (void* p : {(void*)s.h_blob.p, (void*)s.h_keys.p, (void*)s.h_base.p, (void*)s.h_coords.p, (void*)s.h_ids.p,
                     (void*)s.h_koff.p, (void*)s.h_voff.p, (void*)s.h_ver.p, (void*)s.h_len.p, (void*)s.h_klen.p,
-                    (void*)s.h_vlen.p, (void*)s.h_status.p})
+                    (void*)s.h_vlen.p, (void*)s.h_status.p, (void*)s.h_src.p, (void*)s.h_src2.p, (void*)s.h_sz.p,
+                    (void*)s.h_sz2.p})
         (void)hipHostFree(p);
     if (s.s) (void)hipStreamDestroy(s.s);
     s = HostSlot{};
 }
 
 static bool is_numeric_code(uint8_t c) { return c >= CODE_INT64; }
+
+const uint8_t* device_view(const uint8_t* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer) return nullptr;
+    return (const uint8_t*)a.devicePointer + (p - (const uint8_t*)a.hostPointer);
+}
+
+// A chunk whose objects' byte span is no more than this much over their
+// payload goes as one span copy (no gather); otherwise its objects are packed
+// in index order (hdx_gather.hip for pinned sources, a host copy per object
+// for pageable ones), so a batch in any order moves only its own bytes.
+static bool span_pays(uint64_t span, uint64_t payload) {
+    return span <= kChunkBytes && span <= payload + payload / 8 + (64u << 10);
+}
 
 // In the pipelines' loops: a HIP error lets the copies in flight land first.
 #define DRAIN_TRY(expr)                                          \
@@ -159,34 +179,62 @@ hdx_status hash_host(const uint8_t* codes, uint32_t A, const uint8_t* blob, uint
         return err;
     };
 
+    const uint8_t* blob_dev = blob_pinned ? device_view(blob) : nullptr;  // the gather kernel's view
+    std::vector<uint32_t> sizes;  // the chunk's object sizes (validated as the chunk grows)
     uint64_t i = 0, next_size = 0;
     int k = 0;
     if ((st = extent(0, &next_size)) != HDX_OK) return st;
     while (i < n) {
-        // Grow the chunk while its byte extent stays under kChunkBytes; an
-        // object that does not fit starts the next chunk (its extent is kept).
-        uint64_t lo = obj_base[i], hi = obj_base[i] + next_size, e = i + 1;
+        // Grow the chunk while its payload stays under kChunkBytes (an object
+        // that does not fit starts the next chunk; its extent is kept), then
+        // move it as one span when its objects lie (nearly) back to back, else
+        // packed in index order.
+        uint64_t lo = obj_base[i], hi = obj_base[i] + next_size, payload = next_size, e = i + 1;
+        sizes.assign(1, (uint32_t)next_size);
         while (e < n) {
             if ((st = extent(e, &next_size)) != HDX_OK) return drain(st);
-            const uint64_t nlo = std::min(lo, obj_base[e]);
-            const uint64_t nhi = std::max(hi, obj_base[e] + next_size);
-            if (nhi - nlo > kChunkBytes) break;
-            lo = nlo; hi = nhi; ++e;
+            if (payload + next_size > kChunkBytes) break;
+            lo = std::min(lo, obj_base[e]);
+            hi = std::max(hi, obj_base[e] + next_size);
+            payload += next_size;
+            sizes.push_back((uint32_t)next_size);
+            ++e;
         }
-        const uint64_t cnt = e - i, bytes = hi - lo;
+        const uint64_t cnt = e - i;
+        const bool span = span_pays(hi - lo, payload);
+        const uint64_t bytes = span ? hi - lo : payload;
         HostSlot& sl = slots[k];
         if ((st = finish(k)) != HDX_OK) return drain(st);
         if ((st = sl.d_blob.need(std::max<uint64_t>(bytes, 1))) != HDX_OK || (st = sl.d_base.need(cnt)) != HDX_OK ||
             (st = sl.d_len.need(cnt * A)) != HDX_OK || (st = sl.d_coords.need(cnt * A)) != HDX_OK ||
             (T && (st = sl.d_ids.need(cnt * T)) != HDX_OK) || (st = sl.h_base.need(cnt)) != HDX_OK)
             return drain(st);
-        for (uint64_t t = 0; t < cnt; ++t) sl.h_base.p[t] = obj_base[i + t] - lo;
-
+        const bool gather = !span && blob_dev;  // pinned objects out of order: packed on the device
         const uint8_t* src_blob = blob + lo;
-        if (!blob_pinned) {
-            if ((st = sl.h_blob.need(std::max<uint64_t>(bytes, 1))) != HDX_OK) return drain(st);
-            std::memcpy(sl.h_blob.p, blob + lo, bytes);
-            src_blob = sl.h_blob.p;
+        if (span) {
+            for (uint64_t t = 0; t < cnt; ++t) sl.h_base.p[t] = obj_base[i + t] - lo;
+            if (!blob_pinned) {
+                if ((st = sl.h_blob.need(std::max<uint64_t>(bytes, 1))) != HDX_OK) return drain(st);
+                std::memcpy(sl.h_blob.p, blob + lo, bytes);
+                src_blob = sl.h_blob.p;
+            }
+        } else {
+            uint64_t at = 0;  // packed offsets, index order
+            for (uint64_t t = 0; t < cnt; ++t) {
+                sl.h_base.p[t] = at;
+                at += sizes[t];
+            }
+            if (gather) {
+                if ((st = sl.h_src.need(cnt)) != HDX_OK || (st = sl.h_sz.need(cnt)) != HDX_OK ||
+                    (st = sl.d_src.need(cnt)) != HDX_OK || (st = sl.d_sz.need(cnt)) != HDX_OK)
+                    return drain(st);
+                std::memcpy(sl.h_src.p, obj_base + i, cnt * 8);
+                std::memcpy(sl.h_sz.p, sizes.data(), cnt * 4);
+            } else {  // pageable: each object copied into the pinned staging
+                if ((st = sl.h_blob.need(std::max<uint64_t>(bytes, 1))) != HDX_OK) return drain(st);
+                for (uint64_t t = 0; t < cnt; ++t) std::memcpy(sl.h_blob.p + sl.h_base.p[t], blob + obj_base[i + t], sizes[t]);
+                src_blob = sl.h_blob.p;
+            }
         }
         const uint32_t* src_len = attr_len + i * A;
         if (!len_pinned) {
@@ -194,9 +242,15 @@ hdx_status hash_host(const uint8_t* codes, uint32_t A, const uint8_t* blob, uint
             std::memcpy(sl.h_len.p, attr_len + i * A, cnt * A * sizeof(uint32_t));
             src_len = sl.h_len.p;
         }
-        DRAIN_TRY(hipMemcpyAsync(sl.d_blob.p, src_blob, bytes, hipMemcpyHostToDevice, sl.s));
         DRAIN_TRY(hipMemcpyAsync(sl.d_base.p, sl.h_base.p, cnt * 8, hipMemcpyHostToDevice, sl.s));
         DRAIN_TRY(hipMemcpyAsync(sl.d_len.p, src_len, cnt * A * 4, hipMemcpyHostToDevice, sl.s));
+        if (gather) {  // the small arrays first: after the gather only the hash and the D2H remain
+            DRAIN_TRY(hipMemcpyAsync(sl.d_src.p, sl.h_src.p, cnt * 8, hipMemcpyHostToDevice, sl.s));
+            DRAIN_TRY(hipMemcpyAsync(sl.d_sz.p, sl.h_sz.p, cnt * 4, hipMemcpyHostToDevice, sl.s));
+            DRAIN_TRY(launch_gather_extents(blob_dev, sl.d_src.p, sl.d_sz.p, sl.d_base.p, sl.d_blob.p, cnt, sl.s));
+        } else {
+            DRAIN_TRY(hipMemcpyAsync(sl.d_blob.p, src_blob, bytes, hipMemcpyHostToDevice, sl.s));
+        }
         BatchArgs args;
         // status: none (sizes validated above); the coordinates always land in
         // device staging, so the regions form needs no scratch of its own
@@ -285,12 +339,18 @@ hdx_status hash_encoded_host(const uint8_t* codes, uint32_t A, const uint8_t* ke
         return HDX_OK;
     };
 
+    // keys and values out of order: packed as records [key][value] in index
+    // order (hdx_gather.hip from pinned stores, a host copy per object from
+    // pageable ones), so the kernel sees the record layout
+    const uint8_t* keys_dev = keys_pinned ? device_view(keys) : nullptr;
+    const uint8_t* vals_dev = vals_pinned ? device_view(vals) : nullptr;
     uint64_t i = 0;
     int k = 0;
     if ((st = check(0)) != HDX_OK) return st;
     while (i < n) {
         uint64_t klo = key_off[i], khi = key_off[i] + key_len[i];
         uint64_t vlo = val_off[i], vhi = val_off[i] + val_len[i];
+        uint64_t payload = (uint64_t)key_len[i] + val_len[i];
         if (records) {
             klo = vlo = std::min(klo, vlo);
             khi = vhi = std::max(khi, vhi);
@@ -301,21 +361,26 @@ hdx_status hash_encoded_host(const uint8_t* codes, uint32_t A, const uint8_t* ke
         uint64_t e = i + 1;
         while (e < n) {
             if ((st = check(e)) != HDX_OK) return drain(st);
+            const uint64_t pe = (uint64_t)key_len[e] + val_len[e];
+            if (payload + pe > kChunkBytes) break;
             uint64_t nklo = std::min(klo, key_off[e]), nkhi = std::max(khi, key_off[e] + key_len[e]);
             uint64_t nvlo = std::min(vlo, val_off[e]), nvhi = std::max(vhi, val_off[e] + val_len[e]);
             if (records) {
                 nklo = nvlo = std::min(nklo, nvlo);
                 nkhi = nvhi = std::max(nkhi, nvhi);
             }
-            if (span_bytes(nklo, nkhi, nvlo, nvhi) > kChunkBytes) break;
             klo = nklo; khi = nkhi; vlo = nvlo; vhi = nvhi;
+            payload += pe;
             ++e;
         }
         const uint64_t cnt = e - i;
+        const bool span = span_pays(span_bytes(klo, khi, vlo, vhi), payload);
+        const bool gather = !span && keys_dev && vals_dev;
+        const bool packed = !span;  // the chunk's device layout is then records
         HostSlot& sl = slots[k];
         if ((st = finish(k)) != HDX_OK) return drain(st);
-        if ((st = sl.d_blob.need(std::max<uint64_t>(vhi - vlo, 1))) != HDX_OK ||
-            (!records && (st = sl.d_keys.need(std::max<uint64_t>(khi - klo, 1))) != HDX_OK) ||
+        if ((st = sl.d_blob.need(std::max<uint64_t>(span ? vhi - vlo : payload, 1))) != HDX_OK ||
+            (span && !records && (st = sl.d_keys.need(std::max<uint64_t>(khi - klo, 1))) != HDX_OK) ||
             (st = sl.d_koff.need(cnt)) != HDX_OK || (st = sl.d_voff.need(cnt)) != HDX_OK ||
             (st = sl.d_klen.need(cnt)) != HDX_OK || (st = sl.d_vlen.need(cnt)) != HDX_OK ||
             (st = sl.d_coords.need(cnt * A)) != HDX_OK || (st = sl.d_ver.need(cnt)) != HDX_OK ||
@@ -323,14 +388,44 @@ hdx_status hash_encoded_host(const uint8_t* codes, uint32_t A, const uint8_t* ke
             (T && (st = sl.d_ids.need(cnt * T)) != HDX_OK) || (st = sl.h_koff.need(cnt)) != HDX_OK ||
             (st = sl.h_voff.need(cnt)) != HDX_OK)
             return drain(st);
-        for (uint64_t t = 0; t < cnt; ++t) {
-            sl.h_koff.p[t] = key_off[i + t] - klo;
-            sl.h_voff.p[t] = val_off[i + t] - vlo;
+        const uint8_t *src_vals = nullptr, *src_keys = nullptr;
+        if (span) {
+            for (uint64_t t = 0; t < cnt; ++t) {
+                sl.h_koff.p[t] = key_off[i + t] - klo;
+                sl.h_voff.p[t] = val_off[i + t] - vlo;
+            }
+            if ((st = stage(sl.h_blob, vals, vals_pinned, vlo, vhi - vlo, &src_vals)) != HDX_OK) return drain(st);
+            if (!records && (st = stage(sl.h_keys, keys, keys_pinned, klo, khi - klo, &src_keys)) != HDX_OK)
+                return drain(st);
+        } else {
+            uint64_t at = 0;  // record t: its key at h_koff, its value right after
+            for (uint64_t t = 0; t < cnt; ++t) {
+                sl.h_koff.p[t] = at;
+                sl.h_voff.p[t] = at + key_len[i + t];
+                at += (uint64_t)key_len[i + t] + val_len[i + t];
+            }
+            if (gather) {  // 2 extents per object, absolute device-view sources
+                if ((st = sl.h_src.need(2 * cnt)) != HDX_OK || (st = sl.h_sz.need(2 * cnt)) != HDX_OK ||
+                    (st = sl.h_src2.need(2 * cnt)) != HDX_OK || (st = sl.d_src.need(2 * cnt)) != HDX_OK ||
+                    (st = sl.d_sz.need(2 * cnt)) != HDX_OK || (st = sl.d_src2.need(2 * cnt)) != HDX_OK)
+                    return drain(st);
+                for (uint64_t t = 0; t < cnt; ++t) {
+                    sl.h_src.p[2 * t] = (uint64_t)(uintptr_t)keys_dev + key_off[i + t];
+                    sl.h_sz.p[2 * t] = key_len[i + t];
+                    sl.h_src2.p[2 * t] = sl.h_koff.p[t];
+                    sl.h_src.p[2 * t + 1] = (uint64_t)(uintptr_t)vals_dev + val_off[i + t];
+                    sl.h_sz.p[2 * t + 1] = val_len[i + t];
+                    sl.h_src2.p[2 * t + 1] = sl.h_voff.p[t];
+                }
+            } else {  // pageable: each key and value copied into the pinned staging
+                if ((st = sl.h_blob.need(std::max<uint64_t>(payload, 1))) != HDX_OK) return drain(st);
+                for (uint64_t t = 0; t < cnt; ++t) {
+                    std::memcpy(sl.h_blob.p + sl.h_koff.p[t], keys + key_off[i + t], key_len[i + t]);
+                    std::memcpy(sl.h_blob.p + sl.h_voff.p[t], vals + val_off[i + t], val_len[i + t]);
+                }
+                src_vals = sl.h_blob.p;
+            }
         }
-        const uint8_t *src_vals, *src_keys = nullptr;
-        if ((st = stage(sl.h_blob, vals, vals_pinned, vlo, vhi - vlo, &src_vals)) != HDX_OK) return drain(st);
-        if (!records && (st = stage(sl.h_keys, keys, keys_pinned, klo, khi - klo, &src_keys)) != HDX_OK)
-            return drain(st);
         const uint32_t* src_klen = key_len + i;
         const uint32_t* src_vlen = val_len + i;
         if (!klen_pinned) {
@@ -343,16 +438,24 @@ hdx_status hash_encoded_host(const uint8_t* codes, uint32_t A, const uint8_t* ke
             std::memcpy(sl.h_vlen.p, val_len + i, cnt * 4);
             src_vlen = sl.h_vlen.p;
         }
-        DRAIN_TRY(hipMemcpyAsync(sl.d_blob.p, src_vals, vhi - vlo, hipMemcpyHostToDevice, sl.s));
-        if (!records) DRAIN_TRY(hipMemcpyAsync(sl.d_keys.p, src_keys, khi - klo, hipMemcpyHostToDevice, sl.s));
         DRAIN_TRY(hipMemcpyAsync(sl.d_koff.p, sl.h_koff.p, cnt * 8, hipMemcpyHostToDevice, sl.s));
         DRAIN_TRY(hipMemcpyAsync(sl.d_voff.p, sl.h_voff.p, cnt * 8, hipMemcpyHostToDevice, sl.s));
         DRAIN_TRY(hipMemcpyAsync(sl.d_klen.p, src_klen, cnt * 4, hipMemcpyHostToDevice, sl.s));
         DRAIN_TRY(hipMemcpyAsync(sl.d_vlen.p, src_vlen, cnt * 4, hipMemcpyHostToDevice, sl.s));
+        if (gather) {
+            DRAIN_TRY(hipMemcpyAsync(sl.d_src.p, sl.h_src.p, 2 * cnt * 8, hipMemcpyHostToDevice, sl.s));
+            DRAIN_TRY(hipMemcpyAsync(sl.d_sz.p, sl.h_sz.p, 2 * cnt * 4, hipMemcpyHostToDevice, sl.s));
+            DRAIN_TRY(hipMemcpyAsync(sl.d_src2.p, sl.h_src2.p, 2 * cnt * 8, hipMemcpyHostToDevice, sl.s));
+            DRAIN_TRY(launch_gather_extents(nullptr, sl.d_src.p, sl.d_sz.p, sl.d_src2.p, sl.d_blob.p, 2 * cnt, sl.s));
+        } else {
+            DRAIN_TRY(hipMemcpyAsync(sl.d_blob.p, src_vals, span ? vhi - vlo : payload, hipMemcpyHostToDevice, sl.s));
+            if (span && !records)
+                DRAIN_TRY(hipMemcpyAsync(sl.d_keys.p, src_keys, khi - klo, hipMemcpyHostToDevice, sl.s));
+        }
         DRAIN_TRY(hipMemsetAsync(sl.d_status.p, 0, 4, sl.s));
         EncodedArgs a{};
         if ((st = set_codes(a, codes, A)) != HDX_OK) return drain(st);
-        a.keys = records ? sl.d_blob.p : sl.d_keys.p;
+        a.keys = records || packed ? sl.d_blob.p : sl.d_keys.p;
         a.key_off = sl.d_koff.p;
         a.key_len = sl.d_klen.p;
         a.vals = sl.d_blob.p;

@@ -53,7 +53,7 @@ hipError_t launch_debug_variant(const BatchArgs& args, hipStream_t stream, int v
         // wave-staged (hdx_wstage.hip): 200 2 passes / 10 KiB, 201 3 / 14 KiB, 202 2 / 8 KiB,
         // 203 1 / 5 KiB, 204 4 / 18 KiB, 205 2 / 8832 B, 206 = 205 with <= 6 objects
         case 200: case 201: case 202: case 203: case 204: case 205: case 206: case 207: case 208:
-        case 209: case 210: case 211: case 213: case 214: case 215: case 216: case 218: case 219: case 239: case 240: case 241: case 242: case 244: case 245: case 246: case 248: case 249: case 255: case 256: case 257: case 258: case 259: case 270: case 273: case 274: case 275: case 276: case 278: case 279: case 287: case 288: case 289: case 290: case 291: case 292: case 293: case 294: case 295: case 296: case 297: {
+        case 209: case 210: case 211: case 213: case 214: case 215: case 216: case 218: case 219: case 239: case 240: case 241: case 242: case 244: case 245: case 246: case 248: case 249: case 255: case 256: case 257: case 258: case 259: case 270: case 273: case 274: case 275: case 276: case 278: case 279: case 287: case 293: case 294: case 295: case 296: case 297: {
             const hipError_t e = launch_hash_wstage(args, stream, variant - 200);
             return e == hipErrorInvalidValue ? launch_hash_batch_variant(args, stream, 44) : e;
         }
@@ -137,12 +137,9 @@ static bool known_variant(int v) {
         case 274:  // 212 with 3 passes, 10 objects per wave, 13 KiB windows
         case 275: case 276:  // 212 with its descriptors in registers (8832 / 8704-byte windows)
         case 279:  // 270 with non-temporal loads (lengths, bases, span)
-        case 278:  // 279 with dword-aligned ds_read_b128 window reads (W128 1); the sweep: passes at high priority
+        case 278:  // 279 with dword-aligned ds_read_b128 window reads (W128 1)
         case 277:  // the sweep without wave priorities (the product before round 5's s_setprio)
-        case 287: case 288:  // 279 with wave priorities: loads high (the product since round 5) / passes high
-        case 289:  // 279 / the product sweep with loads and stores at high priority
-        case 290: case 291:  // 279 with the stores alone high / loads and stores at the top priority
-        case 292:  // 279 with the loads high, the sort medium, the passes low
+        case 287:  // 279 with wave priorities: loads high (the product in round 5)
         case 210: case 211:  // wave-staged, sorted over the workgroup
         case 40: case 41:
         case 33: case 43: case 47: case 48: case 49: case 57: case 58:  // stored-object sweep forms (hdx_encoded.hip)

@@ -40,50 +40,68 @@ namespace hdx {
 
 // ---- worker threads ---------------------------------------------------------
 
+// One device's worker threads: a queue served by up to kWorkersPerDevice
+// threads, each with its own pipeline (the per-thread slots of hdx_capi.cpp),
+// spawned when a job arrives and every thread is busy.  Concurrent callers
+// (N daemon::loop threads, daemon/daemon.cc:345-351) that each post a share
+// for this device then run side by side instead of queueing on one thread
+// (VERDICT r5 #5).  A thread releases its scratch as it exits.
+constexpr size_t kWorkersPerDevice = 4;
+
 class Worker {
 public:
-    Worker() : th_([this] { run(); }) {}
+    Worker() = default;
+    Worker(const Worker&) = delete;
+    Worker& operator=(const Worker&) = delete;
     // false once join() has begun: the job will never run
     bool post(std::function<void()> job) {
         {
             std::lock_guard<std::mutex> lk(mu_);
             if (stop_) return false;
             q_.push_back(std::move(job));
+            if (idle_ == 0 && th_.size() < kWorkersPerDevice) th_.emplace_back([this] { run(); });
         }
         cv_.notify_one();
         return true;
     }
     void join() {
+        std::vector<std::thread> th;
         {
             std::lock_guard<std::mutex> lk(mu_);
             stop_ = true;
+            th.swap(th_);
         }
-        cv_.notify_one();
-        if (th_.joinable()) th_.join();
+        cv_.notify_all();
+        for (auto& t : th)
+            if (t.joinable()) t.join();
     }
     // a set dropped without destroy_set (a failed create) still ends its
-    // thread: a joinable std::thread's destructor would std::terminate
+    // threads: a joinable std::thread's destructor would std::terminate
     ~Worker() { join(); }
 
 private:
     void run() {
+        std::unique_lock<std::mutex> lk(mu_);
         for (;;) {
-            std::function<void()> job;
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
-                if (q_.empty()) return;
-                job = std::move(q_.front());
-                q_.pop_front();
-            }
+            ++idle_;
+            cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+            --idle_;
+            if (q_.empty()) break;  // stopping, nothing left
+            std::function<void()> job = std::move(q_.front());
+            q_.pop_front();
+            lk.unlock();
             job();
+            lk.lock();
         }
+        lk.unlock();
+        release_thread_scratch();  // this thread's streams and staging, before hdx_shutdown walks the registry
     }
     std::mutex mu_;
     std::condition_variable cv_;
     std::deque<std::function<void()>> q_;
+    size_t idle_ = 0;
     bool stop_ = false;
-    std::thread th_;  // last: started once the queue exists
+    std::vector<std::thread> th_;
 };
 
 // Waits for `count` posted jobs.
@@ -110,7 +128,7 @@ private:
 struct DeviceSet {
     uint64_t mask = 0;
     std::vector<int> devs;                        // ascending HIP ordinals (debug: any list)
-    std::vector<std::unique_ptr<Worker>> workers;  // one per device: the host path
+    std::vector<std::unique_ptr<Worker>> workers;  // one pool per device: the host path
     std::vector<hipStream_t> streams;             // one per device: device-resident shards
     std::vector<ncclComm_t> comms;                // created on the first gather
     std::mutex call_mu;                           // one device-resident multi call at a time
@@ -161,13 +179,9 @@ static std::unique_ptr<SetRef> acquire_set() {
 
 static void destroy_set(DeviceSet* ds) {
     if (!ds) return;
-    // workers first: each frees its thread's scratch as its last job (not in
-    // a thread-local destructor at exit) before hdx_shutdown walks the
-    // scratch registry
-    for (auto& w : ds->workers) {
-        w->post([] { release_thread_scratch(); });
-        w->join();
-    }
+    // workers first: each thread frees its scratch as it exits (not in a
+    // thread-local destructor) before hdx_shutdown walks the scratch registry
+    for (auto& w : ds->workers) w->join();
     ds->workers.clear();
     for (size_t k = 0; k < ds->comms.size(); ++k) {
         (void)hipSetDevice(ds->devs[k]);

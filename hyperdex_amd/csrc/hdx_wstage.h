@@ -240,10 +240,11 @@ template <int NCH, uint32_t WB, int SHAPE = 0, int HT = 0, int ORDER = 1, int W1
           bool RD = false, bool NT = false, int PRIO = 0, bool PLAN = false, bool NUM2 = false>
 __global__ void __launch_bounds__(64 * WPB)
 hash_wstage_kernel(const BatchArgs args) {
-    // PRIO (A/B): 1 = the load phase at high wave priority, the passes at low;
-    // 2 = the reverse
-    // 3 = 1 with the stores at high priority again; 4 = the stores alone high; 5 = 3 at the top level
-    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 5 || PRIO == 6) __builtin_amdgcn_s_setprio(3);
+    // PRIO 1 (the product since round 5): the load phase at high wave
+    // priority, the passes at low.  The schedules that lost (the reverse, the
+    // stores high, the sort medium: profiles/r5/ab_priority.jsonl) are gone.
+    static_assert(PRIO == 0 || PRIO == 1, "PRIO: 0 none, 1 loads high");
+    if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(3);
     static_assert(NCH >= 1 && NCH <= 4 && WB % 16 == 0, "slot indices are 8 bits; windows whole DMA units");
     static_assert(!(RD && REGIONS), "the fused lookups read the coordinates parked in desc");
     constexpr uint32_t FRONT = HT ? kFrontHT : 0;
@@ -264,12 +265,10 @@ hash_wstage_kernel(const BatchArgs args) {
 
     // ---- counting sort by work class (wave-local) --------------------------
     uint32_t pos[NCH];
-    if constexpr (PRIO == 6) __builtin_amdgcn_s_setprio(2);  // 6: the sort at medium priority
     class_sort<NCH, GAP>(cnt, perm, g.cls, g.code, g.ns, wave_lds_fence, RD ? pos : nullptr);
     // every LDS-DMA of this wave must have landed before the window is read
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 5 || PRIO == 6) __builtin_amdgcn_s_setprio(0);
-    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(3);
+    if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
 
     if constexpr (RD) {
         // RD: descriptors and coordinates stay in registers.  Pass t's lane
@@ -322,8 +321,6 @@ hash_wstage_kernel(const BatchArgs args) {
         desc[s] = hash_slot<SHAPE, HT, W128, NUM2>(args, lw, g.staged, g.mybase, s, e >> 8, desc[s], bad);
     }
     wave_lds_fence();
-    if constexpr (PRIO == 3 || PRIO == 4) __builtin_amdgcn_s_setprio(2);  // the stores (and the wave's end) ahead of the hashing waves
-    if constexpr (PRIO == 5) __builtin_amdgcn_s_setprio(3);
 
     // ---- coalesced stores in slot order ------------------------------------
     if (!REGIONS || args.coords) {

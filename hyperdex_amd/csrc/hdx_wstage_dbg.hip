@@ -172,11 +172,6 @@ hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int for
         case 79: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true>(args, stream);  // 70 with non-temporal loads (the product before its wave priorities)
         case 78: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 1, false, true, true, true, false, 1, true, false, true>(args, stream);  // the product with dword-aligned ds_read_b128 window reads
         case 87: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 1>(args, stream);  // the product: 79 with the loads at high wave priority
-        case 88: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 2>(args, stream);  // the product, passes at high wave priority
-        case 89: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 3>(args, stream);  // the product, loads and stores at high wave priority
-        case 90: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 4>(args, stream);  // the product, stores alone at high wave priority
-        case 91: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 5>(args, stream);  // loads and stores at the top priority
-        case 92: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 6>(args, stream);  // loads high, the sort medium, the passes low
         // round 6: the per-schema slot plan (PLAN), numerics by selects (NUM2), the class table (ORDER 5)
         case 93: return launch_wstage_t<2, 8832, 63, 0, 5, 5, 0, false, true, true, true, false, 1, true, false, true, 1, true, true>(args, stream);  // all three
         case 94: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 1, true, false>(args, stream);  // the plan alone

@@ -164,7 +164,11 @@ template <int NCH, uint32_t WB, uint32_t KCAP, bool REGIONS = false, bool GAP = 
           int WPB = 4, bool XS = false, int PRIO = 0, bool NUM2 = false>
 __global__ void __launch_bounds__(64 * WPB)
 hash_sweep_wstage_kernel(const EncodedArgs a) {
-    if constexpr (PRIO == 1 || PRIO == 3 || PRIO == 4 || PRIO == 5) __builtin_amdgcn_s_setprio(3);
+    // PRIO 4 (the product since round 5): loads high, the walk and the sort
+    // medium, the passes low; the schedules that lost are gone
+    // (profiles/r5/ab_priority.jsonl)
+    static_assert(PRIO == 0 || PRIO == 4, "PRIO: 0 none, 4 the product's schedule");
+    if constexpr (PRIO == 4) __builtin_amdgcn_s_setprio(3);
     constexpr uint32_t SL = NCH * 64;
     __shared__ __attribute__((aligned(16))) uint8_t win_all[WPB][kFrontS + WB + kBackS];
     __shared__ uint64_t desc_all[WPB][SL];   // {offset, length | kGlobal}; then the parked coordinate
@@ -290,9 +294,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         if (vheld && SHAPE != 3) copy_span<ASM, DL>(a.vals + v0 - vlead, win + kFrontS + kreg, vheld, lane);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the compiler does not order ds_read after LDS DMA
-    if constexpr (PRIO == 1 || PRIO == 3) __builtin_amdgcn_s_setprio(0);
-    if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(3);
-    if constexpr (PRIO == 4) __builtin_amdgcn_s_setprio(2);  // 4: the walk and sort at medium priority, the passes low
+    if constexpr (PRIO == 4) __builtin_amdgcn_s_setprio(2);  // the walk and sort at medium priority
     wave_fence();
 
     // ---- decode_value (datalayer_encodings.cc:168-217), lane = object --------
@@ -390,7 +392,7 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         }
     }
     class_sort<NCH, GAP>(cnt, perm, cls, cd, ns, wave_fence);
-    if constexpr (PRIO == 4 || PRIO == 5) __builtin_amdgcn_s_setprio(0);  // 5: the walk and sort stay high
+    if constexpr (PRIO == 4) __builtin_amdgcn_s_setprio(0);  // the passes low
 
     // ---- NCH class-sorted passes, coordinates parked over their descriptors ---
     // (PU 0: the loop not unrolled, one copy of the hash code instead of NCH)
@@ -421,7 +423,6 @@ hash_sweep_wstage_kernel(const EncodedArgs a) {
         desc[s] = h;
     }
     wave_fence();
-    if constexpr (PRIO == 3) __builtin_amdgcn_s_setprio(2);  // the stores (and the wave's end) ahead of the hashing waves
     if (!REGIONS || a.coords) {
 #pragma unroll
         for (int c = 0; c < NCH; ++c) {
@@ -553,24 +554,9 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 30: return a.keys == a.vals  // 3 passes, 11 objects per wave in 14 KiB windows
                         ? launch_wsweep_t<3, 14336, 11, false, true, 0, 13, false, true, true, true, true, false, 1, true>(a, stream)
                         : launch_wsweep_t<3, 14336, 11, false, true, 0, 13, false, true, true, false, true, false, 1, true>(a, stream);
-        case 34: return a.keys == a.vals  // loads high, the walk and passes low (PRIO 1, the product before PRIO 4)
-                        ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 1>(a, stream)
-                        : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 1>(a, stream);
-        case 35: return a.keys == a.vals  // loads, the walk and sort high, the passes low (PRIO 5)
-                        ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 5>(a, stream)
-                        : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 5>(a, stream);
-        case 33: return a.keys == a.vals  // the product with its stores at high priority too (PRIO 3)
-                        ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 3>(a, stream)
-                        : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 3>(a, stream);
-        case 31: case 32: {  // 31: the product without wave priorities (round 5 before), 32: passes high, loads low
-            if (form == 31)
-                return a.keys == a.vals
-                           ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 0>(a, stream)
-                           : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 0>(a, stream);
-            return a.keys == a.vals
-                       ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 2>(a, stream)
-                       : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 2>(a, stream);
-        }
+        case 31: return a.keys == a.vals  // the product without wave priorities (round 5 before)
+                        ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 0>(a, stream)
+                        : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 0>(a, stream);
         case 36: return a.keys == a.vals  // round 6: the product with NUM2 (numerics by selects, the class table)
                         ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 4, true>(a, stream)
                         : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 4, true>(a, stream);

@@ -1,0 +1,177 @@
+"""Host-resident batches in any order: a chunk whose objects
+do not lie back to back is packed in index order — on the device from pinned
+memory (hdx_gather.hip), by a host copy per object from pageable memory —
+so only the objects' own bytes cross PCIe.  Coordinates against the oracle
+and the device-resident path on the same shuffled layout."""
+import numpy as np
+import pytest
+
+import hyperdex_amd as hdx
+from hyperdex_amd import datatypes as dt
+from hyperdex_amd import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _shuffle(blob, base, lens, A, rng, max_gap=37, lead=5):
+    """Every object rewritten at a shuffled position with random gaps."""
+    n = len(base)
+    sizes = lens.reshape(n, A).astype(np.uint64).sum(axis=1)
+    gaps = rng.integers(0, max_gap + 1, n).astype(np.uint64)
+    order = rng.permutation(n)
+    new_base = np.zeros(n, np.uint64)
+    starts = np.cumsum(np.concatenate([[lead], (gaps[order] + sizes[order])[:-1]])).astype(np.uint64)
+    starts += gaps[order]
+    new_base[order] = starts
+    out = np.zeros(int(starts[-1] + sizes[order[-1]]) + 64, np.uint8)
+    for k in range(n):  # vectorised enough for a test: one slice per object
+        b, s, d = int(base[k]), int(sizes[k]), int(new_base[k])
+        out[d:d + s] = blob[b:b + s]
+    return out, new_base
+
+
+def _pinned(torch, a):
+    t = torch.empty(a.nbytes, dtype=torch.uint8, pin_memory=True)
+    view = t.numpy()
+    view[:] = a.view(np.uint8)
+    return t, view
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_shuffled_multichunk_batch(oracle, pinned):
+    """~250 MB of config-3b objects in shuffled order (two and a half 128 MiB
+    chunks, every one packed): equal to the device path and the oracle."""
+    import torch
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 230_000, seed=31)
+    A = len(types)
+    rng = np.random.default_rng(5)
+    sblob, sbase = _shuffle(blob, base, lens, A, rng)
+    keep = None
+    if pinned:
+        keep, sblob = _pinned(torch, sblob)
+    got = hdx.hash_batch_host(types, sblob, sbase, lens)
+    idx = np.sort(rng.choice(len(base), 3000, replace=False))
+    want, _ = oracle.hash_batch(types, blob, base[idx], lens.reshape(len(base), A)[idx].ravel())
+    assert np.array_equal(got[idx], want)
+    dev = torch.device("cuda", 0)
+    b = torch.from_numpy(np.ascontiguousarray(sblob).copy()).to(dev)
+    o = torch.from_numpy(sbase.view(np.int64).copy()).to(dev)
+    L = torch.from_numpy(lens.view(np.int32).copy()).to(dev)
+    ref = hdx.hash_batch(types, b, o, L).cpu().numpy().view(np.uint64)
+    assert np.array_equal(got, ref)
+    del keep
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_shuffled_tiny_objects_every_alignment(oracle, pinned):
+    """Objects of 0..40 bytes at every source alignment, shuffled with wide
+    gaps: the gather's byte-wise edge chunks (extents shorter than a chunk,
+    sharing destination chunks with their neighbours)."""
+    import torch
+    rng = np.random.default_rng(17)
+    n = 8000
+    types = [dt.HYPERDATATYPE_STRING, dt.HYPERDATATYPE_STRING]
+    lens = rng.integers(0, 21, 2 * n).astype(np.uint32)
+    lens[::97] = 0
+    sizes = lens.reshape(n, 2).sum(axis=1).astype(np.uint64)
+    base = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    blob = rng.integers(0, 256, int(sizes.sum()) + 64, dtype=np.uint8)
+    sblob, sbase = _shuffle(blob, base, lens, 2, rng, max_gap=200, lead=3)
+    keep = None
+    if pinned:
+        keep, sblob = _pinned(torch, sblob)
+    got = hdx.hash_batch_host(types, sblob, sbase, lens)
+    want, _ = oracle.hash_batch(types, blob, base, lens)
+    assert np.array_equal(got, want)
+    del keep
+
+
+def test_ordered_batch_still_one_span(oracle):
+    """Objects back to back (the common case) keep the single span copy; with
+    a few gaps (< 1/8 of the payload) too — results identical either way."""
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 20_000, seed=2)
+    want, _ = oracle.hash_batch(types, blob, base, lens)
+    assert np.array_equal(hdx.hash_batch_host(types, blob, base, lens), want)
+
+
+def _scatter(buf, off, ln, rng, max_gap):
+    """Each extent [off, +ln) of buf rewritten at a shuffled place with gaps."""
+    n = len(off)
+    order = rng.permutation(n)
+    gaps = rng.integers(0, max_gap + 1, n).astype(np.uint64)
+    new_off = np.zeros(n, np.uint64)
+    pos = np.uint64(3)
+    for k in order:
+        pos += gaps[k]
+        new_off[k] = pos
+        pos += np.uint64(ln[k])
+    out = np.zeros(int(pos) + 16, np.uint8)
+    for k in range(n):
+        out[int(new_off[k]):int(new_off[k]) + int(ln[k])] = buf[int(off[k]):int(off[k]) + int(ln[k])]
+    return out, new_off
+
+
+def _pinned_np(a):
+    import ctypes
+    from hyperdex_amd import _lib
+    lib = hdx.lib()
+    p = ctypes.c_void_p()
+    _lib.check(lib.hdx_alloc_pinned(max(a.nbytes, 1), ctypes.byref(p)))
+    view = np.frombuffer((ctypes.c_uint8 * max(a.nbytes, 1)).from_address(p.value), dtype=a.dtype, count=a.size)
+    view[:] = a
+    return view, lambda: lib.hdx_free_pinned(p)
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+@pytest.mark.parametrize("records", [False, True])
+def test_shuffled_stores(oracle, pinned, records):
+    """Stored objects (the indexer's host arrays) with keys and values at
+    shuffled places and wide gaps: every chunk is packed into records [key]
+    [value] in index order (two gather extents per object from pinned
+    stores); a corrupt value among them fails only itself (HDX_E_BADENC)."""
+    from hyperdex_amd import _lib
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 6000, seed=41)
+    keys, key_off, key_len, vals, val_off, val_len = synth.encode_store_host(types, blob, base, lens,
+                                                                              first_version=7, layout="keycol")
+    rng = np.random.default_rng(9)
+    if records:  # one store: each record's key right before its value, records shuffled
+        rec = np.zeros(int(key_len.astype(np.uint64).sum() + val_len.astype(np.uint64).sum()), np.uint8)
+        roff = np.zeros(len(key_off), np.uint64)
+        at = 0
+        for i in range(len(key_off)):
+            roff[i] = at
+            rec[at:at + int(key_len[i])] = keys[int(key_off[i]):int(key_off[i] + key_len[i])]
+            at += int(key_len[i])
+            rec[at:at + int(val_len[i])] = vals[int(val_off[i]):int(val_off[i] + val_len[i])]
+            at += int(val_len[i])
+        store, noff = _scatter(rec, roff, key_len.astype(np.uint64) + val_len, rng, 3000)
+        enc = [store, noff, key_len, store, noff + key_len.astype(np.uint64), val_len]
+    else:
+        skeys, nkoff = _scatter(keys, key_off, key_len, rng, 200)
+        svals, nvoff = _scatter(vals, val_off, val_len, rng, 3000)
+        enc = [skeys, nkoff, key_len, svals, nvoff, val_len]
+    # a corrupt value: its first length prefix claims more than the value holds
+    victim = 4321
+    vbuf = enc[3]
+    p = int(enc[4][victim]) + 10
+    vbuf[p:p + 4] = np.frombuffer((0x7fffffff).to_bytes(4, "big"), np.uint8)
+    closers = []
+    if pinned:
+        for idx in ((0,) if records else (0, 3)):
+            view, close = _pinned_np(enc[idx])
+            closers.append(close)
+            enc[idx] = view
+        if records:
+            enc[3] = enc[0]  # one store: the same pinned buffer
+    try:
+        want, wver, bad = oracle.hash_encoded(types, *enc)
+        assert bad[victim] and bad.sum() == 1
+        with pytest.raises(hdx.HdxError) as e:
+            hdx.hash_encoded_host(types, *enc, versions=True)
+        assert e.value.status == _lib.HDX_E_BADENC
+        coords, vers, st, _ = hdx.hash_encoded_host_status(types, *enc)
+        assert st == _lib.HDX_E_BADENC
+        assert np.array_equal(coords, want) and np.array_equal(vers, wver)
+    finally:
+        for c in closers:
+            c()
