@@ -79,6 +79,8 @@ def parse_args(argv=None):
                     help="cfg5's stored objects: 'columns' (each key in place in its packed object, values "
                          "back to back: round 3's layout), 'keycol' (a key column and a value column, "
                          "SURVEY §8d) or 'records' ([key][value] back to back, a LevelDB block's adjacency)")
+    ap.add_argument("--store-schema", default="cfg3b",
+                    help="cfg5's schema (synth.CONFIGS name; w200 / w1000 for the wide sweep)")
     ap.add_argument("--config4-objects", type=int, default=100_000_000,
                     help="config 4: objects of the whole sharded batch (0 = skip)")
     ap.add_argument("--cfg5-objects", type=int, default=50_000_000,
@@ -201,7 +203,7 @@ def run_rank(args):
         # config 5: reindex sweep over stored objects (values in the daemon's
         # on-disk encoding, keys apart) of the config-3b shape
         types, keys, key_off, key_len, vals, val_off, val_len = synth.make_encoded_device(
-            "cfg3b", n, first=rank * n, device=dev, layout=args.store_layout)
+            args.store_schema, n, first=rank * n, device=dev, layout=args.store_layout)
         A = len(types)
         key_bytes = int(key_len.to(torch.int64).sum().item())
         payload = key_bytes + int(val_len.to(torch.int64).sum().item())
@@ -276,7 +278,7 @@ def run_rank(args):
         "dtype": "u8",
         "data": "synthetic (splitmix64 seed 0x4859504552444558, generated in HBM)",
         "config": {"workload": {"cfg3a": "config 3a", "cfg3b": "config 3b", "cfg2": "config 2",
-                                "cfg1": "config 1", "cfg5": "config 5 (reindex sweep, stored 3b objects)"
+                                "cfg1": "config 1", "cfg5": "config 5 (reindex sweep, stored %s objects)" % args.store_schema
                                 }.get(cfg, cfg) +
                    ": %dM objects/GPU, key + %d attrs" % (n // 1_000_000, A - 1),
                    "objects_per_gpu": n, "attrs": A, "payload_bytes_per_gpu": payload,
@@ -299,7 +301,9 @@ def run_rank(args):
         result["roofline"]["frac_of_probe"] = round(
             achieved / sp.get("read_write_mix_GBps", sp["read_write_1to8_GBps"]), 4)
     if cfg == "cfg5":
-        result["roofline"]["kernel"] = sweep_kernel_name(args.store_layout)
+        result["roofline"]["kernel"] = (sweep_kernel_name(args.store_layout) if A <= 128
+                                        else "hdx::hash_sweep_wide_kernel(hdx::EncodedArgs)")
+        result["config"]["store_schema"] = args.store_schema
     if world > 1 and not args.no_allgather:
         result["allgather"] = time_allgather(coords, world, dev, backend, max_over_ranks)
         # hash phase then the coordinate exchange, back to back

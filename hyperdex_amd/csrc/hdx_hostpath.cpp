@@ -23,6 +23,15 @@
 namespace hdx {
 
 static constexpr uint64_t kChunkBytes = 128ull << 20;  // payload bytes per in-flight chunk
+// A chunk packed on the device (hdx_gather.hip) grows to this: its two slots'
+// kernels share one hardware queue, so each chunk pays ~0.5 ms of queue
+// turnaround between its gather and the next (profiles/r6/host_order_trace.txt);
+// larger chunks amortise it (device staging only: no pinned copy)
+static constexpr uint64_t kPackChunkBytes = 512ull << 20;
+// A call's first chunk: small, so the first copy starts after a few
+// milliseconds less of host-side validation (later chunks are validated while
+// the previous ones move)
+static constexpr uint64_t kFirstChunkBytes = 16ull << 20;
 
 void free_host_slot(HostSlot& s) {
     if (s.s) (void)hipStreamSynchronize(s.s);
@@ -191,9 +200,14 @@ hdx_status hash_host(const uint8_t* codes, uint32_t A, const uint8_t* blob, uint
         // packed in index order.
         uint64_t lo = obj_base[i], hi = obj_base[i] + next_size, payload = next_size, e = i + 1;
         sizes.assign(1, (uint32_t)next_size);
+        uint64_t limit = i == 0 ? kFirstChunkBytes : kChunkBytes;
         while (e < n) {
             if ((st = extent(e, &next_size)) != HDX_OK) return drain(st);
-            if (payload + next_size > kChunkBytes) break;
+            if (payload + next_size > limit) {
+                // a chunk the device will pack grows further
+                if (limit == kChunkBytes && blob_dev && !span_pays(hi - lo, payload)) limit = kPackChunkBytes;
+                if (payload + next_size > limit) break;
+            }
             lo = std::min(lo, obj_base[e]);
             hi = std::max(hi, obj_base[e] + next_size);
             payload += next_size;
@@ -359,10 +373,15 @@ hdx_status hash_encoded_host(const uint8_t* codes, uint32_t A, const uint8_t* ke
             return records ? d - c : (b - a) + (d - c);
         };
         uint64_t e = i + 1;
+        uint64_t limit = i == 0 ? kFirstChunkBytes : kChunkBytes;
         while (e < n) {
             if ((st = check(e)) != HDX_OK) return drain(st);
             const uint64_t pe = (uint64_t)key_len[e] + val_len[e];
-            if (payload + pe > kChunkBytes) break;
+            if (payload + pe > limit) {
+                if (limit == kChunkBytes && keys_dev && vals_dev && !span_pays(span_bytes(klo, khi, vlo, vhi), payload))
+                    limit = kPackChunkBytes;  // packed on the device: larger chunks
+                if (payload + pe > limit) break;
+            }
             uint64_t nklo = std::min(klo, key_off[e]), nkhi = std::max(khi, key_off[e] + key_len[e]);
             uint64_t nvlo = std::min(vlo, val_off[e]), nvhi = std::max(vhi, val_off[e] + val_len[e]);
             if (records) {

@@ -13,9 +13,9 @@
 //                             global memory with the A4 loads, one coalesced
 //                             coordinate store);
 //   hash_sweep_wide_kernel  — stored objects with A > 128: one wave per
-//                             object; lane 0 walks the value's [u32 BE len]
-//                             chain 63-64 attributes ahead into LDS, then the
-//                             wave hashes them (daemon/datalayer_encodings.cc:
+//                             object; the wave walks the value's [u32 BE len]
+//                             chain from an LDS window of the value, 63-64
+//                             attributes ahead, then hashes them (daemon/datalayer_encodings.cc:
 //                             168-217, as the sweep of hdx_wsweep.hip: the header, the
 //                             count == A - 1, every prefix and attribute inside
 //                             the value, else zero coordinates, version 0 and
@@ -86,8 +86,16 @@ __device__ __forceinline__ uint64_t be64_at(const uint8_t* p) {
     return __builtin_bswap64(pack64(__builtin_amdgcn_alignbyte(d1, d0, r), __builtin_amdgcn_alignbyte(d2, d1, r)));
 }
 
+// The walk reads the value's prefixes from a per-wave LDS window of the
+// value's dwords (round 6; the walk from global memory paid an HBM round trip
+// per attribute — A = 200 / 1000 ran at 0.09 of the HBM roofline,
+// profiles/r6/wide_*.json): the window is refilled from the prefix the walk
+// has reached whenever the next prefix is not inside it, with coalesced dword
+// loads that stay inside the value's dwords.
+constexpr uint32_t kWideWinDwords = 1024;  // 4 KiB per wave
+
 __global__ void __launch_bounds__(64) hash_sweep_wide_kernel(const EncodedArgs a) {
-    __shared__ uint32_t s_off[64], s_len[64];
+    __shared__ uint32_t win[kWideWinDwords + 1];
     const uint32_t lane = threadIdx.x;
     const uint32_t A = a.A;
     bool bad = false, badenc = false;
@@ -102,40 +110,49 @@ __global__ void __launch_bounds__(64) hash_sweep_wide_kernel(const EncodedArgs a
             version = be64_at(v);
             ok = (be32_at(v + 6) & 0xffffu) == A - 1;  // the u16 at bytes 8..9
         }
+        const uint64_t vaddr = (uint64_t)(uintptr_t)v;
+        const uint64_t vd1 = (vaddr + vlen + 3) >> 2;  // one past the value's last dword
+        uint64_t wd = 0, wend = 0;                     // the window's dwords [wd, wend)
+        auto refill = [&](uint32_t at) {               // the window from value byte `at`'s dword
+            wd = (vaddr + at) >> 2;
+            wend = std::min<uint64_t>(wd + kWideWinDwords, vd1);
+            const uint32_t nd = (uint32_t)(wend - wd);
+            const uint32_t* src = (const uint32_t*)(uintptr_t)(wd << 2);
+            __builtin_amdgcn_wave_barrier();  // the previous window's reads are done (one wave)
+            for (uint32_t d = lane; d < nd; d += 64) win[d] = src[d];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        };
         uint32_t pos = 10;  // pos <= vlen throughout
         for (uint32_t j0 = 0; ok && j0 < A; j0 += 64) {
             const uint32_t jend = std::min(A, j0 + 64);
-            // :198-213 — lane 0 walks this step's value attributes
-            if (lane == 0) {
-                for (uint32_t j = std::max(j0, 1u); j < jend; ++j) {
-                    if (vlen - pos < 4) { ok = false; break; }
-                    const uint32_t L = be32_at(v + pos);
-                    pos += 4;
-                    if (L > vlen - pos) { ok = false; break; }
-                    s_off[j - j0] = pos;
-                    s_len[j - j0] = L;
-                    pos += L;
+            // :198-213 — the wave walks this step's value attributes together
+            // (every lane the same LDS reads: broadcasts); lane j - j0 keeps
+            // attribute j's offset and length
+            uint32_t my_off = 0, my_len = 0;
+            for (uint32_t j = std::max(j0, 1u); j < jend; ++j) {
+                if (vlen - pos < 4) { ok = false; break; }
+                const uint64_t pa = vaddr + pos;
+                if (((pa + 3) >> 2) >= wend || (pa >> 2) < wd) refill(pos);
+                const uint32_t r = (uint32_t)(pa & 3), d = (uint32_t)((pa >> 2) - wd);
+                const uint32_t L = __builtin_bswap32(__builtin_amdgcn_alignbyte(win[d + 1], win[d], r));
+                pos += 4;
+                if (L > vlen - pos) { ok = false; break; }
+                if (lane == j - j0) {
+                    my_off = pos;
+                    my_len = L;
                 }
+                pos += L;
             }
-            ok = __shfl(ok ? 1 : 0, 0, 64) != 0;
-            pos = __shfl(pos, 0, 64);
-            __syncthreads();
             if (ok) {
                 const uint32_t j = j0 + lane;
                 if (j < A) {
-                    const uint8_t* p;
-                    uint32_t L;
-                    if (j == 0) {
-                        p = a.keys + a.key_off[i];
-                        L = a.key_len[i];
-                    } else {
-                        p = v + s_off[lane];
-                        L = s_len[lane];
-                    }
+                    const uint8_t* p = j == 0 ? a.keys + a.key_off[i] : v + my_off;
+                    const uint32_t L = j == 0 ? a.key_len[i] : my_len;
                     out[j] = hash_one(a.codes_dev[j], p, L, bad);
                 }
             }
-            __syncthreads();  // s_off / s_len are rewritten by the next step
         }
         if (!ok) {
             for (uint32_t j = lane; j < A; j += 64) out[j] = 0;

@@ -194,6 +194,12 @@ def make_batch_device(name_or_rules, n: int, seed: int = SEED, first: int = 0, d
     rules = CONFIGS[name_or_rules] if isinstance(name_or_rules, str) else list(name_or_rules)
     A = len(rules)
     device = device or torch.device("cuda", torch.cuda.current_device())
+    if A > 64:  # the device generator's rule table holds 64: the host generator, copied
+        types, hb, hbase, hL = make_batch_host(rules, n, seed, first)
+        blob = torch.empty(len(hb) + pad, dtype=torch.uint8, device=device)
+        blob[:len(hb)] = torch.from_numpy(hb).to(device)
+        return (types, blob, torch.from_numpy(hbase.view(np.int64)).to(device),
+                torch.from_numpy(hL.view(np.int32)).to(device))
     cr = c_rules(rules)
     stream = torch.cuda.current_stream(device).cuda_stream
     attr_len = torch.empty(n * A, dtype=torch.int32, device=device)
