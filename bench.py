@@ -302,7 +302,7 @@ def run_rank(args):
             achieved / sp.get("read_write_mix_GBps", sp["read_write_1to8_GBps"]), 4)
     if cfg == "cfg5":
         result["roofline"]["kernel"] = (sweep_kernel_name(args.store_layout) if A <= 128
-                                        else "hdx::hash_sweep_wide_kernel(hdx::EncodedArgs)")
+                                        else "hdx::sweep_wide_walk_kernel + hdx::sweep_wide_hash_kernel (EncodedArgs)")
         result["config"]["store_schema"] = args.store_schema
     if world > 1 and not args.no_allgather:
         result["allgather"] = time_allgather(coords, world, dev, backend, max_over_ranks)

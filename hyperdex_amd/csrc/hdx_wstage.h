@@ -318,6 +318,8 @@ hash_wstage_kernel(const BatchArgs args) {
     for (int t = 0; t < NCH; ++t) {
         const uint32_t e = perm[t * 64 + lane];
         const uint32_t s = e & 0xffu;
+        // (round 6: storing it straight to HBM from the pass instead, 64
+        // scattered 8-byte stores per pass, measured 2.69 vs 2.44 ms)
         desc[s] = hash_slot<SHAPE, HT, W128, NUM2>(args, lw, g.staged, g.mybase, s, e >> 8, desc[s], bad);
     }
     wave_lds_fence();
