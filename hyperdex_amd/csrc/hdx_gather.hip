@@ -89,6 +89,45 @@ __global__ void __launch_bounds__(256) gather_extents_kernel(const GatherArgs g)
     }
 }
 
+// Up to eight contiguous arrays copied by the compute queue (dwords; the
+// sources device views of pinned host memory): the chunk's offsets, sizes and
+// lengths reach the device without an SDMA copy that the gather would wait on
+// (the pipeline's two slots share one hardware queue).
+namespace {
+struct LinearCopies {
+    const uint32_t* src[8];
+    uint32_t* dst[8];
+    uint64_t dwords[8];
+    uint32_t count;
+};
+}  // namespace
+
+__global__ void __launch_bounds__(256) copy_linear_kernel(const LinearCopies c) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint32_t r = 0; r < c.count; ++r)
+        for (uint64_t d = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; d < c.dwords[r]; d += stride)
+            c.dst[r][d] = __builtin_nontemporal_load(c.src[r] + d);
+}
+
+hipError_t launch_copy_linear(const void* const* src, void* const* dst, const uint64_t* bytes, uint32_t count,
+                              hipStream_t stream) {
+    LinearCopies c{};
+    uint64_t most = 0;
+    if (count > 8) return hipErrorInvalidValue;
+    for (uint32_t r = 0; r < count; ++r) {
+        if (bytes[r] & 3) return hipErrorInvalidValue;
+        c.src[c.count] = (const uint32_t*)src[r];
+        c.dst[c.count] = (uint32_t*)dst[r];
+        c.dwords[c.count] = bytes[r] / 4;
+        most = std::max<uint64_t>(most, bytes[r] / 4);
+        ++c.count;
+    }
+    if (most == 0) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>((most + 255) / 256, 512);
+    hipLaunchKernelGGL(copy_linear_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, c);
+    return hipGetLastError();
+}
+
 hipError_t launch_gather_extents(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,
                                  const uint64_t* dst_off, uint8_t* dst, uint64_t n, hipStream_t stream) {
     if (n == 0) return hipSuccess;

@@ -256,13 +256,26 @@ hdx_status hash_host(const uint8_t* codes, uint32_t A, const uint8_t* blob, uint
             std::memcpy(sl.h_len.p, attr_len + i * A, cnt * A * sizeof(uint32_t));
             src_len = sl.h_len.p;
         }
-        DRAIN_TRY(hipMemcpyAsync(sl.d_base.p, sl.h_base.p, cnt * 8, hipMemcpyHostToDevice, sl.s));
-        DRAIN_TRY(hipMemcpyAsync(sl.d_len.p, src_len, cnt * A * 4, hipMemcpyHostToDevice, sl.s));
-        if (gather) {  // the small arrays first: after the gather only the hash and the D2H remain
-            DRAIN_TRY(hipMemcpyAsync(sl.d_src.p, sl.h_src.p, cnt * 8, hipMemcpyHostToDevice, sl.s));
-            DRAIN_TRY(hipMemcpyAsync(sl.d_sz.p, sl.h_sz.p, cnt * 4, hipMemcpyHostToDevice, sl.s));
+        if (gather) {
+            // every input of the chunk moved by the compute queue: the small
+            // arrays by one copy kernel (pinned staging or the caller's pinned
+            // lengths, through their device views), the objects by the gather
+            const void* lsrc[4] = {device_view((const uint8_t*)sl.h_base.p), device_view((const uint8_t*)sl.h_src.p),
+                                   device_view((const uint8_t*)sl.h_sz.p), device_view((const uint8_t*)src_len)};
+            void* ldst[4] = {sl.d_base.p, sl.d_src.p, sl.d_sz.p, sl.d_len.p};
+            const uint64_t lbytes[4] = {cnt * 8, cnt * 8, cnt * 4, cnt * A * 4};
+            if (lsrc[0] && lsrc[1] && lsrc[2] && lsrc[3]) {
+                DRAIN_TRY(launch_copy_linear(lsrc, ldst, lbytes, 4, sl.s));
+            } else {
+                DRAIN_TRY(hipMemcpyAsync(sl.d_base.p, sl.h_base.p, cnt * 8, hipMemcpyHostToDevice, sl.s));
+                DRAIN_TRY(hipMemcpyAsync(sl.d_src.p, sl.h_src.p, cnt * 8, hipMemcpyHostToDevice, sl.s));
+                DRAIN_TRY(hipMemcpyAsync(sl.d_sz.p, sl.h_sz.p, cnt * 4, hipMemcpyHostToDevice, sl.s));
+                DRAIN_TRY(hipMemcpyAsync(sl.d_len.p, src_len, cnt * A * 4, hipMemcpyHostToDevice, sl.s));
+            }
             DRAIN_TRY(launch_gather_extents(blob_dev, sl.d_src.p, sl.d_sz.p, sl.d_base.p, sl.d_blob.p, cnt, sl.s));
         } else {
+            DRAIN_TRY(hipMemcpyAsync(sl.d_base.p, sl.h_base.p, cnt * 8, hipMemcpyHostToDevice, sl.s));
+            DRAIN_TRY(hipMemcpyAsync(sl.d_len.p, src_len, cnt * A * 4, hipMemcpyHostToDevice, sl.s));
             DRAIN_TRY(hipMemcpyAsync(sl.d_blob.p, src_blob, bytes, hipMemcpyHostToDevice, sl.s));
         }
         BatchArgs args;
@@ -457,14 +470,29 @@ hdx_status hash_encoded_host(const uint8_t* codes, uint32_t A, const uint8_t* ke
             std::memcpy(sl.h_vlen.p, val_len + i, cnt * 4);
             src_vlen = sl.h_vlen.p;
         }
-        DRAIN_TRY(hipMemcpyAsync(sl.d_koff.p, sl.h_koff.p, cnt * 8, hipMemcpyHostToDevice, sl.s));
-        DRAIN_TRY(hipMemcpyAsync(sl.d_voff.p, sl.h_voff.p, cnt * 8, hipMemcpyHostToDevice, sl.s));
-        DRAIN_TRY(hipMemcpyAsync(sl.d_klen.p, src_klen, cnt * 4, hipMemcpyHostToDevice, sl.s));
-        DRAIN_TRY(hipMemcpyAsync(sl.d_vlen.p, src_vlen, cnt * 4, hipMemcpyHostToDevice, sl.s));
+        const void* lsrc[7] = {device_view((const uint8_t*)sl.h_koff.p), device_view((const uint8_t*)sl.h_voff.p),
+                               device_view((const uint8_t*)src_klen), device_view((const uint8_t*)src_vlen),
+                               gather ? device_view((const uint8_t*)sl.h_src.p) : nullptr,
+                               gather ? device_view((const uint8_t*)sl.h_sz.p) : nullptr,
+                               gather ? device_view((const uint8_t*)sl.h_src2.p) : nullptr};
+        if (gather && lsrc[0] && lsrc[1] && lsrc[2] && lsrc[3] && lsrc[4] && lsrc[5] && lsrc[6]) {
+            // every input of the chunk moved by the compute queue (one copy
+            // kernel, then the gather): no SDMA copy for the gather to wait on
+            void* ldst[7] = {sl.d_koff.p, sl.d_voff.p, sl.d_klen.p, sl.d_vlen.p, sl.d_src.p, sl.d_sz.p, sl.d_src2.p};
+            const uint64_t lbytes[7] = {cnt * 8, cnt * 8, cnt * 4, cnt * 4, 2 * cnt * 8, 2 * cnt * 4, 2 * cnt * 8};
+            DRAIN_TRY(launch_copy_linear(lsrc, ldst, lbytes, 7, sl.s));
+        } else {
+            DRAIN_TRY(hipMemcpyAsync(sl.d_koff.p, sl.h_koff.p, cnt * 8, hipMemcpyHostToDevice, sl.s));
+            DRAIN_TRY(hipMemcpyAsync(sl.d_voff.p, sl.h_voff.p, cnt * 8, hipMemcpyHostToDevice, sl.s));
+            DRAIN_TRY(hipMemcpyAsync(sl.d_klen.p, src_klen, cnt * 4, hipMemcpyHostToDevice, sl.s));
+            DRAIN_TRY(hipMemcpyAsync(sl.d_vlen.p, src_vlen, cnt * 4, hipMemcpyHostToDevice, sl.s));
+            if (gather) {
+                DRAIN_TRY(hipMemcpyAsync(sl.d_src.p, sl.h_src.p, 2 * cnt * 8, hipMemcpyHostToDevice, sl.s));
+                DRAIN_TRY(hipMemcpyAsync(sl.d_sz.p, sl.h_sz.p, 2 * cnt * 4, hipMemcpyHostToDevice, sl.s));
+                DRAIN_TRY(hipMemcpyAsync(sl.d_src2.p, sl.h_src2.p, 2 * cnt * 8, hipMemcpyHostToDevice, sl.s));
+            }
+        }
         if (gather) {
-            DRAIN_TRY(hipMemcpyAsync(sl.d_src.p, sl.h_src.p, 2 * cnt * 8, hipMemcpyHostToDevice, sl.s));
-            DRAIN_TRY(hipMemcpyAsync(sl.d_sz.p, sl.h_sz.p, 2 * cnt * 4, hipMemcpyHostToDevice, sl.s));
-            DRAIN_TRY(hipMemcpyAsync(sl.d_src2.p, sl.h_src2.p, 2 * cnt * 8, hipMemcpyHostToDevice, sl.s));
             DRAIN_TRY(launch_gather_extents(nullptr, sl.d_src.p, sl.d_sz.p, sl.d_src2.p, sl.d_blob.p, 2 * cnt, sl.s));
         } else {
             DRAIN_TRY(hipMemcpyAsync(sl.d_blob.p, src_vals, span ? vhi - vlo : payload, hipMemcpyHostToDevice, sl.s));

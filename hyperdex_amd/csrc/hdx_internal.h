@@ -192,6 +192,10 @@ hipError_t launch_hash_encoded(const EncodedArgs& a, hipStream_t stream);
 // destination extents must not overlap).
 hipError_t launch_gather_extents(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,
                                  const uint64_t* dst_off, uint8_t* dst, uint64_t n, hipStream_t stream);
+// hdx_gather.hip: up to 8 contiguous copies of whole dwords (src: device
+// views of pinned host memory, or device memory) by a kernel on `stream`.
+hipError_t launch_copy_linear(const void* const* src, void* const* dst, const uint64_t* bytes, uint32_t count,
+                              hipStream_t stream);
 // The wave-staged sweep (hdx_wsweep.hip): K objects per wave, keys and values
 // copied into LDS by DMA, the walk and the hashing from LDS; coords != NULL,
 // A <= 64 * passes (else hipErrorInvalidValue).  The product form, and (debug
