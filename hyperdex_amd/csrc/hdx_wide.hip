@@ -98,6 +98,15 @@ __device__ __forceinline__ uint64_t be64_at(const uint8_t* p) {
 // overwrites them with the coordinates.
 constexpr uint64_t kWideZero = ~0ull;  // a coordinate of 0 (the object does not decode)
 
+// The walk reads each prefix with ONE unaligned dword load (gfx950 serves
+// them): the chains of all objects advance together and HBM lines are the
+// bound (a dword-pair read per step measured 1.42 ms for A = 200 at 200 k
+// objects); an in-chain prefetch cannot help — loads complete in order, so
+// the next step's wait would also wait out the prefetch — and eight chains
+// per wave walking per-object 2 KiB LDS windows lose to the refills' latency
+// (3.87 vs 2.52 ms, profiles/r6/ab_wide_walk.jsonl).
+typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
+
 __global__ void __launch_bounds__(256) sweep_wide_walk_kernel(const EncodedArgs a) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool badenc = false;
@@ -120,7 +129,7 @@ __global__ void __launch_bounds__(256) sweep_wide_walk_kernel(const EncodedArgs 
                 ok = false;
                 break;
             }
-            const uint32_t L = be32_at(v + pos);
+            const uint32_t L = __builtin_bswap32(*(const __attribute__((address_space(1))) u32_unaligned*)(v + pos));
             pos += 4;
             if (L > vlen - pos) {
                 ok = false;
