@@ -340,6 +340,10 @@ def run_rank(args):
         # BASELINE's third config with its mixed attribute types, measured the
         # same way in the same run (the headline line stays config 3a's)
         guarded(secondary, "cfg3b", lambda: time_config("cfg3b", n, dev, stream))
+        # BASELINE config 2 (10 M objects) and the GPU side of config 1 (its
+        # reference run is CPU-only; 10 M keys here, as in the PMC evidence)
+        guarded(secondary, "cfg2", lambda: time_config("cfg2", n, dev, stream))
+        guarded(secondary, "cfg1", lambda: time_config("cfg1", n, dev, stream))
         result["secondary"] = secondary
 
     if args.config4_objects and cfg != "cfg5":
@@ -900,6 +904,9 @@ def time_config(cfg, n, dev, stream, steps=10, warmup=2, warmup_ms=150.0):
            "GiB_s": round(payload / (ms / 1e3) / 2**30, 3), "mobjects_per_s": round(n / (ms / 1e3) / 1e6, 2),
            "kernel_ms": round(ms, 4), "roofline_frac": round(algo / (ms / 1e3) / 1e9 / HBM_PEAK_GBPS, 4),
            "kernel": hdx.hashing.kernel_for(types, n)[1]}
+    traffic, traffic_src = measured_traffic(latest_traffic_file(), cfg, n)
+    res["traffic"] = traffic
+    res["traffic_source"] = traffic_src
     valu = measured_valu(latest_traffic_file(), cfg, n, ms)
     if valu is not None:
         res["valu"] = valu
