@@ -175,3 +175,36 @@ def test_shuffled_stores(oracle, pinned, records):
     finally:
         for c in closers:
             c()
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_shuffled_batch_region_ids(oracle, pinned):
+    """The regions form of the host batch (hdx_hash_batch_regions_host, the
+    ingest path's call) on packed chunks: a key subspace of 64 regions and a
+    3-attribute subspace of 4 x 4 x 4, ids equal to the oracle's lookup of the
+    oracle's coordinates, with and without coordinates returned."""
+    import torch
+    from hyperdex_amd import regions
+    types, blob, base, lens = synth.make_batch_host("cfg3b", 40_000, seed=23)
+    A = len(types)
+    rng = np.random.default_rng(12)
+    sblob, sbase = _shuffle(blob, base, lens, A, rng, max_gap=1500)
+    keep = None
+    if pinned:
+        keep, sblob = _pinned(torch, sblob)
+    want_c, _ = oracle.hash_batch(types, blob, base, lens)
+    lo1, up1 = oracle.partition(1, 64)
+    lo3, up3 = oracle.partition(3, 64)
+    t1 = regions.RegionTable([0], lo1, up1, np.arange(1, len(lo1) + 1, dtype=np.uint64))
+    t3 = regions.RegionTable([1, 2, 3], lo3, up3, np.arange(100, 100 + len(lo3), dtype=np.uint64))
+    try:
+        ids, coords = hdx.hash_batch_regions_host(types, sblob, sbase, lens, [t1, t3], coords=True)
+        assert np.array_equal(coords, want_c)
+        assert np.array_equal(ids[0], oracle.lookup_region([0], lo1, up1, t1.ids, want_c))
+        assert np.array_equal(ids[1], oracle.lookup_region([1, 2, 3], lo3, up3, t3.ids, want_c))
+        ids2 = hdx.hash_batch_regions_host(types, sblob, sbase, lens, [t1, t3])
+        assert np.array_equal(ids2, ids)
+    finally:
+        t1.close()
+        t3.close()
+        del keep
