@@ -30,9 +30,16 @@
 
 #include "hdx_device_hash.h"
 #include "hdx_internal.h"
+#include "hdx_lds_hash.h"
 #include "hdx_loads.h"
 
+#ifndef HDX_DEBUG_BUILD
+#define HDX_DEBUG_BUILD 0
+#endif
+
 namespace hdx {
+
+typedef __attribute__((address_space(3))) void* lds_void_t;
 
 // One attribute from global memory, any class (hash_blk on the A4 pieces).
 __device__ __forceinline__ uint64_t hash_one(uint32_t code, const uint8_t* p, uint32_t n, bool& bad) {
@@ -107,6 +114,12 @@ constexpr uint64_t kWideZero = ~0ull;  // a coordinate of 0 (the object does not
 // (3.87 vs 2.52 ms, profiles/r6/ab_wide_walk.jsonl).
 typedef uint32_t __attribute__((aligned(1))) u32_unaligned;
 
+// G: descriptors buffered in registers and stored G at a time (G = 1: one
+// store per step).  Stored one per step, a lane's 8-byte descriptors reach
+// its row's lines ~16 steps apart, each as a partial write: WRITE_SIZE 1.29 GB
+// for 0.32 GB of descriptors at A = 200 (profiles/r6/pmc_wide_walk.txt); G
+// back-to-back stores fill 8 G contiguous bytes while the line is in L2.
+template <uint32_t G>
 __global__ void __launch_bounds__(256) sweep_wide_walk_kernel(const EncodedArgs a) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool badenc = false;
@@ -124,19 +137,31 @@ __global__ void __launch_bounds__(256) sweep_wide_walk_kernel(const EncodedArgs 
         }
         uint32_t pos = 10;  // pos <= vlen throughout
         // :198-213, and every attribute inside the value
-        for (uint32_t j = 1; ok && j < A; ++j) {
-            if (vlen - pos < 4) {
-                ok = false;
-                break;
+        for (uint32_t j0 = 1; ok && j0 < A; j0 += G) {
+            uint64_t d[G];
+#pragma unroll
+            for (uint32_t k = 0; k < G; ++k) {
+                d[k] = 0;
+                if (ok && j0 + k < A) {
+                    if (vlen - pos < 4) {
+                        ok = false;
+                    } else {
+                        const uint32_t L =
+                            __builtin_bswap32(*(const __attribute__((address_space(1))) u32_unaligned*)(v + pos));
+                        pos += 4;
+                        if (L > vlen - pos) {
+                            ok = false;
+                        } else {
+                            d[k] = (uint64_t)pos | ((uint64_t)L << 32);
+                            pos += L;
+                        }
+                    }
+                }
             }
-            const uint32_t L = __builtin_bswap32(*(const __attribute__((address_space(1))) u32_unaligned*)(v + pos));
-            pos += 4;
-            if (L > vlen - pos) {
-                ok = false;
-                break;
-            }
-            out[j] = (uint64_t)pos | ((uint64_t)L << 32);
-            pos += L;
+            if (!ok) break;
+#pragma unroll
+            for (uint32_t k = 0; k < G; ++k)
+                if (j0 + k < A) out[j0 + k] = d[k];
         }
         out[0] = ok ? 0 : kWideZero;
         if (!ok) {
@@ -172,15 +197,174 @@ __global__ void __launch_bounds__(256) sweep_wide_hash_kernel(const EncodedArgs 
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
 }
 
-hipError_t launch_hash_sweep_wide(const EncodedArgs& a, hipStream_t stream) {
-    if (a.n == 0) return hipSuccess;
-    if (!a.codes_dev || !a.coords) return hipErrorInvalidValue;
+#if HDX_DEBUG_BUILD
+// A streaming form (round 6, late; debug variants 304-308, not the product):
+// a wave per object streams
+// its value through a two-chunk LDS ring by LDS DMA — chunk c + 1 in flight
+// while the walk reads chunk c — and walks the prefix chain from LDS, the
+// whole wave on the same (broadcast) address, the chain's position in scalar
+// registers.  Every 64 attributes the wave hashes the batch it has walked,
+// a lane per attribute from global memory (the lines the DMA has just brought
+// through L2), and stores 64 coordinates.  Each value byte crosses HBM once
+// and the walk pays LDS latency per attribute instead of an HBM round trip
+// under the load of 200 k chains.  A jump past the prefetched chunk (an
+// attribute longer than a chunk) loads the chunk the next prefix is in.
+// Ring: chunk c (stream bytes [c CH, (c + 1) CH) of the value from its
+// 16-byte floor) in half c & 1; the first dword of an even chunk also in the
+// 16-byte pad after the ring, so a prefix read across the ring's end is one
+// unaligned ds_read_b32.  An undecodable object (the checks of §4.4): the
+// batches already stored are overwritten with zero coordinates, version 0,
+// HDX_E_BADENC.
+// Measured slower than the two launches above (w200: 3.35-3.55 vs 2.50 ms;
+// its walk alone, debug shape 307, 3.39 ms): one chain per wave issues ~30
+// scalar instructions per prefix, and a CU's scalar unit serves all of its
+// waves — the walk is scalar-issue-bound where the lane-per-object walk puts
+// 64 chains in each instruction (profiles/r6/ab_wide_stream.jsonl).
+// SHAPE (debug forms, WRONG coordinates): 1 = no hash (a coordinate is its
+// descriptor), 2 = no walk (made-up descriptors inside the value).
+template <uint32_t CH, int SHAPE = 0>
+__global__ void __launch_bounds__(64) sweep_wide_stream_kernel(const EncodedArgs a) {
+    static_assert(CH >= 1024 && (CH & (CH - 1)) == 0, "CH: a power of two, at least 1 KiB");
+    __shared__ __attribute__((aligned(16))) uint8_t ring[2 * CH + 16];
+    const uint32_t lane = threadIdx.x;
+    const uint64_t i = blockIdx.x;
+    const uint32_t A = a.A;
+    const uint8_t* v = a.vals + a.val_off[i];
+    const uint32_t vlen = a.val_len[i];
+    uint64_t* out = a.coords + i * A;
+    const uint8_t* sb = (const uint8_t*)((uintptr_t)v & ~(uintptr_t)15);
+    const uint32_t lead = (uint32_t)((uintptr_t)v & 15);
+    const uint64_t S = (uint64_t)lead + vlen;  // stream bytes
+    const uint64_t nch = (S + CH - 1) / CH;
+
+    // chunk c into half c & 1: whole 16-byte units, the last partial unit as
+    // dwords (never past the dword holding the value's last byte)
+    uint64_t hold[2] = {~0ull, ~0ull};
+    auto load = [&](uint64_t c) {
+        uint8_t* dst = ring + (c & 1) * CH;
+        const uint64_t u0 = c * (CH / 16), U = S >> 4;
+        if (u0 < U) dma_units16<false>(sb + 16 * u0, dst, (uint32_t)std::min<uint64_t>(CH / 16, U - u0));
+        const uint64_t tb = U * 16;
+        const uint32_t td = ((uint32_t)(S & 15) + 3) >> 2;
+        if (td && tb >= c * CH && tb < (c + 1) * CH && lane < td)
+            __builtin_amdgcn_global_load_lds(sb + tb + 4 * lane, (lds_void_t)(dst + (tb - c * CH)), 4, 0, 0);
+        if (!(c & 1) && lane == 0)  // the ring's wrap: an even chunk's first dword again after the ring
+            __builtin_amdgcn_global_load_lds(sb + c * CH, (lds_void_t)(ring + 2 * CH), 4, 0, 0);
+        hold[c & 1] = c;
+    };
+    // Stream bytes below `ready` have landed in the ring (and nothing the walk
+    // still reads has been overwritten): the walk's steps check only that.  At
+    // the edge: the chunks [t, t + 4) lies in are loaded if not held, waited
+    // for, and the next chunk prefetched into the other half when it is dead.
+    uint64_t ready = 0;
+    auto advance = [&](uint64_t t) {
+        const uint64_t c0 = t / CH, c1 = (t + 3) / CH;
+        if (hold[c0 & 1] != c0 || hold[c1 & 1] != c1) {  // a jump: no DMA still in flight into a half reloaded
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (hold[c0 & 1] != c0) load(c0);
+            if (hold[c1 & 1] != c1) load(c1);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS DMA is not ordered before ds_read
+        ready = std::min<uint64_t>(S, (c1 + 1) * CH);
+        if (c1 == c0 && c0 + 1 < nch) load(c0 + 1);  // the other half is dead
+    };
+    auto ring_be32 = [&](uint64_t t) {
+        const uint32_t r = (uint32_t)(t & (2 * CH - 1));
+        return __builtin_amdgcn_readfirstlane(
+            __builtin_bswap32(*(const __attribute__((address_space(3))) u32_unaligned*)(
+                (const __attribute__((address_space(3))) uint8_t*)(lds_void_t)ring + r)));
+    };
+    if (nch) load(0);
+
+    // :174-192 version and count
+    bool ok = vlen >= 10;
+    uint64_t version = 0;
+    if (ok) {
+        advance(lead);  // the header lies in chunk 0
+        version = ((uint64_t)ring_be32(lead) << 32) | ring_be32(lead + 4);
+        ok = (ring_be32(lead + 6) & 0xffffu) == A - 1;
+    }
+    uint32_t pos = 10;  // pos <= vlen throughout
+    bool bad = false;
+    for (uint32_t j0 = 0; j0 < A; j0 += 64) {
+        const uint32_t jend = std::min(j0 + 64, A);
+        uint32_t dpos = 0, dlen = 0;
+        // :198-213, and every attribute inside the value
+        for (uint32_t j = std::max(j0, 1u); ok && j < jend; ++j) {
+            const uint64_t t = (uint64_t)lead + pos;
+            if (vlen - pos < 4) {
+                ok = false;
+                break;
+            }
+            if (SHAPE != 2 && t + 4 > ready) advance(t);
+            const uint32_t L = SHAPE == 2 ? std::min<uint32_t>(64, vlen - pos - 4) : ring_be32(t);
+            pos += 4;
+            if (L > vlen - pos) {
+                ok = false;
+                break;
+            }
+            if (lane == j - j0) {
+                dpos = pos;
+                dlen = L;
+            }
+            pos += L;
+        }
+        if (!ok) break;
+        const uint32_t j = j0 + lane;
+        const bool in = j < jend;
+        const uint8_t* p = j == 0 ? a.keys + a.key_off[i] : v + dpos;
+        const uint32_t L = j == 0 ? a.key_len[i] : dlen;
+        const uint32_t code = in ? (uint32_t)a.codes_dev[j] : (uint32_t)CODE_ZERO;
+        const uint64_t h = SHAPE == 1 ? (uint64_t)(uintptr_t)p ^ L : hash_one(code, p, L, bad);
+        if (in) out[j] = h;
+    }
+    if (!ok) {
+        for (uint32_t j = lane; j < A; j += 64) out[j] = 0;
+        version = 0;
+    }
+    if (a.versions && lane == 0) a.versions[i] = version;
+    if (a.status && lane == 0 && !ok) atomicOr(a.status, 1u << 6 /* HDX_E_BADENC */);
+    if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS DMA outlives the wave
+}
+
+template <uint32_t CH, int SHAPE = 0>
+static hipError_t launch_sweep_wide_stream(const EncodedArgs& a, hipStream_t stream) {
+    if (a.n > 0x7fffffffULL) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((sweep_wide_stream_kernel<CH, SHAPE>), dim3((uint32_t)a.n), dim3(64), 0, stream, a);
+    return hipGetLastError();
+}
+
+#endif  // HDX_DEBUG_BUILD
+
+// The product: the walk, a lane per object from global memory, then the
+// hash, a wave per object.
+template <uint32_t G>
+static hipError_t launch_sweep_wide_two(const EncodedArgs& a, hipStream_t stream) {
     const uint64_t walk_blocks = (a.n + 255) / 256;
     if (walk_blocks > 0x7fffffffULL) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(sweep_wide_walk_kernel, dim3((uint32_t)walk_blocks), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(sweep_wide_walk_kernel<G>, dim3((uint32_t)walk_blocks), dim3(256), 0, stream, a);
     const uint64_t blocks = std::min<uint64_t>((a.n + 3) / 4, 1ull << 20);  // 4 objects per block, grid-stride
     hipLaunchKernelGGL(sweep_wide_hash_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
+}
+
+hipError_t launch_hash_sweep_wide(const EncodedArgs& a, hipStream_t stream) {
+    if (a.n == 0) return hipSuccess;
+    if (!a.codes_dev || !a.coords) return hipErrorInvalidValue;
+#if HDX_DEBUG_BUILD
+    switch (hash_variant()) {
+        case 304: return launch_sweep_wide_stream<4096>(a, stream);
+        case 305: return launch_sweep_wide_stream<2048>(a, stream);
+        case 306: return launch_sweep_wide_stream<8192>(a, stream);
+        case 307: return launch_sweep_wide_stream<4096, 1>(a, stream);  // debug shape: no hash
+        case 308: return launch_sweep_wide_stream<4096, 2>(a, stream);  // debug shape: no walk
+        case 309: return launch_sweep_wide_two<1>(a, stream);  // the walk's stores one per step
+        case 310: return launch_sweep_wide_two<8>(a, stream);  // ... 8 at a time
+        default: break;
+    }
+#endif
+    return launch_sweep_wide_two<16>(a, stream);
 }
 
 }  // namespace hdx

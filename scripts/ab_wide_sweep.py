@@ -1,7 +1,10 @@
-"""Interleaved A/B of the wide sweep's walk forms (debug library; run on the
-GPU box): variant -1 (the product: a lane per object from global memory) vs
-302 (per-object LDS windows, 8 objects per wave), on a key-column store of
-the w200 / w1000 schemas.  Prints one JSON line per form."""
+"""Interleaved A/B of the wide sweep's forms (debug library; run on the GPU
+box): variant -1 (the product: two launches — a lane per object walking the
+prefix chain from global memory, then the hash) vs 304 / 305 / 306 (a wave
+per object streaming its value through an LDS ring in 4 / 2 / 8 KiB chunks)
+and 307 / 308 (304's debug shapes: no hash / no walk), on a key-column store
+of the w200 / w1000 schemas.  Usage: ab_wide_sweep.py [schema] [objects]
+[v1+v2+...].  Prints one JSON line per form."""
 import json
 import os
 import sys
@@ -26,9 +29,11 @@ payload = int(enc[2].to(torch.int64).sum().item()) + int(enc[5].to(torch.int64).
 algo = payload + n * 24 + n * A * 8
 coords = torch.empty((n, A), dtype=torch.int64, device=dev)
 ref = None
-times = {-1: [], 302: []}
+VARIANTS = tuple(int(x) for x in sys.argv[3].split("+")) if len(sys.argv) > 3 else (-1, 304, 305, 306, 307, 308)
+SHAPES = {307, 308}  # debug shapes: WRONG coordinates, not compared
+times = {v: [] for v in VARIANTS}
 for rep in range(reps + 1):
-    for v in (-1, 302):
+    for v in VARIANTS:
         lib.hdxdbg_set_kernel_variant(v)
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         s.record()
@@ -37,6 +42,8 @@ for rep in range(reps + 1):
         torch.cuda.synchronize()
         if rep:
             times[v].append(s.elapsed_time(e))
+        if v in SHAPES:
+            continue
         got = coords.cpu()
         if ref is None:
             ref = got

@@ -225,3 +225,49 @@ def test_gpu_regions_any_width(oracle, A, n):
     assert all(np.array_equal(hids[k], wants[k]) for k in range(len(specs)))
     for t in tables:
         t.close()
+
+
+def _ring_rules(A, seed):
+    """Attributes of 0 bytes up to 9 KiB among short ones: prefixes at every
+    place of the wide sweep's LDS ring (across a chunk's end and the ring's
+    wrap) and jumps past the prefetched chunk (one attribute longer than a
+    chunk, or than the whole ring)."""
+    rng = np.random.default_rng(seed)
+    pool = [synth.Rule(S, U, 0, 40), synth.Rule(S, U, 0, 300), synth.Rule(S, U, 1000, 5000),
+            synth.Rule(S, U, 4000, 9300), synth.Rule(dt.HYPERDATATYPE_INT64, N, 8, 8),
+            synth.Rule(dt.HYPERDATATYPE_FLOAT, N, 8, 8)]
+    p = np.array([0.4, 0.3, 0.05, 0.03, 0.11, 0.11])
+    return [synth.Rule(S, U, 0, 100)] + [pool[int(k)] for k in rng.choice(len(pool), A - 1, p=p)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [-1, 304, 305, 306, 309, 310])
+def test_gpu_sweep_stream_ring(oracle, variant):
+    """The wide sweep on values of 10 bytes to ~100 KB at every 16-byte
+    alignment, with corrupt ones: the product (the lane-per-object walk, its
+    descriptors stored 16 at a time, then the hash) and the debug forms — 304 /
+    305 / 306 a wave per object streaming the value through a two-chunk LDS
+    ring of 4 / 2 / 8 KiB chunks (prefixes across a chunk's end and the ring's
+    wrap, jumps past the prefetched chunk), 309 / 310 the walk storing 1 / 8
+    descriptors at a time."""
+    import contextlib
+
+    import torch
+
+    import hyperdex_amd as hdx
+    from test_encoded import _corrupt, _to_dev
+    dev = torch.device("cuda", 0)
+    with _lib.debug_library(variant) if variant >= 0 else contextlib.nullcontext():
+        for A, n in ((130, 120), (700, 24)):
+            types, blob, base, lens = synth.make_batch_host(_ring_rules(A, A + 5), n, seed=A + 6)
+            enc = synth.encode_values_host(types, blob, base, lens, first_version=17)
+            enc, cases = _corrupt(enc, np.random.default_rng(A)) if n >= 100 else (enc, {})
+            want, wver, bad = oracle.hash_encoded(types, *enc)
+            assert bad.sum() == len(cases)
+            versions = torch.zeros(n, dtype=torch.int64, device=dev)
+            status = torch.zeros(1, dtype=torch.int32, device=dev)
+            got = hdx.hash_encoded(types, *_to_dev(torch, dev, enc), versions=versions, status=status)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy().view(np.uint64), want), (A, n)
+            assert np.array_equal(versions.cpu().numpy().view(np.uint64), wver), (A, n)
+            assert int(status.item()) == (1 << _lib.HDX_E_BADENC if cases else 0)
