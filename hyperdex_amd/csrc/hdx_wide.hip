@@ -32,6 +32,7 @@
 #include "hdx_internal.h"
 #include "hdx_lds_hash.h"
 #include "hdx_loads.h"
+#include "hdx_regroup.h"
 
 #ifndef HDX_DEBUG_BUILD
 #define HDX_DEBUG_BUILD 0
@@ -40,6 +41,15 @@
 namespace hdx {
 
 typedef __attribute__((address_space(3))) void* lds_void_t;
+
+namespace {
+// the wave's LDS accesses ordered (the class sort's phases, a window's reuse)
+__device__ __forceinline__ void wave_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+}  // namespace
 
 // One attribute from global memory, any class (hash_blk on the A4 pieces).
 __device__ __forceinline__ uint64_t hash_one(uint32_t code, const uint8_t* p, uint32_t n, bool& bad) {
@@ -174,24 +184,76 @@ __global__ void __launch_bounds__(256) sweep_wide_walk_kernel(const EncodedArgs 
     if (a.status && __any(badenc) && (threadIdx.x & 63) == 0) atomicOr(a.status, 1u << 6 /* HDX_E_BADENC */);
 }
 
+// 64 attributes per step in schema order.  SORT (debug 311): each window of
+// 256 attributes counting-sorted by CityHash regime (class_sort,
+// hdx_regroup.h) and hashed in 4 passes of 64, the window's descriptors all
+// read (and kept in LDS) before any of its coordinates overwrites them —
+// measured slower (A = 200: 2.27 vs 2.08 ms; A = 1000: 2.53 vs 2.13,
+// profiles/r6/ab_wide_hash_sort.jsonl): the sort and the window's serial
+// load -> sort -> passes chain cost more than the regimes it saves.
+template <bool SORT>
 __global__ void __launch_bounds__(256) sweep_wide_hash_kernel(const EncodedArgs a) {
-    const uint32_t lane = threadIdx.x & 63;
+    constexpr uint32_t W = 256;
+    __shared__ uint64_t desc_all[SORT ? 4 : 1][SORT ? W : 1];
+    __shared__ uint16_t perm_all[SORT ? 4 : 1][SORT ? W : 1];
+    __shared__ uint32_t cnt_all[SORT ? 4 : 1][kClasses];
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     const uint32_t A = a.A;
     bool bad = false;
-    for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); i < a.n; i += nwaves) {
+    for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x >> 6) + w; i < a.n; i += nwaves) {
         const uint8_t* v = a.vals + a.val_off[i];
         uint64_t* out = a.coords + i * A;
-        for (uint32_t j0 = 0; j0 < A; j0 += 64) {
-            const uint32_t j = j0 + lane;
-            const bool in = j < A;
-            const uint64_t d = in ? out[j] : kWideZero;
-            const bool zero = d == kWideZero;
-            const uint8_t* p = j == 0 ? a.keys + a.key_off[i] : v + (uint32_t)d;
-            const uint32_t L = zero ? 0u : j == 0 ? a.key_len[i] : (uint32_t)(d >> 32);
-            const uint32_t code = in && !zero ? (uint32_t)a.codes_dev[j] : (uint32_t)CODE_ZERO;
-            const uint64_t h = hash_one(code, p, L, bad);
-            if (in) out[j] = h;
+        if constexpr (SORT) {
+            uint64_t* desc = desc_all[w];
+            uint16_t* perm = perm_all[w];
+            const uint8_t* kp = a.keys + a.key_off[i];
+            const uint32_t klen = a.key_len[i];
+            for (uint32_t w0 = 0; w0 < A; w0 += W) {
+                const uint32_t ns = std::min(W, A - w0);
+                uint32_t cls[4], cd[4];
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const uint32_t s = (uint32_t)c * 64 + lane, j = w0 + s;
+                    const bool in = s < ns;
+                    const uint64_t d = in ? out[j] : kWideZero;
+                    const bool zero = d == kWideZero;
+                    const uint32_t L = zero ? 0u : j == 0 ? klen : (uint32_t)(d >> 32);
+                    cd[c] = in && !zero ? (uint32_t)a.codes_dev[j] : (uint32_t)CODE_ZERO;
+                    cls[c] = work_class1_bf(cd[c], L, true);
+                    // the slot's byte address (48 bits) and length (16 bits; 0xffff:
+                    // read it again in the pass)
+                    const uint8_t* p = j == 0 ? kp : v + (uint32_t)d;
+                    desc[s] = (uint64_t)(uintptr_t)p | ((uint64_t)std::min(L, 0xffffu) << 48);
+                }
+                class_sort<4, false>(cnt_all[w], perm, cls, cd, ns, wave_fence);
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    if ((uint32_t)t * 64 >= ns) break;
+                    const uint32_t e = perm[t * 64 + lane];
+                    const uint32_t s = e & 0xffu, code = e >> 8, j = w0 + s;
+                    const bool in = s < ns;
+                    const uint64_t d = desc[s];
+                    uint32_t L = (uint32_t)(d >> 48);
+                    const uint8_t* p = (const uint8_t*)(uintptr_t)(d & 0xffffffffffffull);
+                    if (in && L == 0xffffu) L = j == 0 ? klen : (uint32_t)(out[j] >> 32);  // 64 KiB or more
+                    const uint64_t h = hash_one(in ? code : (uint32_t)CODE_ZERO, p, in ? L : 0u, bad);
+                    if (in) out[j] = h;
+                }
+                wave_fence();  // the window's LDS free for the next
+            }
+        } else {
+            for (uint32_t j0 = 0; j0 < A; j0 += 64) {
+                const uint32_t j = j0 + lane;
+                const bool in = j < A;
+                const uint64_t d = in ? out[j] : kWideZero;
+                const bool zero = d == kWideZero;
+                const uint8_t* p = j == 0 ? a.keys + a.key_off[i] : v + (uint32_t)d;
+                const uint32_t L = zero ? 0u : j == 0 ? a.key_len[i] : (uint32_t)(d >> 32);
+                const uint32_t code = in && !zero ? (uint32_t)a.codes_dev[j] : (uint32_t)CODE_ZERO;
+                const uint64_t h = hash_one(code, p, L, bad);
+                if (in) out[j] = h;
+            }
         }
     }
     if (bad && a.status) atomicOr(a.status, 1u << 2 /* HDX_E_BADSIZE */);
@@ -339,13 +401,13 @@ static hipError_t launch_sweep_wide_stream(const EncodedArgs& a, hipStream_t str
 
 // The product: the walk, a lane per object from global memory, then the
 // hash, a wave per object.
-template <uint32_t G>
+template <uint32_t G, bool SORT = false>
 static hipError_t launch_sweep_wide_two(const EncodedArgs& a, hipStream_t stream) {
     const uint64_t walk_blocks = (a.n + 255) / 256;
     if (walk_blocks > 0x7fffffffULL) return hipErrorInvalidValue;
     hipLaunchKernelGGL(sweep_wide_walk_kernel<G>, dim3((uint32_t)walk_blocks), dim3(256), 0, stream, a);
     const uint64_t blocks = std::min<uint64_t>((a.n + 3) / 4, 1ull << 20);  // 4 objects per block, grid-stride
-    hipLaunchKernelGGL(sweep_wide_hash_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(sweep_wide_hash_kernel<SORT>, dim3((uint32_t)blocks), dim3(256), 0, stream, a);
     return hipGetLastError();
 }
 
@@ -361,6 +423,7 @@ hipError_t launch_hash_sweep_wide(const EncodedArgs& a, hipStream_t stream) {
         case 308: return launch_sweep_wide_stream<4096, 2>(a, stream);  // debug shape: no walk
         case 309: return launch_sweep_wide_two<1>(a, stream);  // the walk's stores one per step
         case 310: return launch_sweep_wide_two<8>(a, stream);  // ... 8 at a time
+        case 311: return launch_sweep_wide_two<16, true>(a, stream);  // the hash class-sorted per 256 attributes
         default: break;
     }
 #endif

@@ -241,7 +241,7 @@ def _ring_rules(A, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [-1, 304, 305, 306, 309, 310])
+@pytest.mark.parametrize("variant", [-1, 304, 305, 306, 309, 310, 311])
 def test_gpu_sweep_stream_ring(oracle, variant):
     """The wide sweep on values of 10 bytes to ~100 KB at every 16-byte
     alignment, with corrupt ones: the product (the lane-per-object walk, its
