@@ -259,7 +259,7 @@ def run_rank(args):
     else:  # payload + 4 B length + 8 B coordinate per attribute
         algo_bytes = payload + n * A * ALGO_EXTRA_PER_ATTR
     achieved = algo_bytes / (kernel_ms / 1e3) / 1e9
-    traffic_key = cfg + ({"keycol": "k", "records": "r"}.get(args.store_layout, "") if cfg == "cfg5" else "")
+    traffic_key = pmc_key(cfg, args.store_layout, args.store_schema)
     traffic, traffic_src = measured_traffic(args.traffic, traffic_key, n)
 
     result = {
@@ -1048,6 +1048,16 @@ def source_digest():
         h.update(os.path.relpath(f, ROOT).encode())
         h.update(open(f, "rb").read())
     return h.hexdigest()[:16]
+
+
+def pmc_key(cfg, store_layout="keycol", store_schema="cfg3b"):
+    """The PMC summary's record for a bench line: the config, for config 5 with
+    its store layout (cfg5 / cfg5k / cfg5r); its config-5 records are config-3b
+    objects, so another store schema names a record the summary does not hold."""
+    if cfg != "cfg5":
+        return cfg
+    key = cfg + {"keycol": "k", "records": "r"}.get(store_layout, "")
+    return key if store_schema == "cfg3b" else key + "_" + store_schema
 
 
 def measured_valu(path, cfg, n, kernel_ms):

@@ -38,3 +38,17 @@ def test_default_profile_matches_default_kernel():
     assert '"%s"' % name in stats, name
     line = json.load(open(os.path.join(rnd, "default_bench_under_rocprof.json")))
     assert line["roofline"]["kernel"] == name
+
+
+def test_pmc_record_per_store_schema():
+    """Config 5's PMC records are config-3b objects: a bench line over another
+    store schema (w200, w1000) gets no traffic of theirs."""
+    import bench
+    assert bench.pmc_key("cfg3b") == "cfg3b"
+    assert bench.pmc_key("cfg5", "keycol") == "cfg5k"
+    assert bench.pmc_key("cfg5", "records") == "cfg5r"
+    assert bench.pmc_key("cfg5", "columns") == "cfg5"
+    key = bench.pmc_key("cfg5", "keycol", "w200")
+    assert key == "cfg5k_w200"
+    t, why = bench.measured_traffic(bench.latest_traffic_file(), key, 200_000)
+    assert t is None and "no PMC record" in why
