@@ -78,6 +78,8 @@ hipError_t launch_hash_batch_regions(const BatchArgs& args, hipStream_t stream);
 hipError_t launch_hash_wide(const BatchArgs& args, hipStream_t stream);
 struct EncodedArgs;
 hipError_t launch_hash_sweep_wide(const EncodedArgs& a, hipStream_t stream);
+// Debug library only (hdx_wide_dbg.hip): the wide sweep's retired forms.
+hipError_t launch_sweep_wide_debug(const EncodedArgs& a, hipStream_t stream, int variant);
 // Fills args.uniform_code from args.codes[0..A), and inv_A / a_magic from A.
 void finalize_args(BatchArgs& args);
 // Kernel variants (hdx_kernels.hip, variant_kernel_name): the automatic policy's

@@ -241,7 +241,7 @@ def _ring_rules(A, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [-1, 304, 305, 306, 309, 310, 311])
+@pytest.mark.parametrize("variant", [-1, 304, 305, 306, 309, 310, 311, 312])
 def test_gpu_sweep_stream_ring(oracle, variant):
     """The wide sweep on values of 10 bytes to ~100 KB at every 16-byte
     alignment, with corrupt ones: the product (the lane-per-object walk, its
@@ -249,7 +249,8 @@ def test_gpu_sweep_stream_ring(oracle, variant):
     305 / 306 a wave per object streaming the value through a two-chunk LDS
     ring of 4 / 2 / 8 KiB chunks (prefixes across a chunk's end and the ring's
     wrap, jumps past the prefetched chunk), 309 / 310 the walk storing 1 / 8
-    descriptors at a time."""
+    descriptors at a time, 311 the hash class-sorted, 312 one launch with a
+    lane per object walking and hashing."""
     import contextlib
 
     import torch
