@@ -45,7 +45,7 @@ def sweep_kernel_name(layout):
     """The product sweep's kernel (hdx_wsweep.hip launch_hash_wsweep_product) as
     rocprofv3 names it: the record instantiation when keys and values are one
     store (layout "records"), else the other one."""
-    return ("void hdx::hash_sweep_wstage_kernel<2, 9728u, 7u, false, true, 0, 13, false, true, true, %s, true, "
+    return ("void hdx::hash_sweep_wstage_kernel<2, 9728u, 7u, false, true, 0, 14, false, true, true, %s, true, "
             "false, 1, true, 4, %s>(hdx::EncodedArgs)" % ("true" if layout == "records" else "false",
                                                           "true" if SWEEP_NUM2 else "false"))
 

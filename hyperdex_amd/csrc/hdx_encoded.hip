@@ -484,6 +484,11 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
             if (e != hipErrorInvalidValue) return e;
             break;
         }
+        case 298: {  // the product sweep before LOOP 4 (LOOP 13: two head reads per divergent pass)
+            const hipError_t e = launch_hash_wsweep(a, stream, 37);
+            if (e != hipErrorInvalidValue) return e;
+            break;
+        }
         case 250: case 251: case 252: case 253: case 254: case 255: {  // the product sweep without the record
             // span; 251 also with round 3's dword key gather; 252 its debug shape: no copy, no walk, the hash on
             // made-up descriptors; 253 / 254 the product's non-record / record forms with round 3's per-KiB span

@@ -206,7 +206,7 @@ const char* variant_kernel_name(int v) {
         case 45: return "void hdx::hash_regroup_kernel<2, true, true, true, true, false, true, 2, 4>(hdx::BatchArgs)";
         case 46: return "void hdx::hash_regroup_kernel<8, true, true, true, false, false, true, 1, 1>(hdx::BatchArgs)";
         case 300: return "hdx::hash_wide_kernel(hdx::BatchArgs)";
-        case 212: return "void hdx::hash_wstage_kernel<2, 8832u, 0, 5, 5, 0, false, true, true, true, false, 1, true, false, true, 1, true, true>(hdx::BatchArgs)";
+        case 212: return "void hdx::hash_wstage_kernel<2, 8832u, 0, 6, 5, 0, false, true, true, true, false, 1, true, false, true, 1, true, true>(hdx::BatchArgs)";
         default: return "";
     }
 }

@@ -53,7 +53,7 @@ hipError_t launch_debug_variant(const BatchArgs& args, hipStream_t stream, int v
         // wave-staged (hdx_wstage.hip): 200 2 passes / 10 KiB, 201 3 / 14 KiB, 202 2 / 8 KiB,
         // 203 1 / 5 KiB, 204 4 / 18 KiB, 205 2 / 8832 B, 206 = 205 with <= 6 objects
         case 200: case 201: case 202: case 203: case 204: case 205: case 206: case 207: case 208:
-        case 209: case 210: case 211: case 213: case 214: case 215: case 216: case 218: case 219: case 239: case 240: case 241: case 242: case 244: case 245: case 246: case 248: case 249: case 255: case 256: case 257: case 258: case 259: case 270: case 273: case 274: case 275: case 276: case 278: case 279: case 287: case 293: case 294: case 295: case 296: case 297: {
+        case 209: case 210: case 211: case 213: case 214: case 215: case 216: case 218: case 219: case 239: case 240: case 241: case 242: case 244: case 245: case 246: case 248: case 249: case 255: case 256: case 257: case 258: case 259: case 270: case 273: case 274: case 275: case 276: case 278: case 279: case 287: case 293: case 294: case 295: case 296: case 297: case 298: {
             const hipError_t e = launch_hash_wstage(args, stream, variant - 200);
             return e == hipErrorInvalidValue ? launch_hash_batch_variant(args, stream, 44) : e;
         }
@@ -134,6 +134,7 @@ static bool known_variant(int v) {
         case 258:  // 212 with <= 6 objects and 7.5 KiB windows / the sweep with 7.75 KiB windows (one wave per workgroup)
         case 293: case 294: case 295: case 296:  // 287 with the slot plan + select numerics + class table / each alone; 293: the sweep with NUM2
         case 297:  // debug shape of 293: no hash (WRONG coordinates)
+        case 298:  // the wave-staged kernel / the sweep as before LOOP 4 (two head reads, separate mix16s)
         case 259:  // 212 / the sweep as in round 4: four waves per workgroup
         case 270:  // 212 / the product sweep with the XCD-aware block order
         case 271:  // the sweep with 7 objects per wave (9.5 KiB windows)

@@ -366,7 +366,39 @@ __device__ __forceinline__ uint64_t city_le16_ht(uint64_t h0, uint64_t t3, uint3
 template <int W128 = 0, int LOOP = 1>
 __device__ __forceinline__ uint64_t hash_string_window(ldsw_t w, uint32_t off, uint32_t n, const Q32& t) {
     const u64x2 t01 = {t.q0, t.q1}, t23 = {t.q2, t.q3};
-    if constexpr (LOOP >= 3) {
+    if constexpr (LOOP >= 4) {
+        // LOOP 3's shared final mix16 (also for 4..7-byte strings) with one head
+        // read for both sides of the regime branch: s[n-64, n-32) over 64 bytes,
+        // else s[0, 32)
+        const Q32 h = lds_read32<W128>(w, n > 64 ? off + n - 64 : off);
+        uint64_t u, v, mul;
+        if (n > 64) {
+            Blk b;
+            b.v0 = u64x2{h.q0, h.q1};
+            b.v1 = u64x2{h.q2, h.q3};
+            b.v2 = t01;
+            b.v3 = t23;
+            city_gt64_lds_uv<W128, 2>(w, off, n, b, u, v);
+            mul = KMUL;
+        } else {
+            if (n > 32) return city_33to64(u64x2{h.q0, h.q1}, u64x2{h.q2, h.q3}, t01, t23, n);
+            if (n < 4) return city_le16_ht(h.q0, t.q3, n);
+            mul = K2 + 2ull * n;
+            if (n > 16) {  // city.cc:305-313 (city_17to32)
+                const uint64_t a = h.q0 * K1, b = h.q1, c = t.q3 * mul, d = t.q2 * K2;
+                u = ror(a + b, 43) + ror(c, 30) + d;
+                v = a + ror(b + K2, 18) + c;
+            } else if (n >= 8) {  // city.cc:281-286 (city_le16_ht, n >= 8)
+                const uint64_t a = h.q0 + K2;
+                u = ror(t.q3, 37) * mul + a;
+                v = (ror(a, 25) + t.q3) * mul;
+            } else {  // city.cc:287-291 (4 <= n < 8): Fetch32(s) and Fetch32(s + n - 4)
+                u = n + ((h.q0 & 0xffffffffull) << 3);
+                v = t.q3 >> 32;
+            }
+        }
+        return mix16(u, v, mul);
+    } else if constexpr (LOOP >= 3) {
         uint64_t u, v, mul;
         if (n > 64) {
             const Q32 q = lds_read32<W128>(w, off + n - 64);
@@ -413,7 +445,8 @@ __device__ __forceinline__ uint64_t hash_string_window(ldsw_t w, uint32_t off, u
 }
 
 // LOOP: city_gt64_lds's; LOOP 3 = LOOP 2 with one final mix16 shared by the
-// > 64-byte regime and the 8..32-byte ones (a pass holding both runs it once).
+// > 64-byte regime and the 8..32-byte ones (a pass holding both runs it once);
+// LOOP 4 = LOOP 3 with one head read for both sides of the regime branch.
 // TNUM: every slot reads its last 32 bytes before the type dispatch, and an
 // 8-byte numeric takes its value from them (q3) — one read for the numeric
 // and string lanes of a pass instead of two.

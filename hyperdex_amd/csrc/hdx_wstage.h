@@ -204,7 +204,8 @@ __device__ __forceinline__ Group<NCH> describe_group(const BatchArgs& args, uint
 // dword instead of the hash.
 // HT: staged slots hashed by hash_slot_window (first / last 32 bytes, every
 // regime from the same two reads; lw then points kFrontHT bytes before the
-// window); HT 2 / 3: hash_slot_window's LOOP 2 / 3; HT 5: LOOP 2 with TNUM.
+// window); HT 2 / 3: hash_slot_window's LOOP 2 / 3; HT 5: LOOP 2 with TNUM;
+// HT 6: LOOP 4 with TNUM.
 constexpr uint32_t kFrontHT = 32;
 template <int SHAPE, int HT = 0, int W128 = 0, bool NUM2 = false>
 __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, bool staged, uint64_t mybase,
@@ -212,7 +213,7 @@ __device__ __forceinline__ uint64_t hash_slot(const BatchArgs& args, ldsw_t lw, 
     const uint32_t doff = (uint32_t)d, dn = (uint32_t)(d >> 32);
     if (SHAPE == 1) return lw[doff >> 2] ^ dn;
     if (staged && HT)
-        return hash_slot_window<W128, (HT >= 5 ? 2 : HT > 1 ? HT : 1), (HT >= 5), NUM2 && HT >= 5>(lw, cd, doff + kFrontHT,
+        return hash_slot_window<W128, (HT == 6 ? 4 : HT >= 5 ? 2 : HT > 1 ? HT : 1), (HT >= 5), NUM2 && HT >= 5>(lw, cd, doff + kFrontHT,
                                                                                                   dn, bad);
     if (staged) return cd == CODE_STRING ? hash_string_lds(lw, doff, dn) : hash_numeric_lds(lw, cd, doff, dn, bad);
     const uint32_t o = div_small(s, args.a_magic);

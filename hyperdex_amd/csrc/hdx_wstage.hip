@@ -22,7 +22,10 @@
 // per wave, 2.666 vs 2.709 ms (profiles/r6/ab_plan.jsonl,
 // pmc_lds_cfg3b_plan.txt).  Other schemas (timestamps, non-hashable types:
 // forced debug variants only — the policy gives them the regroup kernel) keep
-// the round-5 instantiation.
+// the round-5 instantiation.  Late round 6 (HT 6, hash_slot_window LOOP 4): a
+// pass holding long and short strings reads each slot's head once and runs one
+// final mix16 (also for 4..7-byte strings): 2.447 vs 2.462 and 2.663 vs 2.681
+// ms on two boxes (debug 298 = the form before it, profiles/r6/ab_loop4.jsonl).
 #include "hdx_wstage.h"
 
 namespace hdx {
@@ -30,18 +33,18 @@ namespace hdx {
 hipError_t launch_hash_wstage_product(const BatchArgs& args, hipStream_t stream) {
     if (args.n == 0) return hipSuccess;
     if (num2_schema(args))
-        return launch_wstage_t<2, 8832, 63, 0, 5, 5, 0, false, true, true, true, false, 1, true, false, true, 1, true,
+        return launch_wstage_t<2, 8832, 63, 0, 6, 5, 0, false, true, true, true, false, 1, true, false, true, 1, true,
                                true>(args, stream);
-    return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 1>(args, stream);
+    return launch_wstage_t<2, 8832, 63, 0, 6, 4, 0, false, true, true, true, false, 1, true, false, true, 1>(args, stream);
 }
 
 // ... with the fused region lookup (args.T tables; args.coords may be NULL)
 hipError_t launch_hash_wstage_regions(const BatchArgs& args, hipStream_t stream) {
     if (args.n == 0) return hipSuccess;
     if (num2_schema(args))
-        return launch_wstage_t<2, 8832, 63, 0, 5, 5, 0, true, true, true, true, false, 1, true, false, true, 1, true,
+        return launch_wstage_t<2, 8832, 63, 0, 6, 5, 0, true, true, true, true, false, 1, true, false, true, 1, true,
                                true>(args, stream);
-    return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, true, true, true, true, false, 1, true, false, true, 1>(args, stream);
+    return launch_wstage_t<2, 8832, 63, 0, 6, 4, 0, true, true, true, true, false, 1, true, false, true, 1>(args, stream);
 }
 
 }  // namespace hdx

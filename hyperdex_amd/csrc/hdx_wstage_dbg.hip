@@ -178,6 +178,7 @@ hipError_t launch_hash_wstage(const BatchArgs& args, hipStream_t stream, int for
         case 95: return launch_wstage_t<2, 8832, 63, 0, 5, 4, 0, false, true, true, true, false, 1, true, false, true, 1, false, true>(args, stream);  // NUM2 alone
         case 96: return launch_wstage_t<2, 8832, 63, 0, 5, 5, 0, false, true, true, true, false, 1, true, false, true, 1, false, false>(args, stream);  // the class table alone
         case 97: return launch_wstage_t<2, 8832, 63, 1, 5, 5, 0, false, true, true, true, false, 1, true, false, true, 1, true, true>(args, stream);  // debug shape of 93: no hash (WRONG coordinates)
+        case 98: return launch_wstage_t<2, 8832, 63, 0, 5, 5, 0, false, true, true, true, false, 1, true, false, true, 1, true, true>(args, stream);  // the product before LOOP 4 (= 93)
         // the slots class-sorted over the workgroup
         case 10: return launch_wgstage_t<2, 8832>(args, stream);
         case 11: return launch_wgstage_t<1, 4352>(args, stream);

@@ -486,12 +486,15 @@ static hipError_t launch_wsweep_t(const EncodedArgs& a, hipStream_t stream) {
 // selects, the class from the table): 3.258 vs 3.304 ms per 10 M on the key
 // column, VALU 971.8 -> 956.8 and SALU 401.1 -> 370.1 per wave
 // (profiles/r6/ab_sweep_num2.jsonl, pmc_lds_cfg5k_num2.txt); other schemas keep
-// the round-5 form.
+// the round-5 form.  Late round 6: LOOP 14 (hash_slot_window LOOP 4, one head
+// read per slot in a pass holding long and short strings): 3.247 vs 3.266 and
+// 3.261 vs 3.287 ms per 10 M on the key column (debug 298 = LOOP 13,
+// profiles/r6/ab_loop4.jsonl).
 template <bool REG, bool RECS>
 static hipError_t launch_wsweep_product_t(const EncodedArgs& a, hipStream_t stream) {
     if (num2_codes(a))
-        return launch_wsweep_t<2, 9728, 7, REG, true, 0, 13, false, true, true, RECS, true, false, 1, true, 4, true>(a, stream);
-    return launch_wsweep_t<2, 9728, 7, REG, true, 0, 13, false, true, true, RECS, true, false, 1, true, 4>(a, stream);
+        return launch_wsweep_t<2, 9728, 7, REG, true, 0, 14, false, true, true, RECS, true, false, 1, true, 4, true>(a, stream);
+    return launch_wsweep_t<2, 9728, 7, REG, true, 0, 14, false, true, true, RECS, true, false, 1, true, 4>(a, stream);
 }
 
 hipError_t launch_hash_wsweep_product(const EncodedArgs& a, hipStream_t stream) {
@@ -558,6 +561,9 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
                         ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 0>(a, stream)
                         : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 0>(a, stream);
         case 36: return a.keys == a.vals  // round 6: the product with NUM2 (numerics by selects, the class table)
+                        ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 4, true>(a, stream)
+                        : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 4, true>(a, stream);
+        case 37: return a.keys == a.vals  // the product before LOOP 4 (two head reads per divergent pass; = 36)
                         ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 4, true>(a, stream)
                         : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 4, true>(a, stream);
         case 26: return a.keys == a.vals  // round 4's product: four waves per workgroup

@@ -189,7 +189,7 @@ def test_gpu_encoded_scattered_layout(oracle, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [-1, 33, 43, 47, 48, 49, 301, 170, 171, 172, 173, 174, 230, 231, 232, 236, 239, 242, 243, 244, 245, 246, 250, 251, 253, 254, 255, 256, 257, 258, 259, 270, 271, 272, 273, 277, 293])
+@pytest.mark.parametrize("variant", [-1, 33, 43, 47, 48, 49, 301, 170, 171, 172, 173, 174, 230, 231, 232, 236, 239, 242, 243, 244, 245, 246, 250, 251, 253, 254, 255, 256, 257, 258, 259, 270, 271, 272, 273, 277, 293, 298])
 def test_gpu_encoded_every_variant(oracle, variant):
     """Every stored-object sweep kernel (hdx_encoded.hip; 33 adds the line
     touch) is bit-exact on every config, on corrupt values, on ragged object

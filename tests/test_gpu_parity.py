@@ -337,7 +337,7 @@ VARIANTS = [12, 18, 19, 20, 21, 25, 26, 30, 31, 35, 37, 38, 39, 44, 45, 46,
 
 
 @pytest.mark.parametrize("variant", [200, 201, 202, 203, 204, 205, 206, 210, 211, 212, 214, 215, 216, 219, 239, 240, 242, 244, 245, 246, 255,
-                                     256, 257, 258, 259, 270, 273, 274, 275, 276, 278, 279, 287, 293, 294, 295, 296])
+                                     256, 257, 258, 259, 270, 273, 274, 275, 276, 278, 279, 287, 293, 294, 295, 296, 298])
 def test_wave_staged_layouts(oracle, torch_dev, variant):
     """The wave-staged kernel (hdx_wstage.hip) stages a group's span only when
     its objects are back to back and fit the window: gaps after some objects
