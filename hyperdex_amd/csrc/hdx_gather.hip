@@ -51,13 +51,14 @@ __global__ void __launch_bounds__(256) gather_extents_kernel(const GatherArgs g)
         const uint32_t lead = (uint32_t)((uintptr_t)s & 15), dlead = (uint32_t)((uintptr_t)d & 15);
         const u32x4* sa = (const u32x4*)(s - lead);
         u32x4* da = (u32x4*)(d - dlead);
-        const int nsc = (int)((lead + L + 15) >> 4), ndc = (int)((dlead + L + 15) >> 4);
+        // 64-bit chunk and byte positions: an extent may reach 4 GiB
+        const int64_t nsc = (int64_t)(((uint64_t)lead + L + 15) >> 4), ndc = (int64_t)(((uint64_t)dlead + L + 15) >> 4);
         const int sh = (int)lead - (int)dlead;     // -15 .. 15
         const int bofs = sh < 0 ? -1 : 0;
         const uint32_t r = (uint32_t)(sh - 16 * bofs);  // 0 .. 15: the pair's byte offset
         const uint32_t k = r >> 2, b = r & 3;           // wave-uniform
-        for (int q0 = 0; q0 < ndc; q0 += 64) {
-            const int q = q0 + lane, c = q + bofs;
+        for (int64_t q0 = 0; q0 < ndc; q0 += 64) {
+            const int64_t q = q0 + lane, c = q + bofs;
             const u32x4 zero = {0u, 0u, 0u, 0u};
             const u32x4 x = c >= 0 && c < nsc ? __builtin_nontemporal_load(sa + c) : zero;
             u32x4 y;
@@ -76,14 +77,14 @@ __global__ void __launch_bounds__(256) gather_extents_kernel(const GatherArgs g)
                 default: o = {pick(w, 3, 0, b), pick(w, 3, 1, b), pick(w, 3, 2, b), pick(w, 3, 3, b)}; break;
             }
             // dst chunk q holds object bytes [16q - dlead, 16q - dlead + 16)
-            const int j0 = 16 * q - (int)dlead;
-            if (j0 >= 0 && j0 + 16 <= (int)L) {
+            const int64_t j0 = 16 * q - (int64_t)dlead;
+            if (j0 >= 0 && j0 + 16 <= (int64_t)L) {
                 da[q] = o;
             } else {
                 const uint32_t ob[4] = {o.x, o.y, o.z, o.w};
                 uint8_t* dq = (uint8_t*)(da + q);
                 for (int t = 0; t < 16; ++t)
-                    if (j0 + t >= 0 && j0 + t < (int)L) dq[t] = (uint8_t)(ob[t >> 2] >> (8 * (t & 3)));
+                    if (j0 + t >= 0 && j0 + t < (int64_t)L) dq[t] = (uint8_t)(ob[t >> 2] >> (8 * (t & 3)));
             }
         }
     }

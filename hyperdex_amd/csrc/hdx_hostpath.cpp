@@ -215,7 +215,7 @@ hdx_status hash_host(const uint8_t* codes, uint32_t A, const uint8_t* blob, uint
             ++e;
         }
         const uint64_t cnt = e - i;
-        const bool span = span_pays(hi - lo, payload);
+        const bool span = cnt == 1 || span_pays(hi - lo, payload);  // one object: its own bytes, however large
         const uint64_t bytes = span ? hi - lo : payload;
         HostSlot& sl = slots[k];
         if ((st = finish(k)) != HDX_OK) return drain(st);
@@ -406,7 +406,9 @@ hdx_status hash_encoded_host(const uint8_t* codes, uint32_t A, const uint8_t* ke
             ++e;
         }
         const uint64_t cnt = e - i;
-        const bool span = span_pays(span_bytes(klo, khi, vlo, vhi), payload);
+        // one object whose spans hold nothing else moves as spans, however large
+        const bool span = span_pays(span_bytes(klo, khi, vlo, vhi), payload) ||
+                          (cnt == 1 && span_bytes(klo, khi, vlo, vhi) == payload);
         const bool gather = !span && keys_dev && vals_dev;
         const bool packed = !span;  // the chunk's device layout is then records
         HostSlot& sl = slots[k];

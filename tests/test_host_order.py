@@ -208,3 +208,61 @@ def test_shuffled_batch_region_ids(oracle, pinned):
         t1.close()
         t3.close()
         del keep
+
+
+def _giant_batch(rng, n=40, big=600 << 20, at=17):
+    """n objects of two strings, object `at` holding a `big`-byte second
+    attribute (alone in its host chunk: larger than a packed chunk), the rest
+    small; objects written at shuffled places."""
+    types = [dt.HYPERDATATYPE_STRING, dt.HYPERDATATYPE_STRING]
+    lens = rng.integers(0, 200, 2 * n).astype(np.uint32)
+    lens[2 * at + 1] = big
+    sizes = lens.reshape(n, 2).sum(axis=1).astype(np.uint64)
+    base = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.uint64)
+    block = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    blob = np.tile(block, int(sizes.sum()) // len(block) + 2)[:int(sizes.sum()) + 64].copy()
+    blob[:4096] = rng.integers(0, 256, 4096, dtype=np.uint8)
+    sblob, sbase = _shuffle(blob, base, lens, 2, rng, max_gap=100)
+    return types, blob, base, lens, sblob, sbase
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_giant_object_alone_in_its_chunk(oracle, pinned):
+    """An object larger than a packed chunk (600 MB) among small shuffled ones:
+    its chunk holds it alone and moves as one span (pinned or pageable), the
+    small objects' chunks are packed; every row equal to the oracle's."""
+    import torch
+    rng = np.random.default_rng(77)
+    types, blob, base, lens, sblob, sbase = _giant_batch(rng)
+    keep = None
+    if pinned:
+        keep, sblob = _pinned(torch, sblob)
+    got = hdx.hash_batch_host(types, sblob, sbase, lens)
+    want, _ = oracle.hash_batch(types, blob, base, lens)
+    assert np.array_equal(got, want)
+    del keep
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_giant_value_alone_in_its_chunk(oracle, pinned):
+    """A stored object whose value is 600 MB, keys in a key column apart from
+    the values: its chunk holds it alone and moves as two spans."""
+    rng = np.random.default_rng(78)
+    types, blob, base, lens, _, _ = _giant_batch(rng)
+    keys, key_off, key_len, vals, val_off, val_len = synth.encode_store_host(types, blob, base, lens,
+                                                                              first_version=3, layout="keycol")
+    enc = [keys, key_off, key_len, vals, val_off, val_len]
+    closers = []
+    if pinned:
+        for idx in (0, 3):
+            view, close = _pinned_np(enc[idx])
+            closers.append(close)
+            enc[idx] = view
+    try:
+        want, wver, bad = oracle.hash_encoded(types, *enc)
+        assert not bad.any()
+        coords, vers = hdx.hash_encoded_host(types, *enc, versions=True)
+        assert np.array_equal(coords, want) and np.array_equal(vers, wver)
+    finally:
+        for c in closers:
+            c()
