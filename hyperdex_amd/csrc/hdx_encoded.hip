@@ -484,6 +484,11 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
             if (e != hipErrorInvalidValue) return e;
             break;
         }
+        case 313: case 314: case 315: {  // the product sweep's debug shapes: no hash / no hash, no walk / no copy, no walk
+            const hipError_t e = launch_hash_wsweep(a, stream, hash_variant() - 313 + 38);
+            if (e != hipErrorInvalidValue) return e;
+            break;
+        }
         case 298: {  // the product sweep before LOOP 4 (LOOP 13: two head reads per divergent pass)
             const hipError_t e = launch_hash_wsweep(a, stream, 37);
             if (e != hipErrorInvalidValue) return e;

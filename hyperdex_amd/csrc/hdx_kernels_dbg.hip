@@ -100,6 +100,7 @@ static bool known_variant(int v) {
         case 309: case 310:  // the wide sweep's walk storing its descriptors one / 8 per step group (hdx_wide.hip)
         case 311:  // the wide sweep's hash class-sorted per 256 attributes
         case 312:  // the wide sweep in one launch, a lane per object (walk and hash fused)
+        case 313: case 314: case 315:  // the product sweep's debug shapes: no hash / no hash, no walk / no copy, no walk (WRONG coordinates)
         case 100: case 101: case 102: case 103: case 104: case 105: case 106: case 107: case 108: case 109:
         case 110: case 111:  // fused hash + lookup_region forms (launch_fused_debug)
         case 170: case 171: case 172: case 173: case 174:  // the sweep's numeric walk (hdx_encoded.hip)

@@ -563,6 +563,10 @@ hipError_t launch_hash_wsweep(const EncodedArgs& a, hipStream_t stream, int form
         case 36: return a.keys == a.vals  // round 6: the product with NUM2 (numerics by selects, the class table)
                         ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 4, true>(a, stream)
                         : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 4, true>(a, stream);
+        // the product's debug shapes (WRONG coordinates): 38 no hash, 39 no hash and no walk, 40 no copy and no walk
+        case 38: return launch_wsweep_t<2, 9728, 7, false, true, 1, 14, false, true, true, false, true, false, 1, true, 4, true>(a, stream);
+        case 39: return launch_wsweep_t<2, 9728, 7, false, true, 2, 14, false, true, true, false, true, false, 1, true, 4, true>(a, stream);
+        case 40: return launch_wsweep_t<2, 9728, 7, false, true, 3, 14, false, true, true, false, true, false, 1, true, 4, true>(a, stream);
         case 37: return a.keys == a.vals  // the product before LOOP 4 (two head reads per divergent pass; = 36)
                         ? launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, true, true, false, 1, true, 4, true>(a, stream)
                         : launch_wsweep_t<2, 9728, 7, false, true, 0, 13, false, true, true, false, true, false, 1, true, 4, true>(a, stream);

@@ -35,7 +35,7 @@ def main():
     lib = ctx.__enter__()
     dev = torch.device("cuda", 0)
     variants = [int(v) for v in args.variants.split(",")]
-    checked = set(int(v) for v in args.check.split(",")) if args.check else set(variants) - {40, 41, 57, 58, 207, 208, 218, 241, 297, 223, 224, 225, 226, 227, 237, 238, 248, 249, 252}
+    checked = set(int(v) for v in args.check.split(",")) if args.check else set(variants) - {40, 41, 57, 58, 207, 208, 218, 241, 297, 313, 314, 315, 223, 224, 225, 226, 227, 237, 238, 248, 249, 252}
     for cfg in args.configs.split(","):
         if cfg in ("cfg5", "cfg5r", "cfg5k"):  # stored-object sweep; cfg5r / cfg5k: records / key column
             types, *enc = synth.make_encoded_device("cfg3b", args.objects, device=dev,
