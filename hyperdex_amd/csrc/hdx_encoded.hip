@@ -461,7 +461,7 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
         case 173: return launch_encoded<false, true, 0, 32, false, true, true>(a, stream);
         case 174: return launch_encoded<false, true, 0, 64, false, true, true>(a, stream);
         case 48: return launch_encoded<false, true, 0, 16>(a, stream);
-        // wave-staged (hdx_wsweep.hip): 230 6 objects / 2 passes, 231 7 objects, 232 11 objects / 3 passes,
+        // wave-staged (hdx_wsweep_dbg.hip): 230 6 objects / 2 passes, 231 7 objects, 232 11 objects / 3 passes,
         // 236 = 230 without the pass-boundary gap, 237 / 238 its debug shapes (no hash / no hash, no walk),
         // 239 = 230 with the one-block > 64-byte loop, 242 without the shared final mix16,
         // 243 with the DMA as inline asm, 244 with the pass loop not unrolled, 245 with the
@@ -507,7 +507,7 @@ hipError_t launch_hash_encoded(const EncodedArgs& a_in, hipStream_t stream) {
     // 49: the gather sweep (the product's sweep up to round 2), for A/B runs
     if (hash_variant() == 49) return launch_encoded<false, true, 0, 32>(a, stream);
 #endif
-    // the wave-staged sweep (hdx_wsweep.hip): 4.65 vs 5.10 ms per 10 M
+    // the wave-staged sweep (hdx_wsweep.h): 4.65 vs 5.10 ms per 10 M
     // config-3b objects, 24.2 vs 25.1 ms at 50 M (profiles/r3/ab_wsweep.jsonl)
     if (a.coords) {
         const hipError_t e = launch_hash_wsweep_product(a, stream);

@@ -198,7 +198,7 @@ hipError_t launch_gather_extents(const uint8_t* src, const uint64_t* src_off, co
 // views of pinned host memory, or device memory) by a kernel on `stream`.
 hipError_t launch_copy_linear(const void* const* src, void* const* dst, const uint64_t* bytes, uint32_t count,
                               hipStream_t stream);
-// The wave-staged sweep (hdx_wsweep.hip): K objects per wave, keys and values
+// The wave-staged sweep (hdx_wsweep.h): K objects per wave, keys and values
 // copied into LDS by DMA, the walk and the hashing from LDS; coords != NULL,
 // A <= 64 * passes (else hipErrorInvalidValue).  The product form, and (debug
 // library) its A/B forms.

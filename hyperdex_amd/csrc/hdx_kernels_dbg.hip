@@ -119,7 +119,7 @@ static bool known_variant(int v) {
         case 244:  // 212 / 230 with the pass loop not unrolled
         case 245:  // 212 / 230 with the branchy work class (and, 230, guarded loads)
         case 246:  // 212 / 230 without TNUM (numerics read apart from the strings' tail)
-        case 230: case 231: case 232: case 233: case 234:  // wave-staged sweep (hdx_wsweep.hip; 233: fused regions; 234: the gather sweep's fused regions)
+        case 230: case 231: case 232: case 233: case 234:  // wave-staged sweep (hdx_wsweep_dbg.hip; 233: fused regions; 234: the gather sweep's fused regions)
         case 236:  // 230 without the pass-boundary gap
         case 237: case 238:  // 230's debug shapes: no hash / no hash, no walk (WRONG coordinates)
         case 235:  // regions by hash + separate lookups at any n, 64 MiB chunks (hdx_regions.hip)

@@ -17,7 +17,7 @@
 //                             [u32 BE len] chain, writing each attribute's
 //                             {offset, length} where its coordinate goes; a
 //                             wave per object then hashes 64 attributes a step (daemon/datalayer_encodings.cc:
-//                             168-217, as the sweep of hdx_wsweep.hip: the header, the
+//                             168-217, as the sweep of hdx_wsweep.h: the header, the
 //                             count == A - 1, every prefix and attribute inside
 //                             the value, else zero coordinates, version 0 and
 //                             HDX_E_BADENC).
